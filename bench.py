@@ -1,0 +1,188 @@
+#!/usr/bin/env python3
+"""bench.py -- BASELINE.json metric on MI355X: Msamples/s through Hilbert -> modulator -> render.
+
+Workload (BASELINE.json configs[1], SURVEY 8(d) "C2"): per GPU, 256 concurrent 48 kHz 16-bit
+stereo streams, quadrature Hilbert with the reference's default Type-1 (order-19) elliptic
+half-band IIR in Kahan mode, one Shift node (+2/-2 Hz) + Master (S_ADD_REIM, 0.8), 16-bit
+ROUND / mid-riser / flat render.  One step = one pass over 2^20 frames of every stream (the
+state carries from step to step, as in a continuous decode).  Inputs are resident in HBM before
+the timed region; the C-ABI is called with device pointers (ICW_F_DEVICE_PTRS).
+
+Metric: rendered output channel-samples per second (2 x frames/s), whole job over all ranks.
+Multi-GPU: one process per GPU, streams sharded (weak scaling, no collective on the data path);
+barrier + synchronize around the K timed steps, max elapsed over ranks.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--streams 256] [--frames 1048576]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT))
+
+HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+FP64_PEAK_TFLOPS = 78.6        # MI355X FP64 vector (256 CU x 2.4 GHz x 128 flop/clk), vendor figure
+ALG_BYTES_PER_FRAME = 8        # C2 = 4 B in (2 x int16) + 4 B out (2 x int16)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--streams", type=int, default=256, help="streams per GPU (C2: 256)")
+    ap.add_argument("--frames", type=int, default=1 << 20, help="frames per stream per step (C2: 2^20)")
+    ap.add_argument("--fs", type=int, default=48000)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-workers", type=int, default=16)
+    ap.add_argument("--cpu-frames", type=int, default=1 << 21)
+    return ap.parse_args()
+
+
+def _cpu_worker(args):
+    """one CPU core: the oracle restatement (scalar C, -O2 -ffp-contract=off) over one stream"""
+    s, n_frames, fs = args
+    from in_cwave_amd import graph, synth
+    from oracle import oracle as O
+    cfg = graph.default_config(fs)
+    raw = synth.stream_pcm(s, n_frames, fs)
+    st = O.Stream(cfg, graph.graph_shift_master())
+    t0 = time.perf_counter()
+    st.process(raw, n_frames)
+    return time.perf_counter() - t0
+
+
+def cpu_baseline(workers, n_frames, fs):
+    import multiprocessing as mp
+    from oracle import oracle as O
+    O.load()
+    ctx = mp.get_context("spawn")
+    t0 = time.perf_counter()
+    with ctx.Pool(workers) as pool:
+        per = pool.map(_cpu_worker, [(s, n_frames, fs) for s in range(workers)])
+    wall = time.perf_counter() - t0
+    busy = max(per)
+    samples = 2.0 * n_frames * workers
+    return {"value": samples / busy / 1e6, "unit": "Msamples/s", "cores": workers, "kind": "port",
+            "sample": f"{workers} streams x {n_frames} frames (C2 shape, oracle C restatement, one process "
+                      f"per core), per-core {2.0 * n_frames / np.mean(per) / 1e6:.3f} Msamples/s, wall {wall:.1f}s"}
+
+
+def main():
+    a = parse()
+    import torch
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", rank=rank, world_size=world)
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+
+    from in_cwave_amd import graph, synth
+    from in_cwave_amd import lib as L
+
+    S, T, fs = a.streams, a.frames, a.fs
+    cfg = graph.default_config(fs)
+    ctx = L.Context(cfg, graph.graph_shift_master(), S, device=local)
+    # synthetic input of the C2 shape for this rank's shard of streams (SURVEY 8(d) generator);
+    # 16 distinct generated streams are tiled over the shard to bound setup time
+    n_gen = min(S, 16)
+    first = rank * S
+    gen = synth.batch_pcm(n_gen, T, fs, first=first)               # uint8 [n_gen, T*4]
+    d_in = torch.empty((S, T * 4), dtype=torch.uint8, device=dev)
+    g = torch.from_numpy(gen).to(dev)
+    for s in range(S):
+        d_in[s].copy_(g[s % n_gen])
+    d_out = torch.empty((S, T * 4), dtype=torch.uint8, device=dev)
+    torch.cuda.synchronize()
+    hip_stream = torch.cuda.current_stream(dev).cuda_stream
+
+    def step(timing):
+        ctx.process_device(d_in, d_in.stride(0), d_out, d_out.stride(0), T, timing=timing, hip_stream=hip_stream)
+
+    for _ in range(a.warmup):
+        step(False)
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    k1_ms = k2_ms = 0.0
+    k1_n = k2_n = 0
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        step(True)
+        (m1, m2), (n1, n2) = ctx.last_timing()
+        k1_ms += m1
+        k2_ms += m2
+        k1_n += n1
+        k2_n += n2
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if dist:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    frames_total = float(S) * T * a.steps * world
+    value = 2.0 * frames_total / elapsed / 1e6
+    ms_per_step = elapsed * 1e3 / a.steps
+
+    # roofline of the dominant kernel (icw_iir_state), algorithmic bytes per launch / avg duration
+    frames_per_launch = float(S) * T * a.steps / max(1, k1_n)
+    k1_avg_s = k1_ms / 1e3 / max(1, k1_n)
+    k2_avg_s = k2_ms / 1e3 / max(1, k2_n)
+    achieved = ALG_BYTES_PER_FRAME * frames_per_launch / k1_avg_s / 1e9 if k1_avg_s > 0 else None
+    flops_per_frame = 4 * 2 * (15 * 19 - 4) / 2    # the recurrence half of 1124 flops/frame
+    roof = {
+        "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+        "frac": (achieved / HBM_PEAK_GBS) if achieved else None, "traffic": None,
+        "kernel": "icw_iir_state", "alg_bytes_per_frame": ALG_BYTES_PER_FRAME,
+        "frames_per_launch": frames_per_launch, "avg_launch_ms": k1_avg_s * 1e3,
+        "output_kernel_avg_launch_ms": k2_avg_s * 1e3,
+        "fp64_tflops_chain": (1124.0 * frames_per_launch / (k1_avg_s + k2_avg_s) / 1e12) if k1_avg_s else None,
+        "fp64_peak_tflops": FP64_PEAK_TFLOPS,
+        "note": "latency-bound serial IIR recurrence: 1024 chains x ~78 dependent FP64 ops/sample (DESIGN.md)",
+    }
+    del flops_per_frame
+
+    cpu = None
+    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+        try:
+            cpu = cpu_baseline(a.cpu_workers, a.cpu_frames, fs)
+        except Exception as e:  # reported, never silently replaced
+            cpu = {"error": repr(e)}
+
+    if rank == 0:
+        line = {
+            "metric": "Msamples/s through Hilbert+mod+render",
+            "value": value, "unit": "Msamples/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
+            "ms_per_step": ms_per_step, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "dtype": "f64", "data": "synthetic",
+            "config": {"workload": "C2: 256 x 48kHz int16 stereo streams/GPU, Type-1 (order 19) Kahan "
+                                   "quadrature Hilbert + Shift(+2/-2 Hz) + Master, 16-bit ROUND",
+                       "streams_per_gpu": S, "frames_per_stream_per_step": T, "fs": fs,
+                       "parallelism": f"stream-shard x{world}"},
+            "roofline": roof,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    ctx.close()
+    if dist:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

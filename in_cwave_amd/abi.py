@@ -1,0 +1,86 @@
+"""ctypes mirror of include/icw.h (the C ABI).  Kept field-for-field identical to the header;
+tests/test_abi.py checks sizes/offsets against the header's layout rules."""
+import ctypes as C
+
+N_INPUTS = 27
+MAX_IIR_ORDER = 20
+
+# status codes
+OK, EINVAL, ENOMEM, EDEVICE, EGRAPH, EUNSUPPORTED = 0, -1, -2, -3, -4, -5
+
+# node modes / master outputs / channel exchange (in_cwave.h:152-287)
+MODE_MASTER, MODE_SHIFT, MODE_PM, MODE_MIX = 0, 1, 2, 3
+S_ADD_REIM, S_SUB_REIM, S_RE, S_IM = 0, 1, 2, 3
+XCH_NORMAL, XCH_SWAP, XCH_LEFTONLY, XCH_RIGHTONLY, XCH_MIXLR = 0, 1, 2, 3, 4
+# input formats (HRW_FMT_*)
+FMT_U8, FMT_I16, FMT_I24, FMT_I32, FMT_F32 = 0, 1, 2, 3, 4
+FMT_BYTES = {FMT_U8: 1, FMT_I16: 2, FMT_I24: 3, FMT_I32: 4, FMT_F32: 4}
+# render (sound_render.h)
+QUANTZ_MID_TREAD, QUANTZ_MID_RISER = 0, 1
+RENDER_ROUND, RENDER_RPDF, RENDER_TPDF, RENDER_STPDF, RENDER_GAUSS = 0, 1, 2, 3, 4
+NSHAPE_FLAT, NSHAPE_FW44, NSHAPE_MEW44 = 0, 1, 2
+NSHAPE_MAX = 17
+SEED_LEFT, SEED_RIGHT = 0x13579BDF, 0x479B22AB
+SR_ZERO_SIGNAL_DB = -555.0
+
+F_DEVICE_PTRS, F_DEBUG_PRE, F_TIMING = 1, 2, 4
+
+
+class Node(C.Structure):
+    _fields_ = [
+        ("mode", C.c_int32), ("n_out", C.c_int32),
+        ("gain", C.c_double * 2),
+        ("inputs", C.c_uint8 * N_INPUTS), ("pad_", C.c_uint8 * 1),
+        ("xch_mode", C.c_int32), ("iq_invert", C.c_int32 * 2),
+        ("tout", C.c_int32 * 2),
+        ("fr_shift", C.c_double * 2), ("is_shift", C.c_int32 * 2),
+        ("pm_freq", C.c_double * 2), ("pm_phase", C.c_double * 2),
+        ("pm_level", C.c_double * 2), ("pm_angle", C.c_double * 2),
+        ("is_pm", C.c_int32 * 2),
+        ("lock_gain", C.c_int32), ("lock_shift", C.c_int32), ("sign_lock_shift", C.c_int32),
+        ("lock_freq", C.c_int32), ("lock_phase", C.c_int32), ("lock_level", C.c_int32),
+        ("lock_angle", C.c_int32), ("reserved_", C.c_int32),
+    ]
+
+
+class RenderCfg(C.Structure):
+    _fields_ = [("dth_bits", C.c_double), ("quantz_type", C.c_uint32), ("render_type", C.c_uint32),
+                ("nshape_type", C.c_uint32), ("sign_bits16", C.c_uint32), ("sign_bits24", C.c_uint32)]
+
+
+class Config(C.Structure):
+    _fields_ = [
+        ("sample_rate", C.c_uint32), ("in_format", C.c_uint32), ("in_channels", C.c_uint32),
+        ("hilbert_type", C.c_uint32), ("iir_kahan", C.c_int32), ("iir_subnorm_reject", C.c_int32),
+        ("frmod_scaled", C.c_int32), ("need24bits", C.c_int32), ("bypass_list", C.c_int32),
+        ("seed_left", C.c_uint32), ("seed_right", C.c_uint32),
+        ("render", RenderCfg),
+    ]
+
+
+class Meters(C.Structure):
+    _fields_ = [("clips", C.c_uint32 * 2), ("peak_db", C.c_double * 2), ("desubnorm", C.c_uint64)]
+
+
+# every function declared in include/icw.h: name -> (restype, argtypes)
+_vp, _sz, _i, _u = C.c_void_p, C.c_size_t, C.c_int, C.c_uint
+SIGNATURES = {
+    "icw_create": (_i, [C.POINTER(Config), C.POINTER(Node), _i, _i, _i, C.POINTER(_vp), C.POINTER(_i)]),
+    "icw_destroy": (_i, [_vp]),
+    "icw_stream_init": (_i, [_vp, _i, _i]),
+    "icw_stream_open": (_i, [_vp, _i, C.c_int64, C.c_uint32, C.c_uint32, C.c_uint32, _i, _i]),
+    "icw_stream_reset_hilbert": (_i, [_vp, _i]),
+    "icw_stream_reset_framecnt": (_i, [_vp, _i]),
+    "icw_process_batch": (_i, [_vp, _vp, _sz, _vp, _sz, _i, _u, _vp, _vp]),
+    "icw_process_streams": (_i, [_vp, _i, _i, _vp, _sz, _vp, _sz, _i, _u, _vp, _vp]),
+    "icw_synchronize": (_i, [_vp]),
+    "icw_get_meters": (_i, [_vp, _i, _i, C.POINTER(Meters)]),
+    "icw_render_size": (_i, [_vp]),
+    "icw_n_frame": (_i, [_vp, _i, C.POINTER(C.c_uint64)]),
+    "icw_state_size": (_sz, [_vp]),
+    "icw_get_state": (_i, [_vp, _i, _vp, _sz]),
+    "icw_set_state": (_i, [_vp, _i, _vp, _sz]),
+    "icw_last_timing": (_i, [_vp, C.POINTER(C.c_double), C.POINTER(_i)]),
+    "icw_version": (C.c_char_p, []),
+    "icw_strerror": (C.c_char_p, [_i]),
+}

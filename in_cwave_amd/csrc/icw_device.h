@@ -1,0 +1,107 @@
+/*
+ * icw_device.h -- data structures shared by the host orchestration (icw_host.cpp) and the
+ * gfx950 kernels (icw_kernels.hip).  Plain structs passed by value as kernel arguments or
+ * placed in device memory; no HIP types.
+ */
+#ifndef ICW_DEVICE_H_
+#define ICW_DEVICE_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#define ICW_MAX_OPS   16     /* compiled DSP ops (nodes) per graph on the device path */
+#define ICW_MAX_REGS  8      /* value registers: `in`, node outputs, persistent slots */
+#define ICW_K2_TILE   256    /* frames per output-kernel workgroup */
+#define ICW_HIST_PITCH 20    /* doubles per chain in the delay-line state */
+
+/* Arguments of the input prep kernel (one thread = one frame). */
+struct IcwK0Args {
+    const unsigned char *in;       /* stream s at in + s*in_stride */
+    size_t in_stride;
+    uint32_t fmt, csz, fsz, nch;   /* sample format, channel/frame bytes, channels */
+    int32_t n_streams, T;
+    const long long *pos;          /* [n_streams] reader position (frames into track) */
+    const long long *fade;         /* [n_streams][3] n_samples, n_fade_in, n_fade_out */
+    double *xd;                    /* [n_streams][2][x_pitch] faded input, channel-planar */
+    size_t x_pitch;
+};
+
+/* Arguments of the IIR state kernel (one lane = one DF-II chain). */
+struct IcwK1Args {
+    const double *xd;              /* K0 output */
+    size_t x_pitch;
+    uint32_t nch;
+    int32_t n_streams, n_chains, T;
+    double *hist;                  /* [n_chains][ICW_HIST_PITCH], index 0 = most recent w */
+    unsigned long long *sncnt;     /* [n_chains] subnorm rejections */
+    uint32_t *hq_phase;            /* [n_streams][2] Hilbert sample phase (sampe_ix) */
+    long long *pos;                /* [n_streams] reader position, advanced by T */
+    unsigned long long *n_frame;   /* [n_streams] modulator frame counter */
+    unsigned long long ssr;        /* sample_rate * HZ_SCALE (scaled mode) */
+    int32_t scaled;
+    double *w;                     /* [n_chains][w_pitch]: rows [0,N) history, [N,N+T) block */
+    size_t w_pitch;
+    uint32_t *info_phase;          /* [n_streams][2] block-start Hilbert phases (for K2) */
+    unsigned long long *info_nframe; /* [n_streams] block-start n_frame (for K2) */
+    double pc[20];                 /* loop-back coefficients -a[i+1]/a0 */
+};
+
+/* One compiled DSP node (adv_modulator.c:637-751), executed in list order tail -> head. */
+struct IcwOp {
+    int32_t mode;                  /* ICW_MODE_* */
+    int32_t n_in;                  /* inputs, in bus-slot order */
+    int32_t in_reg[27];            /* value register each input resolves to */
+    int32_t out_reg;               /* register the node's output lands in (not MASTER) */
+    int32_t xch, iqinv[2];
+    int32_t tout[2];
+    int32_t act[2];                /* is_shift / is_pm per channel */
+    int32_t neg[2];                /* shift: negative frequency -> sin_v = -sin_v */
+    double gain[2];
+    double f[2];                   /* effective (scaled) frequency */
+    double pp[2], lp[2], fa[2];    /* PM: fphase*PI, flevel*PI, fangle */
+};
+
+struct IcwProg {
+    int32_t n_ops;
+    int32_t n_regs;
+    int32_t bypass;                /* am.is_bypass_list: only the Master, on raw `in` */
+    int32_t n_persist;             /* slots read before any write in the frame and never written */
+    int32_t persist_reg[ICW_MAX_REGS], persist_slot[ICW_MAX_REGS];
+    int32_t n_wb;                  /* slots written in the frame: final value -> persistent bus */
+    int32_t wb_reg[ICW_MAX_REGS + ICW_MAX_OPS], wb_slot[ICW_MAX_REGS + ICW_MAX_OPS];
+    IcwOp ops[ICW_MAX_OPS];
+};
+
+/* Render constants computed on the host by the sound_render_recalc arithmetic
+ * (sound_render.c:499-581), so pow() runs once on the CPU exactly as in the reference. */
+struct IcwRenderK {
+    double norm_mul, dth_mul, hi, lo, round_offset;
+    int32_t sign_delta, norm_shift, is24;
+    int32_t render_type, ns_kind, ns_n;
+    double ns_c[40];
+};
+
+/* Arguments of the output kernel (frame-parallel: Kahan output sums, unmix, graph, render). */
+struct IcwK2Args {
+    const double *w;               /* [n_chains][w_pitch] */
+    size_t w_pitch;
+    int32_t n_streams, T, n_chains;
+    const uint32_t *info_phase;
+    const unsigned long long *info_nframe;
+    unsigned long long ssr;
+    int32_t scaled;
+    uint32_t sample_rate;
+    const IcwProg *prog;
+    double *bus;                   /* [n_streams][27][4] persistent bus */
+    unsigned char *out;            /* stream s at out + s*out_stride */
+    size_t out_stride;
+    double *pre;                   /* nullable [n_streams][T][2] pre-render doubles */
+    size_t pre_stride;             /* in doubles, per stream */
+    int32_t do_render;             /* elementwise ROUND/flat render in this kernel */
+    uint32_t *clips;               /* [n_streams][2] */
+    unsigned long long *peak_bits; /* [n_streams][2] max |q| as ordered bits */
+    IcwRenderK rk;
+    double pc[20], pd[20], d0;
+};
+
+#endif

@@ -1,0 +1,772 @@
+/*
+ * icw_host.cpp -- host side of the in_cwave_amd C ABI (include/icw.h): context lifecycle,
+ * DSP-list normalisation and compilation, per-stream state in HBM, block scheduling of the
+ * gfx950 kernels, meters and state (de)serialisation.
+ *
+ * There is no CPU compute path here: every sample goes through icw_kernels.hip.  A missing or
+ * unusable HIP device is an error (ICW_EDEVICE), never a fallback.
+ */
+#include <hip/hip_runtime_api.h>
+
+#include <math.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <algorithm>
+#include <mutex>
+#include <new>
+#include <vector>
+
+#include "../../include/icw.h"
+#include "icw_device.h"
+#include "icw_tables.inc"
+
+extern "C" hipError_t icw_launch_unpack(const IcwK0Args *a, hipStream_t st);
+extern "C" hipError_t icw_launch_iir_state(const IcwK1Args *a, int nord, int kahan, int subn, hipStream_t st);
+extern "C" hipError_t icw_launch_output(const IcwK2Args *a, int nord, int kahan, hipStream_t st);
+
+#define ICW_PI_H (3.1415926535897932384626433832795029)
+
+namespace {
+
+double u2d(unsigned long long u)
+{
+    double d;
+    memcpy(&d, &u, 8);
+    return d;
+}
+
+/* frames per kernel launch: bounds the w scratch buffer (n_chains * (T+N) doubles) */
+constexpr int kMaxBlockFrames = 1 << 16;
+
+struct DevState {
+    double *hist = nullptr;               /* [chains][20] */
+    unsigned long long *sncnt = nullptr;  /* [chains] */
+    uint32_t *hq_phase = nullptr;         /* [streams][2] */
+    long long *pos = nullptr;             /* [streams] */
+    long long *fade = nullptr;            /* [streams][3] */
+    unsigned long long *n_frame = nullptr;/* [streams] */
+    double *bus = nullptr;                /* [streams][27][4] */
+    uint32_t *clips = nullptr;            /* [streams][2] */
+    unsigned long long *peak_bits = nullptr; /* [streams][2] */
+};
+
+}  // namespace
+
+struct icw_ctx {
+    icw_config cfg{};
+    std::vector<icw_node> nodes;
+    int n_streams = 0;
+    int device = 0;
+    int nord = 0;
+    double pc[20]{}, pd[20]{}, d0 = 0.0;
+    IcwRenderK rk{};
+    IcwProg prog{};
+    IcwProg *d_prog = nullptr;
+    DevState st;
+    /* host mirrors of meters that survive "reset" semantics */
+    std::vector<double> peak_db;          /* [streams][2] */
+    /* scratch */
+    double *w = nullptr;
+    size_t w_bytes = 0;
+    double *xd = nullptr;
+    size_t xd_bytes = 0;
+    uint32_t *info_phase = nullptr;
+    unsigned long long *info_nframe = nullptr;
+    unsigned char *d_in = nullptr, *d_out = nullptr;
+    size_t d_in_bytes = 0, d_out_bytes = 0;
+    double *d_pre = nullptr;
+    size_t d_pre_bytes = 0;
+    hipStream_t stream = nullptr;
+    std::vector<hipEvent_t> ev;
+    double last_ms[2]{};
+    int last_launches[2]{};
+    std::mutex mu;
+};
+
+namespace {
+
+int set_dev(icw_ctx *c)
+{
+    return hipSetDevice(c->device) == hipSuccess ? ICW_OK : ICW_EDEVICE;
+}
+
+template <class T>
+int dalloc(T **p, size_t n)
+{
+    *p = nullptr;
+    if (n == 0) n = 1;
+    if (hipMalloc((void **)p, n * sizeof(T)) != hipSuccess) return ICW_ENOMEM;
+    if (hipMemset(*p, 0, n * sizeof(T)) != hipSuccess) return ICW_EDEVICE;
+    return ICW_OK;
+}
+
+unsigned fmt_size(unsigned fmt)
+{
+    static const unsigned sz[5] = {1, 2, 3, 4, 4};
+    return fmt < 5 ? sz[fmt] : 0;
+}
+
+/* amod_init (adv_modulator.c:216-331): accept the list only if its head is the one and only
+ * Master and every mode is known; apply the L/R locks.  Otherwise the default Master. */
+bool graph_accept(std::vector<icw_node> &n)
+{
+    if (n.empty() || n[0].mode != ICW_MODE_MASTER) return false;
+    bool was_master = false;
+    for (auto &t : n) {
+        if (t.lock_gain) { t.gain[1] = t.gain[0]; t.iq_invert[1] = t.iq_invert[0]; }
+        switch (t.mode) {
+        case ICW_MODE_MASTER:
+            if (was_master) return false;
+            was_master = true;
+            break;
+        case ICW_MODE_SHIFT:
+            if (t.lock_shift) {
+                t.fr_shift[1] = t.sign_lock_shift ? -t.fr_shift[0] : t.fr_shift[0];
+                t.is_shift[1] = t.is_shift[0];
+            }
+            break;
+        case ICW_MODE_PM:
+            if (t.lock_freq) { t.pm_freq[1] = t.pm_freq[0]; t.is_pm[1] = t.is_pm[0]; }
+            if (t.lock_phase) t.pm_phase[1] = t.pm_phase[0];
+            if (t.lock_level) t.pm_level[1] = t.pm_level[0];
+            if (t.lock_angle) t.pm_angle[1] = t.pm_angle[0];
+            break;
+        case ICW_MODE_MIX:
+            break;
+        default:
+            return false;
+        }
+    }
+    return true;
+}
+
+icw_node default_master()
+{
+    icw_node n;
+    memset(&n, 0, sizeof(n));
+    n.mode = ICW_MODE_MASTER;
+    n.gain[0] = n.gain[1] = 0.8;           /* DEF_GAIN_MASTER, in_cwave.h:167 */
+    n.tout[0] = n.tout[1] = ICW_S_ADD_REIM;
+    n.inputs[0] = 1;                       /* adv_modulator.c:112-118 */
+    n.lock_gain = 1;
+    return n;
+}
+
+/* DGET_SCALED_FR (adv_modulator.c:35-39) */
+double scaled_fr(double f) { return (double)((unsigned)(f * ((double)ICW_HZ_SCALE) + 0.5)); }
+
+/* Compile the normalised DSP list into register form.  Execution order is tail -> head
+ * (adv_modulator.c:637).  Each input slot resolves to the value most recently written in the
+ * same frame; a slot never written by any node reads its persistent bus value.  A slot read
+ * before its writer runs (a one-frame delay, doc 3.1) is not yet on the device path. */
+int compile_graph(const std::vector<icw_node> &nodes, int bypass, IcwProg &P)
+{
+    memset(&P, 0, sizeof(P));
+    P.bypass = bypass;
+    std::vector<int> order;
+    if (bypass) order.push_back(0);
+    else for (int i = (int)nodes.size() - 1; i >= 0; --i) order.push_back(i);
+    if ((int)order.size() > ICW_MAX_OPS) return ICW_EUNSUPPORTED;
+
+    bool written_any[ICW_N_INPUTS] = {false};
+    for (int i : order)
+        if (nodes[i].mode != ICW_MODE_MASTER) {
+            const int o = nodes[i].n_out;
+            if (o < 0 || o >= ICW_N_INPUTS) return ICW_EGRAPH;
+            written_any[o] = true;
+        }
+    int cur[ICW_N_INPUTS];
+    for (int k = 0; k < ICW_N_INPUTS; ++k) cur[k] = -1;
+    cur[0] = 0;
+    int n_regs = 1;
+    for (size_t oi = 0; oi < order.size(); ++oi) {
+        const icw_node &n = nodes[order[oi]];
+        IcwOp &op = P.ops[oi];
+        op.mode = n.mode;
+        if (!bypass) {
+            for (int k = 0; k < ICW_N_INPUTS; ++k) {
+                if (!n.inputs[k]) continue;
+                int r = cur[k];
+                if (r < 0) {
+                    if (written_any[k]) return ICW_EUNSUPPORTED;   /* delayed (feedback) read */
+                    if (n_regs >= ICW_MAX_REGS) return ICW_EUNSUPPORTED;
+                    r = n_regs++;
+                    P.persist_reg[P.n_persist] = r;
+                    P.persist_slot[P.n_persist] = k;
+                    ++P.n_persist;
+                    cur[k] = r;
+                }
+                op.in_reg[op.n_in++] = r;
+            }
+        }
+        op.xch = n.xch_mode;
+        op.iqinv[0] = n.iq_invert[0];
+        op.iqinv[1] = n.iq_invert[1];
+        op.gain[0] = n.gain[0];
+        op.gain[1] = n.gain[1];
+        for (int c = 0; c < 2; ++c) {
+            op.tout[c] = n.tout[c];
+            if (n.mode == ICW_MODE_SHIFT) {
+                op.act[c] = n.is_shift[c];
+                double f = n.fr_shift[c];
+                op.neg[c] = f < 0.0;
+                if (f < 0.0) f = -f;
+                op.f[c] = f;   /* scaled below if frmod_scaled */
+            } else if (n.mode == ICW_MODE_PM) {
+                op.act[c] = n.is_pm[c];
+                op.f[c] = n.pm_freq[c];
+                op.pp[c] = n.pm_phase[c] * ICW_PI_H;              /* fphase * PI */
+                op.lp[c] = n.pm_level[c] * ICW_PI_H;              /* flevel * PI */
+                op.fa[c] = n.pm_angle[c];
+            }
+        }
+        if (n.mode != ICW_MODE_MASTER) {
+            if (n_regs >= ICW_MAX_REGS) return ICW_EUNSUPPORTED;
+            op.out_reg = n_regs++;
+            cur[n.n_out] = op.out_reg;
+        }
+    }
+    P.n_ops = (int)order.size();
+    P.n_regs = n_regs;
+    for (int k = 0; k < ICW_N_INPUTS; ++k)
+        if (written_any[k] && cur[k] >= 0) {
+            P.wb_reg[P.n_wb] = cur[k];
+            P.wb_slot[P.n_wb] = k;
+            ++P.n_wb;
+        }
+    return ICW_OK;
+}
+
+/* sound_render_recalc arithmetic (sound_render.c:499-581) */
+void render_consts(const icw_render_cfg &cfg, int is24, IcwRenderK &k)
+{
+    memset(&k, 0, sizeof(k));
+    k.dth_mul = pow(2.0, cfg.dth_bits) - 1.0;
+    if (cfg.quantz_type == ICW_QUANTZ_MID_TREAD) { k.round_offset = 0.5; k.sign_delta = 0; }
+    else { k.round_offset = 0.0; k.sign_delta = -1; }
+    if (is24) {
+        long long hib = 0x800000LL;
+        k.norm_shift = 24 - (int)cfg.sign_bits24;
+        hib >>= k.norm_shift;
+        k.hi = (double)hib;
+        k.lo = -(double)(hib + 1 + k.sign_delta);
+        k.norm_mul = (k.norm_shift < 8) ? (double)(0x100 >> k.norm_shift)
+                                         : 1.0 / (double)(1ULL << (k.norm_shift - 8));
+    } else {
+        long long hib = 0x8000LL;
+        k.norm_shift = 16 - (int)cfg.sign_bits16;
+        hib >>= k.norm_shift;
+        k.hi = (double)hib;
+        k.lo = -(double)(hib + 1 + k.sign_delta);
+        k.norm_mul = 1.0 / (double)(1ULL << k.norm_shift);
+    }
+    k.lo -= (double)k.sign_delta;
+    k.is24 = is24;
+    k.render_type = (int)cfg.render_type;
+    unsigned t = cfg.nshape_type > ICW_NSHAPE_MAX ? ICW_NSHAPE_FLAT : cfg.nshape_type;
+    k.ns_kind = icw_ns_kind[t];
+    k.ns_n = icw_ns_n[t];
+    const int nc = k.ns_kind == 2 ? 2 * k.ns_n : k.ns_n;
+    for (int i = 0; i < nc; ++i) k.ns_c[i] = u2d(icw_ns_c[t][i]);
+}
+
+int grow(void **p, size_t *cur, size_t need)
+{
+    if (*cur >= need) return ICW_OK;
+    if (*p) hipFree(*p);
+    *p = nullptr;
+    *cur = 0;
+    if (hipMalloc(p, need) != hipSuccess) return ICW_ENOMEM;
+    *cur = need;
+    return ICW_OK;
+}
+
+void free_all(icw_ctx *c)
+{
+    DevState &s = c->st;
+    void *ptrs[] = {s.hist, s.sncnt, s.hq_phase, s.pos, s.fade, s.n_frame, s.bus, s.clips, s.peak_bits,
+                    c->d_prog, c->w, c->xd, c->info_phase, c->info_nframe, c->d_in, c->d_out, c->d_pre};
+    for (void *p : ptrs)
+        if (p) hipFree(p);
+    for (auto e : c->ev) hipEventDestroy(e);
+    if (c->stream) hipStreamDestroy(c->stream);
+}
+
+}  // namespace
+
+extern "C" {
+
+const char *icw_version(void) { return "in_cwave_amd 0.1 (gfx950)"; }
+
+const char *icw_strerror(int s)
+{
+    switch (s) {
+    case ICW_OK: return "ok";
+    case ICW_EINVAL: return "invalid argument";
+    case ICW_ENOMEM: return "out of memory";
+    case ICW_EDEVICE: return "HIP device error";
+    case ICW_EGRAPH: return "DSP list rejected";
+    case ICW_EUNSUPPORTED: return "configuration not supported on the device path";
+    }
+    return "unknown";
+}
+
+int icw_create(const icw_config *cfg, const icw_node *nodes, int n_nodes, int n_streams, int device,
+               icw_ctx **out, int *accepted)
+{
+    if (!cfg || !out || n_streams <= 0 || n_nodes < 0 || (n_nodes > 0 && !nodes)) return ICW_EINVAL;
+    *out = nullptr;
+    if (cfg->hilbert_type > 5 || cfg->in_format > ICW_FMT_F32 || cfg->in_channels == 0 ||
+        cfg->sample_rate == 0 || cfg->sample_rate > ICW_MAX_FS_SRC)
+        return ICW_EINVAL;
+    if (cfg->render.sign_bits16 < 2 || cfg->render.sign_bits16 > 16 || cfg->render.sign_bits24 < 2 ||
+        cfg->render.sign_bits24 > 24 || cfg->render.quantz_type > 1 || cfg->render.render_type > 4)
+        return ICW_EINVAL;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return ICW_EDEVICE;
+    icw_ctx *c = new (std::nothrow) icw_ctx();
+    if (!c) return ICW_ENOMEM;
+    c->cfg = *cfg;
+    if (device < 0) {
+        if (hipGetDevice(&device) != hipSuccess) { delete c; return ICW_EDEVICE; }
+    }
+    c->device = device;
+    if (set_dev(c)) { delete c; return ICW_EDEVICE; }
+    c->nodes.assign(nodes, nodes + n_nodes);
+    const bool ok = graph_accept(c->nodes);
+    if (!ok) c->nodes.assign(1, default_master());
+    if (accepted) *accepted = ok ? 1 : 0;
+    if (cfg->frmod_scaled)
+        for (auto &n : c->nodes)
+            if (n.mode == ICW_MODE_SHIFT || n.mode == ICW_MODE_PM) {
+                /* scaled frequencies are formed from |f| (dsp_shift) or f (dsp_pm) */
+                for (int ch = 0; ch < 2; ++ch) {
+                    if (n.mode == ICW_MODE_PM) n.pm_freq[ch] = scaled_fr(n.pm_freq[ch]);
+                }
+            }
+    int rc = compile_graph(c->nodes, cfg->bypass_list, c->prog);
+    if (rc) { delete c; return rc; }
+    if (cfg->frmod_scaled)
+        for (int i = 0; i < c->prog.n_ops; ++i)
+            if (c->prog.ops[i].mode == ICW_MODE_SHIFT)
+                for (int ch = 0; ch < 2; ++ch) c->prog.ops[i].f[ch] = scaled_fr(c->prog.ops[i].f[ch]);
+    /* filter coefficients exactly as iir_rp_create (hblpf.c:849-856) */
+    const int t = (int)cfg->hilbert_type;
+    c->nord = icw_hb_order[t];
+    const double a0 = u2d(icw_hb_a[t][0]);
+    c->d0 = u2d(icw_hb_b[t][0]) / a0;
+    for (int i = 0; i < c->nord; ++i) {
+        c->pc[i] = -u2d(icw_hb_a[t][i + 1]) / a0;
+        c->pd[i] = u2d(icw_hb_b[t][i + 1]) / a0;
+    }
+    render_consts(cfg->render, cfg->need24bits, c->rk);
+    if (!(cfg->render.render_type == ICW_RENDER_ROUND && c->rk.ns_kind == 0)) {
+        delete c;
+        return ICW_EUNSUPPORTED;   /* dithered / noise-shaped render: serial kernel pending */
+    }
+    c->n_streams = n_streams;
+    const size_t S = (size_t)n_streams, C = S * 4;
+    rc = ICW_OK;
+    DevState &s = c->st;
+    rc |= dalloc(&s.hist, C * ICW_HIST_PITCH);
+    rc |= dalloc(&s.sncnt, C);
+    rc |= dalloc(&s.hq_phase, S * 2);
+    rc |= dalloc(&s.pos, S);
+    rc |= dalloc(&s.fade, S * 3);
+    rc |= dalloc(&s.n_frame, S);
+    rc |= dalloc(&s.bus, S * ICW_N_INPUTS * 4);
+    rc |= dalloc(&s.clips, S * 2);
+    rc |= dalloc(&s.peak_bits, S * 2);
+    rc |= dalloc(&c->info_phase, S * 2);
+    rc |= dalloc(&c->info_nframe, S);
+    rc |= dalloc(&c->d_prog, 1);
+    if (rc == ICW_OK && hipMemcpy(c->d_prog, &c->prog, sizeof(IcwProg), hipMemcpyHostToDevice) != hipSuccess)
+        rc = ICW_EDEVICE;
+    if (rc == ICW_OK && hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) rc = ICW_EDEVICE;
+    if (rc != ICW_OK) {
+        free_all(c);
+        delete c;
+        return rc < 0 ? (rc == ICW_ENOMEM ? ICW_ENOMEM : ICW_EDEVICE) : ICW_EDEVICE;
+    }
+    c->peak_db.assign(S * 2, ICW_SR_ZERO_SIGNAL_DB);
+    rc = icw_stream_init(c, 0, n_streams);
+    if (rc) { free_all(c); delete c; return rc; }
+    *out = c;
+    return ICW_OK;
+}
+
+int icw_destroy(icw_ctx *c)
+{
+    if (!c) return ICW_EINVAL;
+    set_dev(c);
+    hipStreamSynchronize(c->stream);
+    free_all(c);
+    delete c;
+    return ICW_OK;
+}
+
+int icw_stream_init(icw_ctx *c, int first, int count)
+{
+    if (!c || first < 0 || count < 0 || first + count > c->n_streams) return ICW_EINVAL;
+    if (count == 0) return ICW_OK;
+    std::lock_guard<std::mutex> lk(c->mu);
+    if (set_dev(c)) return ICW_EDEVICE;
+    DevState &s = c->st;
+    const size_t f = (size_t)first, n = (size_t)count;
+    hipStream_t st = c->stream;
+    bool ok = true;
+    ok &= hipMemsetAsync(s.hist + f * 4 * ICW_HIST_PITCH, 0, n * 4 * ICW_HIST_PITCH * sizeof(double), st) == hipSuccess;
+    ok &= hipMemsetAsync(s.sncnt + f * 4, 0, n * 4 * sizeof(unsigned long long), st) == hipSuccess;
+    ok &= hipMemsetAsync(s.hq_phase + f * 2, 0, n * 2 * sizeof(uint32_t), st) == hipSuccess;
+    ok &= hipMemsetAsync(s.pos + f, 0, n * sizeof(long long), st) == hipSuccess;
+    ok &= hipMemsetAsync(s.n_frame + f, 0, n * sizeof(unsigned long long), st) == hipSuccess;
+    ok &= hipMemsetAsync(s.bus + f * ICW_N_INPUTS * 4, 0, n * ICW_N_INPUTS * 4 * sizeof(double), st) == hipSuccess;
+    ok &= hipMemsetAsync(s.clips + f * 2, 0, n * 2 * sizeof(uint32_t), st) == hipSuccess;
+    ok &= hipMemsetAsync(s.peak_bits + f * 2, 0, n * 2 * sizeof(unsigned long long), st) == hipSuccess;
+    /* no track open: n_samples "infinite", no fades (xwave_unpack_csample never fades) */
+    std::vector<long long> fd(n * 3);
+    for (size_t i = 0; i < n; ++i) { fd[i * 3] = (long long)1 << 62; fd[i * 3 + 1] = 0; fd[i * 3 + 2] = 0; }
+    ok &= hipMemcpyAsync(s.fade + f * 3, fd.data(), fd.size() * sizeof(long long), hipMemcpyHostToDevice, st) == hipSuccess;
+    ok &= hipStreamSynchronize(st) == hipSuccess;
+    for (size_t i = f * 2; i < (f + n) * 2; ++i) c->peak_db[i] = ICW_SR_ZERO_SIGNAL_DB;
+    return ok ? ICW_OK : ICW_EDEVICE;
+}
+
+int icw_stream_open(icw_ctx *c, int s, int64_t n_samples, uint32_t fade_in, uint32_t fade_out,
+                    uint32_t sec_align, int clr_nframe, int clr_hilb)
+{
+    if (!c || s < 0 || s >= c->n_streams || n_samples < 0) return ICW_EINVAL;
+    (void)sec_align;   /* the virtual zero tail is produced by the reader (xwave_read_samples) */
+    long long nfi = (long long)(((uint64_t)fade_in * (uint64_t)c->cfg.sample_rate) / 1000ULL);
+    long long nfo = (long long)(((uint64_t)fade_out * (uint64_t)c->cfg.sample_rate) / 1000ULL);
+    if (nfi + nfo >= n_samples) {
+        if (n_samples < 300LL) nfi = nfo = 0;
+        else {
+            if (nfi) nfi = n_samples / 3;
+            if (nfo) nfo = n_samples / 3;
+        }
+    }
+    std::lock_guard<std::mutex> lk(c->mu);
+    if (set_dev(c)) return ICW_EDEVICE;
+    long long fd[3] = {(long long)n_samples, nfi, nfo};
+    bool ok = hipMemcpy(c->st.fade + (size_t)s * 3, fd, sizeof(fd), hipMemcpyHostToDevice) == hipSuccess;
+    ok &= hipMemset(c->st.pos + s, 0, sizeof(long long)) == hipSuccess;
+    if (clr_nframe) ok &= hipMemset(c->st.n_frame + s, 0, sizeof(unsigned long long)) == hipSuccess;
+    if (clr_hilb) {
+        ok &= hipMemset(c->st.hist + (size_t)s * 4 * ICW_HIST_PITCH, 0, 4 * ICW_HIST_PITCH * sizeof(double)) == hipSuccess;
+        ok &= hipMemset(c->st.sncnt + (size_t)s * 4, 0, 4 * sizeof(unsigned long long)) == hipSuccess;
+        ok &= hipMemset(c->st.hq_phase + (size_t)s * 2, 0, 2 * sizeof(uint32_t)) == hipSuccess;
+    }
+    /* sound_render_set_outbits -> recalc: ROUND/flat keeps no shaping state on this path */
+    return ok ? ICW_OK : ICW_EDEVICE;
+}
+
+int icw_stream_reset_hilbert(icw_ctx *c, int s)
+{
+    if (!c || s < 0 || s >= c->n_streams) return ICW_EINVAL;
+    std::lock_guard<std::mutex> lk(c->mu);
+    if (set_dev(c)) return ICW_EDEVICE;
+    bool ok = hipMemset(c->st.hist + (size_t)s * 4 * ICW_HIST_PITCH, 0, 4 * ICW_HIST_PITCH * sizeof(double)) == hipSuccess;
+    ok &= hipMemset(c->st.sncnt + (size_t)s * 4, 0, 4 * sizeof(unsigned long long)) == hipSuccess;
+    ok &= hipMemset(c->st.hq_phase + (size_t)s * 2, 0, 2 * sizeof(uint32_t)) == hipSuccess;
+    return ok ? ICW_OK : ICW_EDEVICE;
+}
+
+int icw_stream_reset_framecnt(icw_ctx *c, int s)
+{
+    if (!c || s < 0 || s >= c->n_streams) return ICW_EINVAL;
+    std::lock_guard<std::mutex> lk(c->mu);
+    if (set_dev(c)) return ICW_EDEVICE;
+    return hipMemset(c->st.n_frame + s, 0, sizeof(unsigned long long)) == hipSuccess ? ICW_OK : ICW_EDEVICE;
+}
+
+int icw_render_size(const icw_ctx *c) { return c ? (c->cfg.need24bits ? 3 : 2) : ICW_EINVAL; }
+
+int icw_process_streams(icw_ctx *c, int first, int count, const void *in, size_t in_stride, void *out,
+                        size_t out_stride, int n_frames, unsigned flags, void *dbg, void *hip_stream)
+{
+    if (!c || first < 0 || count <= 0 || first + count > c->n_streams || n_frames < 0 || !in || !out)
+        return ICW_EINVAL;
+    if (n_frames == 0) return ICW_OK;
+    std::lock_guard<std::mutex> lk(c->mu);
+    if (set_dev(c)) return ICW_EDEVICE;
+    hipStream_t st = hip_stream ? (hipStream_t)hip_stream : c->stream;
+    const icw_config &cfg = c->cfg;
+    const unsigned csz = fmt_size(cfg.in_format);
+    const unsigned nch = cfg.in_channels;
+    const unsigned fsz = csz * nch;
+    const int osz = 2 * (cfg.need24bits ? 3 : 2);
+    const bool dev = flags & ICW_F_DEVICE_PTRS;
+    const bool timing = flags & 4u;
+    const size_t S = (size_t)count;
+    if (!dev && (in_stride < (size_t)n_frames * fsz || out_stride < (size_t)n_frames * osz)) return ICW_EINVAL;
+
+    const unsigned char *d_in;
+    unsigned char *d_out;
+    size_t dis, dos;
+    if (dev) {
+        d_in = (const unsigned char *)in;
+        d_out = (unsigned char *)out;
+        dis = in_stride;
+        dos = out_stride;
+    } else {
+        dis = (size_t)n_frames * fsz;
+        dos = (size_t)n_frames * osz;
+        if (grow((void **)&c->d_in, &c->d_in_bytes, dis * S)) return ICW_ENOMEM;
+        if (grow((void **)&c->d_out, &c->d_out_bytes, dos * S)) return ICW_ENOMEM;
+        if (hipMemcpy2DAsync(c->d_in, dis, in, in_stride, dis, S, hipMemcpyHostToDevice, st) != hipSuccess)
+            return ICW_EDEVICE;
+        d_in = c->d_in;
+        d_out = c->d_out;
+    }
+    double *d_pre = nullptr;
+    if (flags & ICW_F_DEBUG_PRE) {
+        if (!dbg) return ICW_EINVAL;
+        if (dev) d_pre = (double *)dbg;
+        else {
+            if (grow((void **)&c->d_pre, &c->d_pre_bytes, S * (size_t)n_frames * 2 * sizeof(double))) return ICW_ENOMEM;
+            d_pre = c->d_pre;
+        }
+    }
+
+    const int N = c->nord;
+    const int Tb = std::min(n_frames, kMaxBlockFrames);
+    const size_t w_pitch = (size_t)Tb + N + 1;
+    if (grow((void **)&c->w, &c->w_bytes, S * 4 * w_pitch * sizeof(double))) return ICW_ENOMEM;
+    const size_t x_pitch = ((size_t)Tb + 1) & ~(size_t)1;
+    if (grow((void **)&c->xd, &c->xd_bytes, S * 2 * x_pitch * sizeof(double))) return ICW_ENOMEM;
+
+    DevState &ds = c->st;
+    const size_t f0 = (size_t)first;
+    const int n_blocks = (n_frames + Tb - 1) / Tb;
+    if (timing && (int)c->ev.size() < 3 * n_blocks) {
+        while ((int)c->ev.size() < 3 * n_blocks) {
+            hipEvent_t e;
+            if (hipEventCreate(&e) != hipSuccess) return ICW_EDEVICE;
+            c->ev.push_back(e);
+        }
+    }
+    for (int b = 0; b < n_blocks; ++b) {
+        const int t0 = b * Tb;
+        const int T = std::min(Tb, n_frames - t0);
+        IcwK0Args a0;
+        memset(&a0, 0, sizeof(a0));
+        a0.in = d_in + (size_t)t0 * fsz;
+        a0.in_stride = dis;
+        a0.fmt = cfg.in_format;
+        a0.csz = csz;
+        a0.fsz = fsz;
+        a0.nch = nch;
+        a0.n_streams = count;
+        a0.T = T;
+        a0.pos = ds.pos + f0;
+        a0.fade = ds.fade + f0 * 3;
+        a0.xd = c->xd;
+        a0.x_pitch = x_pitch;
+        if (icw_launch_unpack(&a0, st) != hipSuccess) return ICW_EDEVICE;
+
+        IcwK1Args a1;
+        memset(&a1, 0, sizeof(a1));
+        a1.xd = c->xd;
+        a1.x_pitch = x_pitch;
+        a1.nch = nch;
+        a1.n_streams = count;
+        a1.n_chains = count * 4;
+        a1.T = T;
+        a1.hist = ds.hist + f0 * 4 * ICW_HIST_PITCH;
+        a1.sncnt = ds.sncnt + f0 * 4;
+        a1.hq_phase = ds.hq_phase + f0 * 2;
+        a1.pos = ds.pos + f0;
+        a1.n_frame = ds.n_frame + f0;
+        a1.ssr = (unsigned long long)cfg.sample_rate * ICW_HZ_SCALE;
+        a1.scaled = cfg.frmod_scaled;
+        a1.w = c->w;
+        a1.w_pitch = w_pitch;
+        a1.info_phase = c->info_phase;
+        a1.info_nframe = c->info_nframe;
+        memcpy(a1.pc, c->pc, sizeof(a1.pc));
+        if (timing) hipEventRecord(c->ev[3 * b], st);
+        if (icw_launch_iir_state(&a1, N, cfg.iir_kahan, cfg.iir_subnorm_reject, st) != hipSuccess) return ICW_EDEVICE;
+        if (timing) hipEventRecord(c->ev[3 * b + 1], st);
+
+        IcwK2Args a2;
+        memset(&a2, 0, sizeof(a2));
+        a2.w = c->w;
+        a2.w_pitch = w_pitch;
+        a2.n_streams = count;
+        a2.T = T;
+        a2.n_chains = count * 4;
+        a2.info_phase = c->info_phase;
+        a2.info_nframe = c->info_nframe;
+        a2.ssr = a1.ssr;
+        a2.scaled = cfg.frmod_scaled;
+        a2.sample_rate = cfg.sample_rate;
+        a2.prog = c->d_prog;
+        a2.bus = ds.bus + f0 * ICW_N_INPUTS * 4;
+        a2.out = d_out + (size_t)t0 * osz;
+        a2.out_stride = dos;
+        if (d_pre) {
+            a2.pre = d_pre + (size_t)t0 * 2;
+            a2.pre_stride = (size_t)n_frames * 2;
+        }
+        a2.do_render = 1;
+        a2.clips = ds.clips + f0 * 2;
+        a2.peak_bits = ds.peak_bits + f0 * 2;
+        a2.rk = c->rk;
+        memcpy(a2.pc, c->pc, sizeof(a2.pc));
+        memcpy(a2.pd, c->pd, sizeof(a2.pd));
+        a2.d0 = c->d0;
+        if (icw_launch_output(&a2, N, cfg.iir_kahan, st) != hipSuccess) return ICW_EDEVICE;
+        if (timing) hipEventRecord(c->ev[3 * b + 2], st);
+    }
+    if (!dev) {
+        if (hipMemcpy2DAsync(out, out_stride, d_out, dos, dos, S, hipMemcpyDeviceToHost, st) != hipSuccess)
+            return ICW_EDEVICE;
+        if (d_pre && hipMemcpyAsync(dbg, d_pre, S * (size_t)n_frames * 2 * sizeof(double), hipMemcpyDeviceToHost, st) != hipSuccess)
+            return ICW_EDEVICE;
+        if (hipStreamSynchronize(st) != hipSuccess) return ICW_EDEVICE;
+    }
+    if (timing) {
+        if (hipStreamSynchronize(st) != hipSuccess) return ICW_EDEVICE;
+        double m1 = 0, m2 = 0;
+        for (int b = 0; b < n_blocks; ++b) {
+            float x = 0, y = 0;
+            hipEventElapsedTime(&x, c->ev[3 * b], c->ev[3 * b + 1]);
+            hipEventElapsedTime(&y, c->ev[3 * b + 1], c->ev[3 * b + 2]);
+            m1 += x;
+            m2 += y;
+        }
+        c->last_ms[0] = m1;
+        c->last_ms[1] = m2;
+        c->last_launches[0] = c->last_launches[1] = n_blocks;
+    }
+    return hipGetLastError() == hipSuccess ? ICW_OK : ICW_EDEVICE;
+}
+
+int icw_process_batch(icw_ctx *c, const void *in, size_t in_stride, void *out, size_t out_stride, int n_frames,
+                      unsigned flags, void *dbg, void *hip_stream)
+{
+    if (!c) return ICW_EINVAL;
+    return icw_process_streams(c, 0, c->n_streams, in, in_stride, out, out_stride, n_frames, flags, dbg, hip_stream);
+}
+
+int icw_synchronize(icw_ctx *c)
+{
+    if (!c) return ICW_EINVAL;
+    if (set_dev(c)) return ICW_EDEVICE;
+    return hipStreamSynchronize(c->stream) == hipSuccess ? ICW_OK : ICW_EDEVICE;
+}
+
+int icw_get_meters(icw_ctx *c, int s, int reset, icw_meters *m)
+{
+    if (!c || !m || s < 0 || s >= c->n_streams) return ICW_EINVAL;
+    std::lock_guard<std::mutex> lk(c->mu);
+    if (set_dev(c)) return ICW_EDEVICE;
+    uint32_t cl[2];
+    unsigned long long pb[2], sn[4];
+    bool ok = hipMemcpy(cl, c->st.clips + (size_t)s * 2, sizeof(cl), hipMemcpyDeviceToHost) == hipSuccess;
+    ok &= hipMemcpy(pb, c->st.peak_bits + (size_t)s * 2, sizeof(pb), hipMemcpyDeviceToHost) == hipSuccess;
+    ok &= hipMemcpy(sn, c->st.sncnt + (size_t)s * 4, sizeof(sn), hipMemcpyDeviceToHost) == hipSuccess;
+    if (!ok) return ICW_EDEVICE;
+    for (int ch = 0; ch < 2; ++ch) {
+        /* peak meter (sound_render.c:769-780): max over samples of 20*log10(|q|/hi) equals
+         * 20*log10(max|q| / hi) because the map is monotone; 0 -> SR_ZERO_SIGNAL_DB */
+        double mx;
+        memcpy(&mx, &pb[ch], 8);
+        double cv = mx / c->rk.hi;
+        cv = cv ? 20.0 * log10(cv) : ICW_SR_ZERO_SIGNAL_DB;
+        double &pv = c->peak_db[(size_t)s * 2 + ch];
+        if (cv > pv) pv = cv;
+        m->clips[ch] = cl[ch];
+        m->peak_db[ch] = pv;
+    }
+    m->desubnorm = sn[0] + sn[1] + sn[2] + sn[3];
+    if (reset) {
+        ok = hipMemset(c->st.clips + (size_t)s * 2, 0, sizeof(cl)) == hipSuccess;
+        ok &= hipMemset(c->st.peak_bits + (size_t)s * 2, 0, sizeof(pb)) == hipSuccess;
+        c->peak_db[(size_t)s * 2] = c->peak_db[(size_t)s * 2 + 1] = ICW_SR_ZERO_SIGNAL_DB;
+        if (!ok) return ICW_EDEVICE;
+    }
+    return ICW_OK;
+}
+
+int icw_n_frame(icw_ctx *c, int s, uint64_t *nf)
+{
+    if (!c || !nf || s < 0 || s >= c->n_streams) return ICW_EINVAL;
+    std::lock_guard<std::mutex> lk(c->mu);
+    if (set_dev(c)) return ICW_EDEVICE;
+    unsigned long long v = 0;
+    if (hipMemcpy(&v, c->st.n_frame + s, sizeof(v), hipMemcpyDeviceToHost) != hipSuccess) return ICW_EDEVICE;
+    *nf = v;
+    return ICW_OK;
+}
+
+/* canonical state blob: see DESIGN.md "Per-stream state" */
+struct IcwBlob {
+    uint64_t magic, n_frame;
+    int64_t pos, n_samples, n_fade_in, n_fade_out;
+    uint32_t hq_phase[2], nord, pad;
+    double hist[4][ICW_HIST_PITCH];
+    uint64_t sncnt[4];
+    double bus[ICW_N_INPUTS][4];
+};
+
+size_t icw_state_size(const icw_ctx *c) { return c ? sizeof(IcwBlob) : 0; }
+
+int icw_get_state(icw_ctx *c, int s, void *blob, size_t size)
+{
+    if (!c || !blob || size < sizeof(IcwBlob) || s < 0 || s >= c->n_streams) return ICW_EINVAL;
+    std::lock_guard<std::mutex> lk(c->mu);
+    if (set_dev(c)) return ICW_EDEVICE;
+    IcwBlob b;
+    memset(&b, 0, sizeof(b));
+    b.magic = 0x31574349ull;
+    b.nord = (uint32_t)c->nord;
+    long long fd[3];
+    bool ok = hipStreamSynchronize(c->stream) == hipSuccess;
+    ok &= hipMemcpy(&b.n_frame, c->st.n_frame + s, 8, hipMemcpyDeviceToHost) == hipSuccess;
+    ok &= hipMemcpy(&b.pos, c->st.pos + s, 8, hipMemcpyDeviceToHost) == hipSuccess;
+    ok &= hipMemcpy(fd, c->st.fade + (size_t)s * 3, sizeof(fd), hipMemcpyDeviceToHost) == hipSuccess;
+    ok &= hipMemcpy(b.hq_phase, c->st.hq_phase + (size_t)s * 2, 8, hipMemcpyDeviceToHost) == hipSuccess;
+    ok &= hipMemcpy(b.hist, c->st.hist + (size_t)s * 4 * ICW_HIST_PITCH, sizeof(b.hist), hipMemcpyDeviceToHost) == hipSuccess;
+    ok &= hipMemcpy(b.sncnt, c->st.sncnt + (size_t)s * 4, sizeof(b.sncnt), hipMemcpyDeviceToHost) == hipSuccess;
+    ok &= hipMemcpy(b.bus, c->st.bus + (size_t)s * ICW_N_INPUTS * 4, sizeof(b.bus), hipMemcpyDeviceToHost) == hipSuccess;
+    b.n_samples = fd[0]; b.n_fade_in = fd[1]; b.n_fade_out = fd[2];
+    if (!ok) return ICW_EDEVICE;
+    memcpy(blob, &b, sizeof(b));
+    return ICW_OK;
+}
+
+int icw_set_state(icw_ctx *c, int s, const void *blob, size_t size)
+{
+    if (!c || !blob || size < sizeof(IcwBlob) || s < 0 || s >= c->n_streams) return ICW_EINVAL;
+    IcwBlob b;
+    memcpy(&b, blob, sizeof(b));
+    if (b.magic != 0x31574349ull || b.nord != (uint32_t)c->nord) return ICW_EINVAL;
+    std::lock_guard<std::mutex> lk(c->mu);
+    if (set_dev(c)) return ICW_EDEVICE;
+    long long fd[3] = {b.n_samples, b.n_fade_in, b.n_fade_out};
+    bool ok = hipStreamSynchronize(c->stream) == hipSuccess;
+    ok &= hipMemcpy(c->st.n_frame + s, &b.n_frame, 8, hipMemcpyHostToDevice) == hipSuccess;
+    ok &= hipMemcpy(c->st.pos + s, &b.pos, 8, hipMemcpyHostToDevice) == hipSuccess;
+    ok &= hipMemcpy(c->st.fade + (size_t)s * 3, fd, sizeof(fd), hipMemcpyHostToDevice) == hipSuccess;
+    ok &= hipMemcpy(c->st.hq_phase + (size_t)s * 2, b.hq_phase, 8, hipMemcpyHostToDevice) == hipSuccess;
+    ok &= hipMemcpy(c->st.hist + (size_t)s * 4 * ICW_HIST_PITCH, b.hist, sizeof(b.hist), hipMemcpyHostToDevice) == hipSuccess;
+    ok &= hipMemcpy(c->st.sncnt + (size_t)s * 4, b.sncnt, sizeof(b.sncnt), hipMemcpyHostToDevice) == hipSuccess;
+    ok &= hipMemcpy(c->st.bus + (size_t)s * ICW_N_INPUTS * 4, b.bus, sizeof(b.bus), hipMemcpyHostToDevice) == hipSuccess;
+    return ok ? ICW_OK : ICW_EDEVICE;
+}
+
+int icw_last_timing(icw_ctx *c, double ms[2], int launches[2])
+{
+    if (!c || !ms || !launches) return ICW_EINVAL;
+    ms[0] = c->last_ms[0];
+    ms[1] = c->last_ms[1];
+    launches[0] = c->last_launches[0];
+    launches[1] = c->last_launches[1];
+    return ICW_OK;
+}
+
+}  /* extern "C" */

@@ -1,0 +1,607 @@
+/*
+ * icw_kernels.hip -- gfx950 (CDNA4) kernels of the in_cwave Hilbert -> modulator -> render path.
+ *
+ * Built with `-ffp-contract=off` and no fast-math; every floating-point expression below keeps
+ * the operand order of the reference so that results are bit-identical to the x86 SSE2 build
+ * of in_cwave (IEEE binary64, round-to-nearest, no FMA contraction, denormals preserved).
+ *
+ * Kernel roles (DESIGN.md "Kernels"):
+ *   icw_iir_state   one lane per DF-II chain (stream x channel x {I,Q} filter).  Runs the
+ *                   serial part of iir_rp_process_kahan (hblpf.c:1017-1054) -- the loop-back
+ *                   Kahan sum that produces the delay-line value w[n] -- with the delay line held
+ *                   in VGPRs as a compile-time-rotated ring (unrolled by the filter order N).
+ *                   Writes w[] per chain to HBM.  This is the latency-bound critical path.
+ *   icw_output      one thread per frame.  Everything that is NOT on the recurrence: the output
+ *                   Kahan sum y[n] = sum d_i z_i + d0*c_i z_i (hblpf.c:1029-1043) from the w
+ *                   window (frame-parallel), the fs/4 un-mix (lpf_hilbert_quad.c:129-156), the
+ *                   DSP graph (adv_modulator.c:637-751) and the elementwise render
+ *                   (sound_render.c:691-809, ROUND/flat).  Coalesced tile loads via LDS.
+ */
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdint.h>
+
+#include "../../include/icw.h"
+#include "icw_device.h"
+
+#pragma clang fp contract(off)
+
+#define ICW_PI (3.1415926535897932384626433832795029)
+#define ICW_SQRT2 (1.4142135623730950488016887242097)
+
+/* ------------------------------------------------------------------ input unpack --------- */
+/* xwave_reader.c:205-239 + unpack_lsb.h:53-125 (little-endian, exact conversions) */
+__device__ __forceinline__ double icw_unpack(const unsigned char *p, uint32_t fmt)
+{
+    switch (fmt) {
+    case ICW_FMT_I16: {
+        int v = (int)(short)((unsigned)p[0] | ((unsigned)p[1] << 8));
+        return (double)v;
+    }
+    case ICW_FMT_U8:
+        return 256.0 * (double)((signed char)(unsigned char)(p[0] - 0x80u));
+    case ICW_FMT_I24: {
+        int v = ((int)(((unsigned)p[0] << 8) | ((unsigned)p[1] << 16) | ((unsigned)p[2] << 24))) >> 8;
+        return ((double)v) / 256.0;
+    }
+    case ICW_FMT_I32: {
+        int v = (int)((unsigned)p[0] | ((unsigned)p[1] << 8) | ((unsigned)p[2] << 16) | ((unsigned)p[3] << 24));
+        return ((double)v) / 65536.0;
+    }
+    default: {
+        unsigned u = (unsigned)p[0] | ((unsigned)p[1] << 8) | ((unsigned)p[2] << 16) | ((unsigned)p[3] << 24);
+        return 32768.0 * (double)__uint_as_float(u);
+    }
+    }
+}
+
+/* fade factor of xwave_unpack_csample (xwave_reader.c:918-936); < 0 means "no fade" */
+__device__ __forceinline__ double icw_fade(long long ix, long long ns, long long fi, long long fo)
+{
+    double fade = -1.0;
+    if (ix < fi)
+        fade = ((double)ix) / ((double)fi);
+    else if (ix > ns - fo && ix < ns)
+        fade = ((double)(ns - ix)) / ((double)fo);
+    return fade;
+}
+
+/* ------------------------------------------------------------ IIR state kernel (K1) ----- */
+/* One unrolled step of the loop-back sum for sample J of an N-block.  The delay line lives in
+ * R[]: at step J the logical z_i (i = 0 most recent) is R[(J-1-i) mod N]; the new w is written
+ * to R[J], overwriting the oldest value.  All indices are compile-time constants. */
+template <int N, bool KAHAN, bool SUBN, int J>
+__device__ __forceinline__ void icw_iir_step(double (&R)[N], double xin, const double (&pc)[20],
+                                             unsigned &cnt)
+{
+    double S;
+    if (KAHAN) {
+        /* kahan_init(sample); i = 0 term first (hblpf.c:1017-1027) then i = 1..N-1 */
+        double t0 = R[(J - 1 + N) % N] * pc[0];
+        double C = 0.0, Y, T;
+        S = xin;
+        Y = t0 - C; T = S + Y; C = (T - S) - Y; S = T;
+#pragma unroll
+        for (int i = 1; i < N; ++i) {
+            double ti = R[(J - 1 - i + 2 * N) % N] * pc[i];
+            Y = ti - C; T = S + Y; C = (T - S) - Y; S = T;
+        }
+    } else {
+        /* baseline: sum_i = sample; sum_i += z_k * c_i (hblpf.c:898-913) */
+        S = xin;
+#pragma unroll
+        for (int i = 0; i < N; ++i) S += R[(J - 1 - i + 2 * N) % N] * pc[i];
+    }
+    if (SUBN) {
+        /* fabs(sum) < is_subnorm_reject, a BOOL == 1 -> threshold 1.0 (hblpf.c:915, 1046) */
+        const bool z = fabs(S) < 1.0;
+        cnt += z ? 1u : 0u;
+        S = z ? 0.0 : S;
+    }
+    R[J] = S;
+}
+
+/* input of the I (f=0) / Q (f=1) filter for Hilbert phase k (lpf_hilbert_quad.c:133-151):
+ *   I: {x, +0, -x, +0}   Q: {+0, -x, +0, x}   ==  k' = (k+f)&3: {x, +0, -x, +0}[k'] */
+__device__ __forceinline__ double icw_filter_in(double x, unsigned kq)
+{
+    return kq == 0 ? x : (kq == 2 ? -x : 0.0);
+}
+
+template <int N, int J>
+__device__ __forceinline__ void icw_store_hist(const double (&R)[N], double *hist, int g, int n_chains)
+{
+    /* after J steps of a block, logical z_i = R[(J-1-i) mod N] */
+#pragma unroll
+    for (int i = 0; i < N; ++i) hist[(size_t)g * ICW_HIST_PITCH + i] = R[(J - 1 - i + 2 * N) % N];
+}
+
+/* R[k] <- R[k+1 mod N]: one static rotation of the ring (moves only) */
+template <int N>
+__device__ __forceinline__ void icw_rotate1(double (&R)[N])
+{
+    const double r0 = R[0];
+#pragma unroll
+    for (int k = 0; k < N - 1; ++k) R[k] = R[k + 1];
+    R[N - 1] = r0;
+}
+
+/* After `rem` (< N) steps the logical order is R[(rem-1-i) mod N].  Rotating left by rem
+ * restores the block-start mapping R[(N-1-i)] without any runtime-indexed register access
+ * (which the compiler would otherwise demote to scratch). */
+template <int N>
+__device__ __forceinline__ void icw_normalise_ring(double (&R)[N], int rem)
+{
+#pragma unroll
+    for (int k = 1; k < N; ++k)
+        if (k <= rem) icw_rotate1<N>(R);
+}
+
+template <int N, int J0, bool KAHAN, bool SUBN>
+__device__ __forceinline__ void icw_block_steps(double (&R)[N], const double (&xv)[N], unsigned kq0,
+                                                const double (&pc)[20], unsigned &cnt, int lim)
+{
+    if constexpr (J0 < N) {
+        if (J0 < lim) {
+            icw_iir_step<N, KAHAN, SUBN, J0>(R, icw_filter_in(xv[J0], (kq0 + J0) & 3u), pc, cnt);
+            icw_block_steps<N, J0 + 1, KAHAN, SUBN>(R, xv, kq0, pc, cnt, lim);
+        }
+    }
+}
+
+template <int N, int J0, bool KAHAN, bool SUBN>
+__device__ __forceinline__ void icw_block_steps_full(double (&R)[N], const double (&xv)[N], unsigned kq0,
+                                                     const double (&pc)[20], unsigned &cnt)
+{
+    if constexpr (J0 < N) {
+        icw_iir_step<N, KAHAN, SUBN, J0>(R, icw_filter_in(xv[J0], (kq0 + J0) & 3u), pc, cnt);
+        icw_block_steps_full<N, J0 + 1, KAHAN, SUBN>(R, xv, kq0, pc, cnt);
+    }
+}
+
+/* Input prep (K0): unpack + fade each frame once (xwave_unpack_csample, xwave_reader.c:908-1001)
+ * into channel-planar doubles xd[s][ch][t].  Mono input writes plane 0 only; the right-channel
+ * chains then read plane 0, which is exactly the reference's reuse of `val` (xwave_reader.c:988). */
+__global__ __launch_bounds__(256) void icw_unpack_frames(IcwK0Args a)
+{
+    const int t = blockIdx.x * 256 + threadIdx.x;
+    const int s = blockIdx.y;
+    if (t >= a.T) return;
+    const unsigned char *fp = a.in + (size_t)s * a.in_stride + (size_t)t * a.fsz;
+    const long long ix = a.pos[s] + t;
+    const double fd = icw_fade(ix, a.fade[s * 3 + 0], a.fade[s * 3 + 1], a.fade[s * 3 + 2]);
+    double *xs = a.xd + (size_t)s * 2 * a.x_pitch;
+    double v = icw_unpack(fp, a.fmt);
+    if (fd >= 0.0) v *= fd;
+    xs[t] = v;
+    if (a.nch > 1) {
+        v = icw_unpack(fp + a.csz, a.fmt);
+        if (fd >= 0.0) v *= fd;
+        xs[a.x_pitch + t] = v;
+    }
+}
+
+template <int N>
+__device__ __forceinline__ void icw_load_x(double (&xv)[N], const double *xp)
+{
+#pragma unroll
+    for (int j = 0; j < N; ++j) xv[j] = xp[j];
+}
+
+template <int N, bool KAHAN, bool SUBN>
+__global__ __launch_bounds__(64) void icw_iir_state(IcwK1Args a)
+{
+    const int g = blockIdx.x * 64 + threadIdx.x;
+    if (g >= a.n_chains) return;
+    const int s = g >> 2, c = (g >> 1) & 1, f = g & 1;
+    const int n_chains = a.n_chains;
+    double pc[20];
+#pragma unroll
+    for (int i = 0; i < 20; ++i) pc[i] = a.pc[i];
+
+    double R[N];
+#pragma unroll
+    for (int i = 0; i < N; ++i) R[N - 1 - i] = a.hist[(size_t)g * ICW_HIST_PITCH + i];
+
+    const unsigned ph0 = a.hq_phase[s * 2 + c];
+    const double *xp = a.xd + ((size_t)s * 2 + (a.nch > 1 ? c : 0)) * a.x_pitch;
+    double *wrow = a.w + (size_t)g * a.w_pitch;
+    /* history rows [0, N): row j = z_{N-1-j} = R[j] */
+#pragma unroll
+    for (int j = 0; j < N; ++j) wrow[j] = R[j];
+
+    const int T = a.T;
+    unsigned cnt = 0;
+    int t = 0;
+    if (T >= N) {
+        /* software pipeline: the next block's inputs are in flight while this block computes */
+        double xv[N], xn[N];
+        icw_load_x<N>(xv, xp);
+        for (; t + N <= T; t += N) {
+            if (t + 2 * N <= T) icw_load_x<N>(xn, xp + t + N);
+            const unsigned kq0 = (ph0 + (unsigned)t + (unsigned)f) & 3u;
+            icw_block_steps_full<N, 0, KAHAN, SUBN>(R, xv, kq0, pc, cnt);
+            double *wo = wrow + N + t;
+#pragma unroll
+            for (int j = 0; j < N; ++j) wo[j] = R[j];
+#pragma unroll
+            for (int j = 0; j < N; ++j) xv[j] = xn[j];
+        }
+    }
+    const int rem = T - t;
+    if (rem > 0) {
+        double xv[N];
+#pragma unroll
+        for (int j = 0; j < N; ++j) xv[j] = (j < rem) ? xp[t + j] : 0.0;
+        const unsigned kq0 = (ph0 + (unsigned)t + (unsigned)f) & 3u;
+        icw_block_steps<N, 0, KAHAN, SUBN>(R, xv, kq0, pc, cnt, rem);
+        double *wo = wrow + N + t;
+#pragma unroll
+        for (int j = 0; j < N; ++j)
+            if (j < rem) wo[j] = R[j];
+        icw_normalise_ring<N>(R, rem);
+    }
+    icw_store_hist<N, 0>(R, a.hist, g, n_chains);
+    a.sncnt[g] += cnt;
+    if (f == 0) {
+        a.info_phase[s * 2 + c] = ph0;
+        a.hq_phase[s * 2 + c] = (ph0 + (unsigned)T) & 3u;
+        if (c == 0) {
+            a.pos[s] += T;
+            const unsigned long long n0 = a.n_frame[s];
+            a.info_nframe[s] = n0;
+            a.n_frame[s] = a.scaled ? (n0 + (unsigned long long)T) % a.ssr : n0 + (unsigned long long)T;
+        }
+    }
+}
+
+/* ------------------------------------------------------------- output kernel (K2) ------- */
+struct IcwLR { double lre, lim, rre, rim; };
+
+/* output Kahan sum of iir_rp_process_kahan (hblpf.c:1029-1043) for the sample whose delay line
+ * is z_i = win[N-1-i] (win = w[t-N .. t-1]); baseline form (hblpf.c:898-925) needs w[t]=win[N] */
+template <int N, bool KAHAN>
+__device__ __forceinline__ double icw_iir_out(const double *win, const double (&pc)[20],
+                                              const double (&pd)[20], double d0)
+{
+    if (KAHAN) {
+        double z = win[N - 1];
+        double t0 = z * pc[0];
+        double S = z * pd[0], C = 0.0, Y, T;
+        double x = t0 * d0;
+        Y = x - C; T = S + Y; C = (T - S) - Y; S = T;
+#pragma unroll
+        for (int i = 1; i < N; ++i) {
+            z = win[N - 1 - i];
+            const double ti = z * pc[i];
+            x = z * pd[i];
+            Y = x - C; T = S + Y; C = (T - S) - Y; S = T;
+            x = ti * d0;
+            Y = x - C; T = S + Y; C = (T - S) - Y; S = T;
+        }
+        return S;
+    } else {
+        double so = 0.0;
+#pragma unroll
+        for (int i = 0; i < N; ++i) so += win[N - 1 - i] * pd[i];
+        return win[N] * d0 + so;
+    }
+}
+
+__device__ __forceinline__ double icw_master(int tout, double re, double im)
+{
+    switch (tout) {
+    case ICW_S_RE: return re;
+    case ICW_S_IM: return im;
+    case ICW_S_ADD_REIM: return (re + im) / ICW_SQRT2;
+    case ICW_S_SUB_REIM: return (re - im) / ICW_SQRT2;
+    }
+    return 0.0;
+}
+
+__device__ __forceinline__ void icw_getreg(const IcwLR (&R)[ICW_MAX_REGS], int r, IcwLR &v)
+{
+    switch (r) {
+    case 0: v = R[0]; break;
+    case 1: v = R[1]; break;
+    case 2: v = R[2]; break;
+    case 3: v = R[3]; break;
+    case 4: v = R[4]; break;
+    case 5: v = R[5]; break;
+    case 6: v = R[6]; break;
+    default: v = R[7]; break;
+    }
+}
+
+__device__ __forceinline__ void icw_setreg(IcwLR (&R)[ICW_MAX_REGS], int r, const IcwLR &v)
+{
+    switch (r) {
+    case 0: R[0] = v; break;
+    case 1: R[1] = v; break;
+    case 2: R[2] = v; break;
+    case 3: R[3] = v; break;
+    case 4: R[4] = v; break;
+    case 5: R[5] = v; break;
+    case 6: R[6] = v; break;
+    default: R[7] = v; break;
+    }
+}
+
+/* rotate (re,im) by e^{j phi} given cos/sin (adv_modulator.c:546-547, 576-577) */
+__device__ __forceinline__ void icw_rot(double re, double im, double cs, double sn, double &ore, double &oim)
+{
+    ore = re * cs - im * sn;
+    oim = re * sn + im * cs;
+}
+
+/* sound_render_value for ROUND render + flat shaper (sound_render.c:691-809): elementwise */
+__device__ __forceinline__ int icw_render_round(double input, const IcwRenderK &k, unsigned &clips, double &pk)
+{
+    input = (input * k.norm_mul) - 0.0;           /* prev_ns_err == 0.0 for the flat shaper */
+    double q = input + (0.0 * k.dth_mul);         /* rnd_dth == 0.0 for ROUND */
+    int delta;
+    if (q < 0.0) { q -= k.round_offset; delta = k.sign_delta; }
+    else { q += k.round_offset; delta = 0; }
+    const double aq = fabs(q);
+    pk = aq > pk ? aq : pk;
+    if (q >= k.hi) { q = k.hi - 1.0; ++clips; }
+    if (q <= k.lo) { q = k.lo + 1.0; ++clips; }
+    /* x86 cvttsd2si semantics: NaN -> INT_MIN ("integer indefinite") */
+    int v = isnan(q) ? (int)0x80000000 : (int)q;
+    return (v + delta) << k.norm_shift;
+}
+
+template <int N, bool KAHAN>
+__global__ __launch_bounds__(ICW_K2_TILE) void icw_output(IcwK2Args a)
+{
+    __shared__ double lw[4][ICW_K2_TILE + 24];
+    __shared__ unsigned red_clip[2][ICW_K2_TILE / 64];
+    __shared__ double red_pk[2][ICW_K2_TILE / 64];
+    const int s = blockIdx.y;
+    const int t0 = blockIdx.x * ICW_K2_TILE;
+    const int tl = threadIdx.x;
+    const int t = t0 + tl;
+    const int T = a.T;
+    const int nrow = min(ICW_K2_TILE, T - t0) + N + (KAHAN ? 0 : 1);
+
+    /* stage the w windows of the stream's 4 chains: rows [t0, t0+nrow) */
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        const double *src = a.w + (size_t)(s * 4 + c) * a.w_pitch + t0;
+        for (int r = tl; r < nrow; r += ICW_K2_TILE) lw[c][r] = src[r];
+    }
+    __syncthreads();
+
+    double pc[20], pd[20];
+#pragma unroll
+    for (int i = 0; i < 20; ++i) { pc[i] = a.pc[i]; pd[i] = a.pd[i]; }
+
+    unsigned clip_l = 0, clip_r = 0;
+    double pk_l = 0.0, pk_r = 0.0;
+    if (t < T) {
+        /* filter outputs of the 4 chains (L-I, L-Q, R-I, R-Q) */
+        double y[4];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) y[c] = icw_iir_out<N, KAHAN>(&lw[c][tl], pc, pd, a.d0);
+
+        /* fs/4 un-mix (lpf_hilbert_quad.c:129-156) */
+        IcwLR in;
+        {
+            double oI[2], oQ[2];
+#pragma unroll
+            for (int ch = 0; ch < 2; ++ch) {
+                const double yi = y[ch * 2], yq = y[ch * 2 + 1];
+                const unsigned k = (a.info_phase[s * 2 + ch] + (unsigned)t) & 3u;
+                switch (k) {
+                case 0: oI[ch] = yi * 2.0; oQ[ch] = yq * 2.0; break;
+                case 1: oI[ch] = -yq * 2.0; oQ[ch] = yi * 2.0; break;
+                case 2: oI[ch] = -yi * 2.0; oQ[ch] = -yq * 2.0; break;
+                default: oI[ch] = yq * 2.0; oQ[ch] = -yi * 2.0; break;
+                }
+            }
+            in.lre = oI[0]; in.lim = oQ[0]; in.rre = oI[1]; in.rim = oQ[1];
+        }
+
+        /* modulator frame counter -> norm_omega (adv_modulator.c:611-625) */
+        const unsigned long long n0 = a.info_nframe[s];
+        double omega;
+        if (a.scaled) {
+            const unsigned long long n = (t == 0) ? n0 : (n0 + (unsigned long long)t) % a.ssr;
+            omega = (2.0 * ICW_PI) * ((double)n) / ((double)a.ssr);
+        } else {
+            omega = (2.0 * ICW_PI) * ((double)(n0 + (unsigned long long)t)) / (double)a.sample_rate;
+        }
+
+        /* DSP list (adv_modulator.c:637-751) */
+        const IcwProg *P = a.prog;
+        IcwLR R[ICW_MAX_REGS];
+        R[0] = in;
+        for (int r = 1; r < ICW_MAX_REGS; ++r) R[r].lre = R[r].lim = R[r].rre = R[r].rim = 0.0;
+        for (int r = 0; r < P->n_persist; ++r) {
+            const double *b = a.bus + ((size_t)s * ICW_N_INPUTS + P->persist_slot[r]) * 4;
+            IcwLR v; v.lre = b[0]; v.lim = b[1]; v.rre = b[2]; v.rim = b[3];
+            icw_setreg(R, P->persist_reg[r], v);
+        }
+        double lOut = 0.0, rOut = 0.0;
+        for (int oi = 0; oi < P->n_ops; ++oi) {
+            const IcwOp &op = P->ops[oi];
+            IcwLR d;
+            if (P->bypass) {
+                d = in;
+            } else {
+                d.lre = d.lim = d.rre = d.rim = 0.0;
+                for (int k = 0; k < op.n_in; ++k) {
+                    IcwLR v;
+                    icw_getreg(R, op.in_reg[k], v);
+                    d.lre += v.lre; d.lim += v.lim; d.rre += v.rre; d.rim += v.rim;
+                }
+            }
+            double xt;
+            switch (op.xch) {
+            case ICW_XCH_SWAP:
+                xt = d.lre; d.lre = d.rre; d.rre = xt;
+                xt = d.lim; d.lim = d.rim; d.rim = xt;
+                break;
+            case ICW_XCH_LEFTONLY: d.rre = d.lre; d.rim = d.lim; break;
+            case ICW_XCH_RIGHTONLY: d.lre = d.rre; d.lim = d.rim; break;
+            case ICW_XCH_MIXLR:
+                d.lre = d.rre = (d.lre + d.rre) / 2.0;
+                d.lim = d.rim = (d.lim + d.rim) / 2.0;
+                break;
+            default: break;
+            }
+            if (op.iqinv[0]) { xt = d.lre; d.lre = d.lim; d.lim = xt; }
+            if (op.iqinv[1]) { xt = d.rre; d.rre = d.rim; d.rim = xt; }
+            d.lre *= op.gain[0]; d.lim *= op.gain[0];
+            d.rre *= op.gain[1]; d.rim *= op.gain[1];
+            IcwLR o;
+            switch (op.mode) {
+            case ICW_MODE_MASTER:
+                lOut = icw_master(op.tout[0], d.lre, d.lim);
+                rOut = icw_master(op.tout[1], d.rre, d.rim);
+                break;
+            case ICW_MODE_SHIFT: {
+                double cs, sn;
+                if (op.act[0]) {
+                    const double ph = fmod(omega * op.f[0], 2.0 * ICW_PI);
+                    sincos(ph, &sn, &cs);
+                    if (op.neg[0]) sn = -sn;
+                    icw_rot(d.lre, d.lim, cs, sn, o.lre, o.lim);
+                } else { o.lre = d.lre; o.lim = d.lim; }
+                if (op.act[1]) {
+                    const double ph = fmod(omega * op.f[1], 2.0 * ICW_PI);
+                    sincos(ph, &sn, &cs);
+                    if (op.neg[1]) sn = -sn;
+                    icw_rot(d.rre, d.rim, cs, sn, o.rre, o.rim);
+                } else { o.rre = d.rre; o.rim = d.rim; }
+                icw_setreg(R, op.out_reg, o);
+                break;
+            }
+            case ICW_MODE_PM: {
+                double cs, sn;
+                if (op.act[0]) {
+                    const double ph = fmod(omega * op.f[0], 2.0 * ICW_PI);
+                    const double psi = op.lp[0] * (sin(ph + op.pp[0]) + op.fa[0]);
+                    sincos(psi, &sn, &cs);
+                    icw_rot(d.lre, d.lim, cs, sn, o.lre, o.lim);
+                } else { o.lre = d.lre; o.lim = d.lim; }
+                if (op.act[1]) {
+                    const double ph = fmod(omega * op.f[1], 2.0 * ICW_PI);
+                    const double psi = op.lp[1] * (sin(ph + op.pp[1]) + op.fa[1]);
+                    sincos(psi, &sn, &cs);
+                    icw_rot(d.rre, d.rim, cs, sn, o.rre, o.rim);
+                } else { o.rre = d.rre; o.rim = d.rim; }
+                icw_setreg(R, op.out_reg, o);
+                break;
+            }
+            default: /* MIX */
+                icw_setreg(R, op.out_reg, d);
+                break;
+            }
+        }
+
+        if (a.pre) {
+            double *p = a.pre + (size_t)s * a.pre_stride + (size_t)t * 2;
+            p[0] = lOut; p[1] = rOut;
+        }
+        if (a.do_render) {
+            const int vl = icw_render_round(lOut, a.rk, clip_l, pk_l);
+            const int vr = icw_render_round(rOut, a.rk, clip_r, pk_r);
+            unsigned char *o = a.out + (size_t)s * a.out_stride;
+            if (a.rk.is24) {
+                unsigned char *q = o + (size_t)t * 6;
+                q[0] = (unsigned char)vl; q[1] = (unsigned char)(vl >> 8); q[2] = (unsigned char)(vl >> 16);
+                q[3] = (unsigned char)vr; q[4] = (unsigned char)(vr >> 8); q[5] = (unsigned char)(vr >> 16);
+            } else {
+                const unsigned pk = ((unsigned)vl & 0xffffu) | ((unsigned)vr << 16);
+                *(unsigned *)(o + (size_t)t * 4) = pk;
+            }
+        }
+        /* persistent bus write-back from the block's last frame */
+        if (t == T - 1) {
+            double *b0 = a.bus + (size_t)s * ICW_N_INPUTS * 4;
+            b0[0] = in.lre; b0[1] = in.lim; b0[2] = in.rre; b0[3] = in.rim;
+            for (int k = 0; k < P->n_wb; ++k) {
+                IcwLR v;
+                icw_getreg(R, P->wb_reg[k], v);
+                double *b = b0 + P->wb_slot[k] * 4;
+                b[0] = v.lre; b[1] = v.lim; b[2] = v.rre; b[3] = v.rim;
+            }
+        }
+    }
+
+    if (a.do_render) {
+        /* per-workgroup meters: wave reduce, LDS, one atomic per stream/channel */
+        for (int off = 32; off > 0; off >>= 1) {
+            clip_l += __shfl_xor(clip_l, off);
+            clip_r += __shfl_xor(clip_r, off);
+            pk_l = fmax(pk_l, __shfl_xor(pk_l, off));
+            pk_r = fmax(pk_r, __shfl_xor(pk_r, off));
+        }
+        const int wv = tl >> 6;
+        if ((tl & 63) == 0) {
+            red_clip[0][wv] = clip_l; red_clip[1][wv] = clip_r;
+            red_pk[0][wv] = pk_l; red_pk[1][wv] = pk_r;
+        }
+        __syncthreads();
+        if (tl < 2) {
+            unsigned cs = 0; double pm = 0.0;
+            for (int i = 0; i < ICW_K2_TILE / 64; ++i) { cs += red_clip[tl][i]; pm = fmax(pm, red_pk[tl][i]); }
+            if (cs) atomicAdd(&a.clips[s * 2 + tl], cs);
+            if (pm > 0.0) atomicMax(&a.peak_bits[s * 2 + tl], (unsigned long long)__double_as_longlong(pm));
+        }
+    }
+}
+
+/* ---------------------------------------------------------------- launch wrappers ------- */
+template <int N, bool K, bool S>
+static hipError_t launch_k1_t(const IcwK1Args &a, hipStream_t st)
+{
+    const int blocks = (a.n_chains + 63) / 64;
+    hipLaunchKernelGGL((icw_iir_state<N, K, S>), dim3(blocks), dim3(64), 0, st, a);
+    return hipGetLastError();
+}
+
+template <int N>
+static hipError_t launch_k1_n(const IcwK1Args &a, bool kahan, bool subn, hipStream_t st)
+{
+    if (kahan) return subn ? launch_k1_t<N, true, true>(a, st) : launch_k1_t<N, true, false>(a, st);
+    return subn ? launch_k1_t<N, false, true>(a, st) : launch_k1_t<N, false, false>(a, st);
+}
+
+extern "C" hipError_t icw_launch_unpack(const IcwK0Args *a, hipStream_t st)
+{
+    dim3 grid((a->T + 255) / 256, a->n_streams);
+    hipLaunchKernelGGL(icw_unpack_frames, grid, dim3(256), 0, st, *a);
+    return hipGetLastError();
+}
+
+extern "C" hipError_t icw_launch_iir_state(const IcwK1Args *a, int nord, int kahan, int subn, hipStream_t st)
+{
+    switch (nord) {
+    case 15: return launch_k1_n<15>(*a, kahan, subn, st);
+    case 18: return launch_k1_n<18>(*a, kahan, subn, st);
+    case 19: return launch_k1_n<19>(*a, kahan, subn, st);
+    case 20: return launch_k1_n<20>(*a, kahan, subn, st);
+    }
+    return hipErrorInvalidValue;
+}
+
+template <int N, bool K>
+static hipError_t launch_k2_t(const IcwK2Args &a, hipStream_t st)
+{
+    dim3 grid((a.T + ICW_K2_TILE - 1) / ICW_K2_TILE, a.n_streams);
+    hipLaunchKernelGGL((icw_output<N, K>), grid, dim3(ICW_K2_TILE), 0, st, a);
+    return hipGetLastError();
+}
+
+extern "C" hipError_t icw_launch_output(const IcwK2Args *a, int nord, int kahan, hipStream_t st)
+{
+    switch (nord) {
+    case 15: return kahan ? launch_k2_t<15, true>(*a, st) : launch_k2_t<15, false>(*a, st);
+    case 18: return kahan ? launch_k2_t<18, true>(*a, st) : launch_k2_t<18, false>(*a, st);
+    case 19: return kahan ? launch_k2_t<19, true>(*a, st) : launch_k2_t<19, false>(*a, st);
+    case 20: return kahan ? launch_k2_t<20, true>(*a, st) : launch_k2_t<20, false>(*a, st);
+    }
+    return hipErrorInvalidValue;
+}

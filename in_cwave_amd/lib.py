@@ -1,0 +1,141 @@
+"""Loader for the in-tree HIP library in_cwave_amd/libicw.so and a thin Pythonic wrapper of the
+C ABI (include/icw.h).  There is no CPU fallback: if the library or a HIP device is missing the
+calls raise."""
+import ctypes as C
+import os
+from pathlib import Path
+
+import numpy as np
+
+from . import abi
+
+LIB_PATH = Path(__file__).resolve().parent / "libicw.so"
+_lib = None
+
+
+class IcwError(RuntimeError):
+    pass
+
+
+def load():
+    global _lib
+    if _lib is None:
+        if not LIB_PATH.exists():
+            raise IcwError(f"{LIB_PATH} is missing: run __graft_entry__.build() (no CPU fallback exists)")
+        lib = C.CDLL(str(LIB_PATH))
+        for name, (res, args) in abi.SIGNATURES.items():
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = lib
+    return _lib
+
+
+def _check(rc, what):
+    if rc != abi.OK:
+        msg = load().icw_strerror(rc).decode()
+        raise IcwError(f"{what} failed: {rc} ({msg})")
+
+
+def _ptr(x):
+    """device/host pointer of a numpy array, torch tensor or int"""
+    if x is None:
+        return None
+    if isinstance(x, int):
+        return x
+    if hasattr(x, "data_ptr"):
+        return x.data_ptr()
+    if isinstance(x, np.ndarray):
+        return x.ctypes.data
+    raise TypeError(type(x))
+
+
+class Context:
+    """One icw_ctx: n_streams streams sharing a config and a DSP list, state resident in HBM."""
+
+    def __init__(self, cfg, nodes, n_streams, device=-1):
+        lib = load()
+        self._lib = lib
+        arr = (abi.Node * max(1, len(nodes)))(*nodes) if nodes else (abi.Node * 1)()
+        h = C.c_void_p()
+        acc = C.c_int()
+        _check(lib.icw_create(C.byref(cfg), arr, len(nodes), n_streams, device, C.byref(h), C.byref(acc)),
+               "icw_create")
+        self.h = h
+        self.accepted = bool(acc.value)
+        self.cfg = cfg
+        self.n_streams = n_streams
+        self.render_size = lib.icw_render_size(h)
+        self.fsz = abi.FMT_BYTES[cfg.in_format] * cfg.in_channels
+
+    def close(self):
+        if self.h:
+            self._lib.icw_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def stream_init(self, first=0, count=None):
+        _check(self._lib.icw_stream_init(self.h, first, self.n_streams - first if count is None else count),
+               "icw_stream_init")
+
+    def stream_open(self, s, n_samples, fade_in_ms=0, fade_out_ms=0, sec_align=0, clr_nframe=0, clr_hilb=0):
+        _check(self._lib.icw_stream_open(self.h, s, n_samples, fade_in_ms, fade_out_ms, sec_align,
+                                         clr_nframe, clr_hilb), "icw_stream_open")
+
+    def process(self, inp, n_frames, first=0, count=None, want_pre=False):
+        """Host numpy path: inp uint8 [count, >= n_frames*fsz]; returns (out uint8 [count, n_frames*2*rs],
+        pre float64 [count, n_frames, 2] or None)."""
+        count = self.n_streams - first if count is None else count
+        inp = np.ascontiguousarray(inp)
+        assert inp.dtype == np.uint8 and inp.shape[0] == count and inp.shape[1] >= n_frames * self.fsz
+        osz = 2 * self.render_size
+        out = np.zeros((count, n_frames * osz), dtype=np.uint8)
+        pre = np.zeros((count, n_frames, 2), dtype=np.float64) if want_pre else None
+        flags = abi.F_DEBUG_PRE if want_pre else 0
+        _check(self._lib.icw_process_streams(self.h, first, count, _ptr(inp), inp.strides[0], _ptr(out),
+                                             out.strides[0], n_frames, flags, _ptr(pre), None),
+               "icw_process_streams")
+        return out, pre
+
+    def process_device(self, d_in, in_stride, d_out, out_stride, n_frames, first=0, count=None,
+                       timing=False, hip_stream=None):
+        count = self.n_streams - first if count is None else count
+        flags = abi.F_DEVICE_PTRS | (abi.F_TIMING if timing else 0)
+        _check(self._lib.icw_process_streams(self.h, first, count, _ptr(d_in), in_stride, _ptr(d_out),
+                                             out_stride, n_frames, flags, None, hip_stream),
+               "icw_process_streams")
+
+    def synchronize(self):
+        _check(self._lib.icw_synchronize(self.h), "icw_synchronize")
+
+    def meters(self, s, reset=False):
+        m = abi.Meters()
+        _check(self._lib.icw_get_meters(self.h, s, 1 if reset else 0, C.byref(m)), "icw_get_meters")
+        return {"clips": (m.clips[0], m.clips[1]), "peak_db": (m.peak_db[0], m.peak_db[1]),
+                "desubnorm": m.desubnorm}
+
+    def n_frame(self, s):
+        v = C.c_uint64()
+        _check(self._lib.icw_n_frame(self.h, s, C.byref(v)), "icw_n_frame")
+        return v.value
+
+    def get_state(self, s):
+        n = self._lib.icw_state_size(self.h)
+        buf = (C.c_uint8 * n)()
+        _check(self._lib.icw_get_state(self.h, s, buf, n), "icw_get_state")
+        return bytes(buf)
+
+    def set_state(self, s, blob):
+        buf = (C.c_uint8 * len(blob)).from_buffer_copy(blob)
+        _check(self._lib.icw_set_state(self.h, s, buf, len(blob)), "icw_set_state")
+
+    def last_timing(self):
+        ms = (C.c_double * 2)()
+        n = (C.c_int * 2)()
+        _check(self._lib.icw_last_timing(self.h, ms, n), "icw_last_timing")
+        return (ms[0], ms[1]), (n[0], n[1])

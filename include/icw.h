@@ -1,0 +1,203 @@
+/*
+ * icw.h -- C ABI of in_cwave_amd: the MI355X-native Hilbert -> modulator-graph -> render
+ * hot path of rat-and-catcher/in_cwave (V2.4.4), batched over many independent streams.
+ *
+ * Plain C types only (no torch, no HIP types).  Every entry point returns an int status:
+ * ICW_OK (0) or a negative ICW_E* code -- an improvement over the reference's overloaded 0
+ * return of amod_process_samples (adv_modulator.c:601-602), which cannot tell EOF from error.
+ *
+ * Reference interfaces replaced (file:line into the reference tree):
+ *   icw_process_batch / icw_process_block
+ *        <- int amod_process_samples(char *buf, MOD_CONTEXT *mc)      in_cwave.h:648,
+ *           adv_modulator.c:587-763 (one block: n_frame -> unpack+Hilbert -> graph -> render)
+ *   icw_create(cfg, nodes)     <- mod_context_init (in_cwave.c:46-80) + amod_init
+ *                                 (adv_modulator.c:216-331: head==Master validation, L/R locks)
+ *   icw_stream_open            <- mod_context_fopen (in_cwave.c:207-236) + the fade /
+ *                                 sec_align arithmetic of xwave_reader_create
+ *                                 (xwave_reader.c:688-725)
+ *   icw_stream_reset_hilbert   <- mod_context_reset_hilbert / hq_rp_reset (lpf_hilbert_quad.c:160-165)
+ *   icw_stream_reset_framecnt  <- mod_context_reset_framecnt (in_cwave.c:287-296)
+ *   icw_get_meters             <- amod_get_clips_peaks (adv_modulator.c:445-465) and
+ *                                 mod_context_get_desubnorm_counter (in_cwave.c:300-321)
+ *   icw_render_size            <- sound_render_size (sound_render.c:684-687)
+ *
+ * Threading: a context is driven by one host thread at a time (as MOD_CONTEXT is driven by one
+ * decode thread, playback.c:567-671); parameters are snapshotted per call (block granularity,
+ * SURVEY 3.4).  Different contexts may be used concurrently from different threads / devices.
+ */
+#ifndef ICW_H_
+#define ICW_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- status codes ---- */
+#define ICW_OK              0
+#define ICW_EINVAL         -1   /* bad argument / unsupported configuration */
+#define ICW_ENOMEM         -2   /* device or host allocation failed */
+#define ICW_EDEVICE        -3   /* HIP runtime error */
+#define ICW_EGRAPH         -4   /* DSP list rejected (no unique Master at head, bad plug ...) */
+#define ICW_EUNSUPPORTED   -5   /* valid for the reference, not (yet) on this path */
+
+/* ---- constants mirrored from in_cwave.h / sound_render.h / lpf_hilbert_quad.h ---- */
+#define ICW_N_INPUTS        27  /* in[0], A[1]..Z[26]             in_cwave.h:244 */
+#define ICW_MAX_IIR_ORDER   20  /* largest canned HB LPF order    hblpf.c:740-820 */
+#define ICW_MAX_NS_TAPS     20  /* largest noise shaper            sound_render.c:75-235 */
+#define ICW_HZ_SCALE        1000u
+#define ICW_MAX_FS_SRC      2000000u
+
+/* node modes (NODE_DSP.mode, in_cwave.h:283-287) */
+#define ICW_MODE_MASTER 0
+#define ICW_MODE_SHIFT  1
+#define ICW_MODE_PM     2
+#define ICW_MODE_MIX    3
+/* master output conversions (in_cwave.h:152-155) */
+#define ICW_S_ADD_REIM  0
+#define ICW_S_SUB_REIM  1
+#define ICW_S_RE        2
+#define ICW_S_IM        3
+/* channel exchange (in_cwave.h:186-193) */
+#define ICW_XCH_NORMAL    0
+#define ICW_XCH_SWAP      1
+#define ICW_XCH_LEFTONLY  2
+#define ICW_XCH_RIGHTONLY 3
+#define ICW_XCH_MIXLR     4
+/* real (RWAVE/WAV) input sample formats (HRW_FMT_*, in_cwave.h:318-323) */
+#define ICW_FMT_U8   0
+#define ICW_FMT_I16  1
+#define ICW_FMT_I24  2
+#define ICW_FMT_I32  3
+#define ICW_FMT_F32  4
+/* render (sound_render.h:54-84) */
+#define ICW_QUANTZ_MID_TREAD 0
+#define ICW_QUANTZ_MID_RISER 1
+#define ICW_RENDER_ROUND 0
+#define ICW_RENDER_RPDF  1
+#define ICW_RENDER_TPDF  2
+#define ICW_RENDER_STPDF 3
+#define ICW_RENDER_GAUSS 4
+#define ICW_NSHAPE_FLAT  0
+#define ICW_NSHAPE_MEW44 2
+#define ICW_NSHAPE_MAX   17
+/* default render seeds (in_cwave.c:69-70) */
+#define ICW_SEED_LEFT   0x13579BDFu
+#define ICW_SEED_RIGHT  0x479B22ABu
+#define ICW_SR_ZERO_SIGNAL_DB (-555.0)
+
+/* One DSP node (NODE_DSP, in_cwave.h:273-287, without list links / name).  Channel arrays are
+ * [0]=left, [1]=right.  The list is passed head first: nodes[0] must be the Master. */
+typedef struct icw_node {
+    int32_t  mode;                    /* ICW_MODE_* */
+    int32_t  n_out;                   /* output bus slot 1..26 (SHIFT/PM/MIX) */
+    double   gain[2];                 /* l_gain / r_gain */
+    uint8_t  inputs[ICW_N_INPUTS];    /* bus slots mixed into the node */
+    uint8_t  pad_[1];
+    int32_t  xch_mode;                /* ICW_XCH_* */
+    int32_t  iq_invert[2];            /* l_iq_invert / r_iq_invert */
+    int32_t  tout[2];                 /* MASTER: ICW_S_* */
+    double   fr_shift[2];             /* SHIFT: signed shift, Hz */
+    int32_t  is_shift[2];
+    double   pm_freq[2], pm_phase[2], pm_level[2], pm_angle[2];   /* PM */
+    int32_t  is_pm[2];
+    /* L/R locks applied at icw_create exactly as amod_init does (adv_modulator.c:247-293) */
+    int32_t  lock_gain, lock_shift, sign_lock_shift;
+    int32_t  lock_freq, lock_phase, lock_level, lock_angle;
+    int32_t  reserved_;
+} icw_node;
+
+/* SR_VCONFIG (sound_render.h:145-153) */
+typedef struct icw_render_cfg {
+    double   dth_bits;
+    uint32_t quantz_type, render_type, nshape_type, sign_bits16, sign_bits24;
+} icw_render_cfg;
+
+/* Context-wide configuration (IN_CWAVE_CFG hot-path fields, in_cwave.h:435-459) */
+typedef struct icw_config {
+    uint32_t sample_rate;         /* Hz, <= ICW_MAX_FS_SRC */
+    uint32_t in_format;           /* ICW_FMT_* */
+    uint32_t in_channels;         /* 1 (mono: R fed with L) or >= 2 (channels > 2 skipped) */
+    uint32_t hilbert_type;        /* IX_LPF_HILB_TYPE0..5 (default 1) */
+    int32_t  iir_kahan;           /* IIR_SUM_KAHAN (default 1) */
+    int32_t  iir_subnorm_reject;  /* IIR_SUBN_ZERO (default 1) */
+    int32_t  frmod_scaled;        /* FRMOD_SCALED (default 1) */
+    int32_t  need24bits;          /* NEED24BITS */
+    int32_t  bypass_list;         /* am.is_bypass_list */
+    uint32_t seed_left, seed_right;
+    icw_render_cfg render;
+} icw_config;
+
+/* Per-stream meters (the reference keeps them global in `am`, adv_modulator.c:54-56). */
+typedef struct icw_meters {
+    uint32_t clips[2];            /* InterlockedIncrement'ed clip counters, sound_render.c:782-795 */
+    double   peak_db[2];          /* max 20*log10(|q|/hi_bound), SR_ZERO_SIGNAL_DB if silent */
+    uint64_t desubnorm;           /* sum of the 4 IIR subnorm_cnt of the stream, hblpf.c:918/1049 */
+} icw_meters;
+
+typedef struct icw_ctx icw_ctx;
+
+/* flags for icw_process_batch */
+#define ICW_F_DEVICE_PTRS  1u     /* in/out are device pointers already resident in HBM */
+#define ICW_F_DEBUG_PRE    2u     /* also write the 2 pre-render doubles/frame to dbg (tests) */
+#define ICW_F_TIMING       4u     /* time the kernels with HIP events (icw_last_timing) */
+
+/* Create a context for n_streams streams on HIP device `device` (-1: current device).
+ * The DSP list is normalised exactly as amod_init (adv_modulator.c:216-331) does; a list it
+ * would reject (no Master at head, 2 Masters, bad mode) is replaced by the default Master
+ * (S_ADD_REIM, gain 0.8, input `in`) and *accepted is set to 0, like amod_init's return. */
+int icw_create(const icw_config *cfg, const icw_node *nodes, int n_nodes, int n_streams,
+               int device, icw_ctx **out, int *accepted);
+int icw_destroy(icw_ctx *ctx);
+
+/* Fresh reference state for streams [first, first+count): Hilbert rings zeroed, n_frame=0,
+ * bus zeroed, renders re-seeded (mod_context_init, in_cwave.c:46-80). */
+int icw_stream_init(icw_ctx *ctx, int first, int count);
+/* Open a track on stream s (mod_context_fopen): track length in frames, fades in ms,
+ * sec_align in s.  Resets the renders' shaping state (sound_render_set_outbits), not the RNG;
+ * clears n_frame / Hilbert only if the flags say so (is_clr_nframe_trk / is_clr_hilb_trk). */
+int icw_stream_open(icw_ctx *ctx, int s, int64_t n_samples, uint32_t fade_in_ms,
+                    uint32_t fade_out_ms, uint32_t sec_align, int clr_nframe, int clr_hilb);
+int icw_stream_reset_hilbert(icw_ctx *ctx, int s);
+int icw_stream_reset_framecnt(icw_ctx *ctx, int s);
+
+/* Process n_frames frames of every stream (the batched amod_process_samples).
+ *   in  : stream s starts at (char*)in  + s*in_stride_bytes,  frames interleaved by channel
+ *         in cfg->in_format (what xwave_read_samples leaves in xr->tbuff).
+ *   out : stream s starts at (char*)out + s*out_stride_bytes, interleaved L,R, 2 or 3 bytes LE.
+ *   dbg : ICW_F_DEBUG_PRE only -- double[n_streams][n_frames][2] pre-render values (lOut,rOut).
+ * Host pointers are staged through pinned buffers; with ICW_F_DEVICE_PTRS nothing crosses
+ * PCIe.  hip_stream: a hipStream_t or NULL for the context's own stream.  Returns ICW_OK. */
+int icw_process_batch(icw_ctx *ctx, const void *in, size_t in_stride_bytes, void *out,
+                      size_t out_stride_bytes, int n_frames, unsigned flags, void *dbg,
+                      void *hip_stream);
+/* Same for a subset of streams [first, first+count) (e.g. one decode thread's stream). */
+int icw_process_streams(icw_ctx *ctx, int first, int count, const void *in,
+                        size_t in_stride_bytes, void *out, size_t out_stride_bytes,
+                        int n_frames, unsigned flags, void *dbg, void *hip_stream);
+
+int icw_synchronize(icw_ctx *ctx);
+int icw_get_meters(icw_ctx *ctx, int s, int reset, icw_meters *m);
+int icw_render_size(const icw_ctx *ctx);     /* bytes per output channel-sample: 2 or 3 */
+int icw_n_frame(icw_ctx *ctx, int s, uint64_t *n_frame);
+
+/* Serialisable per-stream state (checkpoint / resume).  Canonical layout documented
+ * in DESIGN.md: IIR histories most-recent-first, Hilbert phases, n_frame, bus, render state. */
+size_t icw_state_size(const icw_ctx *ctx);
+int icw_get_state(icw_ctx *ctx, int s, void *blob, size_t size);
+int icw_set_state(icw_ctx *ctx, int s, const void *blob, size_t size);
+
+/* Kernel timing of the last icw_process_* call, measured with HIP events on the stream the
+ * kernels ran on (bench.py roofline).  ms[0] = IIR state kernel total, ms[1] = output kernel
+ * total, launches[0..1] = launch counts. */
+int icw_last_timing(icw_ctx *ctx, double ms[2], int launches[2]);
+
+const char *icw_version(void);
+const char *icw_strerror(int status);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* ICW_H_ */
