@@ -68,12 +68,16 @@ struct icw_ctx {
     /* host mirrors of meters that survive "reset" semantics */
     std::vector<double> peak_db;          /* [streams][2] */
     /* scratch */
-    double *w = nullptr;
-    size_t w_bytes = 0;
-    double *xd = nullptr;
-    size_t xd_bytes = 0;
-    uint32_t *info_phase = nullptr;
-    unsigned long long *info_nframe = nullptr;
+    /* double-buffered block scratch: block b uses set b & 1, so the output kernel of block b
+     * (second stream) overlaps the IIR state kernel of block b+1 */
+    double *w[2] = {nullptr, nullptr};
+    size_t w_bytes[2] = {0, 0};
+    double *xd[2] = {nullptr, nullptr};
+    size_t xd_bytes[2] = {0, 0};
+    uint32_t *info_phase[2] = {nullptr, nullptr};
+    unsigned long long *info_nframe[2] = {nullptr, nullptr};
+    hipStream_t stream2 = nullptr;
+    hipEvent_t k1done[2] = {nullptr, nullptr}, k2done[2] = {nullptr, nullptr}, join = nullptr;
     unsigned char *d_in = nullptr, *d_out = nullptr;
     size_t d_in_bytes = 0, d_out_bytes = 0;
     double *d_pre = nullptr;
@@ -287,9 +291,13 @@ void free_all(icw_ctx *c)
 {
     DevState &s = c->st;
     void *ptrs[] = {s.hist, s.sncnt, s.hq_phase, s.pos, s.fade, s.n_frame, s.bus, s.clips, s.peak_bits,
-                    c->d_prog, c->w, c->xd, c->info_phase, c->info_nframe, c->d_in, c->d_out, c->d_pre};
+                    c->d_prog, c->w[0], c->w[1], c->xd[0], c->xd[1], c->info_phase[0], c->info_phase[1],
+                    c->info_nframe[0], c->info_nframe[1], c->d_in, c->d_out, c->d_pre};
     for (void *p : ptrs)
         if (p) hipFree(p);
+    for (hipEvent_t e : {c->k1done[0], c->k1done[1], c->k2done[0], c->k2done[1], c->join})
+        if (e) hipEventDestroy(e);
+    if (c->stream2) hipStreamDestroy(c->stream2);
     for (auto e : c->ev) hipEventDestroy(e);
     if (c->stream) hipStreamDestroy(c->stream);
 }
@@ -379,12 +387,20 @@ int icw_create(const icw_config *cfg, const icw_node *nodes, int n_nodes, int n_
     rc |= dalloc(&s.bus, S * ICW_N_INPUTS * 4);
     rc |= dalloc(&s.clips, S * 2);
     rc |= dalloc(&s.peak_bits, S * 2);
-    rc |= dalloc(&c->info_phase, S * 2);
-    rc |= dalloc(&c->info_nframe, S);
+    for (int p = 0; p < 2; ++p) {
+        rc |= dalloc(&c->info_phase[p], S * 2);
+        rc |= dalloc(&c->info_nframe[p], S);
+    }
     rc |= dalloc(&c->d_prog, 1);
     if (rc == ICW_OK && hipMemcpy(c->d_prog, &c->prog, sizeof(IcwProg), hipMemcpyHostToDevice) != hipSuccess)
         rc = ICW_EDEVICE;
     if (rc == ICW_OK && hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) rc = ICW_EDEVICE;
+    if (rc == ICW_OK && hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking) != hipSuccess) rc = ICW_EDEVICE;
+    for (int p = 0; p < 2 && rc == ICW_OK; ++p)
+        if (hipEventCreateWithFlags(&c->k1done[p], hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&c->k2done[p], hipEventDisableTiming) != hipSuccess)
+            rc = ICW_EDEVICE;
+    if (rc == ICW_OK && hipEventCreateWithFlags(&c->join, hipEventDisableTiming) != hipSuccess) rc = ICW_EDEVICE;
     if (rc != ICW_OK) {
         free_all(c);
         delete c;
@@ -534,15 +550,22 @@ int icw_process_streams(icw_ctx *c, int first, int count, const void *in, size_t
     const int N = c->nord;
     const int Tb = std::min(n_frames, kMaxBlockFrames);
     const size_t w_pitch = (size_t)Tb + N + 1;
-    if (grow((void **)&c->w, &c->w_bytes, S * 4 * w_pitch * sizeof(double))) return ICW_ENOMEM;
     const size_t x_pitch = ((size_t)Tb + 1) & ~(size_t)1;
-    if (grow((void **)&c->xd, &c->xd_bytes, S * 2 * x_pitch * sizeof(double))) return ICW_ENOMEM;
+    const int n_blocks = (n_frames + Tb - 1) / Tb;
+    const int n_sets = n_blocks > 1 ? 2 : 1;
+    for (int p = 0; p < n_sets; ++p) {
+        if (grow((void **)&c->w[p], &c->w_bytes[p], S * 4 * w_pitch * sizeof(double))) return ICW_ENOMEM;
+        if (grow((void **)&c->xd[p], &c->xd_bytes[p], S * 2 * x_pitch * sizeof(double))) return ICW_ENOMEM;
+    }
+    hipStream_t st2 = c->stream2;
+    /* second stream starts after everything already queued on st (inputs, previous calls) */
+    if (hipEventRecord(c->join, st) != hipSuccess || hipStreamWaitEvent(st2, c->join, 0) != hipSuccess)
+        return ICW_EDEVICE;
 
     DevState &ds = c->st;
     const size_t f0 = (size_t)first;
-    const int n_blocks = (n_frames + Tb - 1) / Tb;
-    if (timing && (int)c->ev.size() < 3 * n_blocks) {
-        while ((int)c->ev.size() < 3 * n_blocks) {
+    if (timing && (int)c->ev.size() < 4 * n_blocks) {
+        while ((int)c->ev.size() < 4 * n_blocks) {
             hipEvent_t e;
             if (hipEventCreate(&e) != hipSuccess) return ICW_EDEVICE;
             c->ev.push_back(e);
@@ -551,6 +574,7 @@ int icw_process_streams(icw_ctx *c, int first, int count, const void *in, size_t
     for (int b = 0; b < n_blocks; ++b) {
         const int t0 = b * Tb;
         const int T = std::min(Tb, n_frames - t0);
+        const int p = b & (n_sets - 1);
         IcwK0Args a0;
         memset(&a0, 0, sizeof(a0));
         a0.in = d_in + (size_t)t0 * fsz;
@@ -563,13 +587,13 @@ int icw_process_streams(icw_ctx *c, int first, int count, const void *in, size_t
         a0.T = T;
         a0.pos = ds.pos + f0;
         a0.fade = ds.fade + f0 * 3;
-        a0.xd = c->xd;
+        a0.xd = c->xd[p];
         a0.x_pitch = x_pitch;
         if (icw_launch_unpack(&a0, st) != hipSuccess) return ICW_EDEVICE;
 
         IcwK1Args a1;
         memset(&a1, 0, sizeof(a1));
-        a1.xd = c->xd;
+        a1.xd = c->xd[p];
         a1.x_pitch = x_pitch;
         a1.nch = nch;
         a1.n_streams = count;
@@ -582,24 +606,28 @@ int icw_process_streams(icw_ctx *c, int first, int count, const void *in, size_t
         a1.n_frame = ds.n_frame + f0;
         a1.ssr = (unsigned long long)cfg.sample_rate * ICW_HZ_SCALE;
         a1.scaled = cfg.frmod_scaled;
-        a1.w = c->w;
+        a1.w = c->w[p];
         a1.w_pitch = w_pitch;
-        a1.info_phase = c->info_phase;
-        a1.info_nframe = c->info_nframe;
+        a1.info_phase = c->info_phase[p];
+        a1.info_nframe = c->info_nframe[p];
         memcpy(a1.pc, c->pc, sizeof(a1.pc));
-        if (timing) hipEventRecord(c->ev[3 * b], st);
+        /* w[p]/info[p] were last read by the output kernel of block b-2 */
+        if (b >= 2 && hipStreamWaitEvent(st, c->k2done[p], 0) != hipSuccess) return ICW_EDEVICE;
+        if (timing) hipEventRecord(c->ev[4 * b], st);
         if (icw_launch_iir_state(&a1, N, cfg.iir_kahan, cfg.iir_subnorm_reject, st) != hipSuccess) return ICW_EDEVICE;
-        if (timing) hipEventRecord(c->ev[3 * b + 1], st);
+        if (timing) hipEventRecord(c->ev[4 * b + 1], st);
+        if (hipEventRecord(c->k1done[p], st) != hipSuccess || hipStreamWaitEvent(st2, c->k1done[p], 0) != hipSuccess)
+            return ICW_EDEVICE;
 
         IcwK2Args a2;
         memset(&a2, 0, sizeof(a2));
-        a2.w = c->w;
+        a2.w = c->w[p];
         a2.w_pitch = w_pitch;
         a2.n_streams = count;
         a2.T = T;
         a2.n_chains = count * 4;
-        a2.info_phase = c->info_phase;
-        a2.info_nframe = c->info_nframe;
+        a2.info_phase = c->info_phase[p];
+        a2.info_nframe = c->info_nframe[p];
         a2.ssr = a1.ssr;
         a2.scaled = cfg.frmod_scaled;
         a2.sample_rate = cfg.sample_rate;
@@ -618,9 +646,14 @@ int icw_process_streams(icw_ctx *c, int first, int count, const void *in, size_t
         memcpy(a2.pc, c->pc, sizeof(a2.pc));
         memcpy(a2.pd, c->pd, sizeof(a2.pd));
         a2.d0 = c->d0;
-        if (icw_launch_output(&a2, N, cfg.iir_kahan, st) != hipSuccess) return ICW_EDEVICE;
-        if (timing) hipEventRecord(c->ev[3 * b + 2], st);
+        if (timing) hipEventRecord(c->ev[4 * b + 2], st2);
+        if (icw_launch_output(&a2, N, cfg.iir_kahan, st2) != hipSuccess) return ICW_EDEVICE;
+        if (timing) hipEventRecord(c->ev[4 * b + 3], st2);
+        if (hipEventRecord(c->k2done[p], st2) != hipSuccess) return ICW_EDEVICE;
     }
+    /* join: the caller's stream completes only after the last output kernel */
+    if (hipEventRecord(c->join, st2) != hipSuccess || hipStreamWaitEvent(st, c->join, 0) != hipSuccess)
+        return ICW_EDEVICE;
     if (!dev) {
         if (hipMemcpy2DAsync(out, out_stride, d_out, dos, dos, S, hipMemcpyDeviceToHost, st) != hipSuccess)
             return ICW_EDEVICE;
@@ -633,8 +666,8 @@ int icw_process_streams(icw_ctx *c, int first, int count, const void *in, size_t
         double m1 = 0, m2 = 0;
         for (int b = 0; b < n_blocks; ++b) {
             float x = 0, y = 0;
-            hipEventElapsedTime(&x, c->ev[3 * b], c->ev[3 * b + 1]);
-            hipEventElapsedTime(&y, c->ev[3 * b + 1], c->ev[3 * b + 2]);
+            hipEventElapsedTime(&x, c->ev[4 * b], c->ev[4 * b + 1]);
+            hipEventElapsedTime(&y, c->ev[4 * b + 2], c->ev[4 * b + 3]);
             m1 += x;
             m2 += y;
         }

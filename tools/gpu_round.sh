@@ -1,0 +1,35 @@
+#!/bin/bash
+# GPU-box driver: each GPU step under its own timeout; stop at the first crash/timeout.
+# Test failures (pytest rc 1) do not stop later steps; faults (rc >= 124, 134, 139) do.
+mkdir -p gpurun_out
+ok() { local rc=$1; [ "$rc" -eq 0 ] || [ "$rc" -eq 1 ]; }
+step() {   # step <name> <timeout> <cmd...>
+  local name=$1 to=$2; shift 2
+  timeout -k 10 "$to" "$@" > "gpurun_out/$name.txt" 2>&1
+  local rc=$?
+  echo "[$name] rc=$rc" | tee -a gpurun_out/steps.txt
+  return $rc
+}
+for s in "$@"; do
+  case $s in
+    probe) step lat_probe 60 ./tools/lat_probe || exit 2 ;;
+    test)  step pytest_gpu 900 python -m pytest tests -m gpu -q -x; ok $? || exit 2 ;;
+    testall) step pytest_gpu 900 python -m pytest tests -m gpu -q; ok $? || exit 2 ;;
+    bench) step bench 600 python bench.py --steps 3 --warmup 1 --no-cpu-baseline || exit 2 ;;
+    benchfull) step bench_full 900 python bench.py || exit 2 ;;
+    smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" || exit 2 ;;
+    prof)
+      R=$(pwd); export TMPDIR=/tmp
+      ( cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/gpurun_out/prof" -o run \
+          -- python3 "$R/bench.py" --steps 3 --warmup 1 --no-cpu-baseline ) > gpurun_out/prof.txt 2>&1
+      rc=$?; echo "[prof] rc=$rc" | tee -a gpurun_out/steps.txt; [ $rc -eq 0 ] || exit 2 ;;
+    pmc)
+      R=$(pwd); export TMPDIR=/tmp
+      ( cd /tmp && timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$R/gpurun_out/pmc_fetch" -o run \
+          -- python3 "$R/bench.py" --steps 2 --warmup 1 --no-cpu-baseline ) > gpurun_out/pmc_fetch.txt 2>&1
+      rc=$?; echo "[pmc_fetch] rc=$rc" | tee -a gpurun_out/steps.txt; [ $rc -eq 0 ] || exit 2
+      ( cd /tmp && timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$R/gpurun_out/pmc_write" -o run \
+          -- python3 "$R/bench.py" --steps 2 --warmup 1 --no-cpu-baseline ) > gpurun_out/pmc_write.txt 2>&1
+      rc=$?; echo "[pmc_write] rc=$rc" | tee -a gpurun_out/steps.txt; [ $rc -eq 0 ] || exit 2 ;;
+  esac
+done

@@ -47,6 +47,37 @@ __global__ void kahan(const double *in, double *out, long long *cyc)
     if (threadIdx.x == 0) cyc[blockIdx.x] = t1 - t0;
 }
 
+__global__ void dep_add_lanes(const double *in, double *out, long long *cyc, int lanes)
+{
+    double a = in[threadIdx.x & 63], c = in[64 + (threadIdx.x & 63)];
+    long long t0 = clock64();
+    if ((int)(threadIdx.x & 63) < lanes) {
+#pragma unroll 64
+        for (int i = 0; i < REPS; ++i) a = a + c;
+    }
+    long long t1 = clock64();
+    out[threadIdx.x] = a;
+    if (threadIdx.x == 0) cyc[blockIdx.x] = t1 - t0;
+}
+
+__global__ void kahan_lanes(const double *in, double *out, long long *cyc, int lanes)
+{
+    double S = in[threadIdx.x & 63], C = 0.0, x = in[64 + (threadIdx.x & 63)];
+    long long t0 = clock64();
+    if ((int)(threadIdx.x & 63) < lanes) {
+#pragma unroll 64
+        for (int i = 0; i < REPS; ++i) {
+            double Y = x - C;
+            double T = S + Y;
+            C = (T - S) - Y;
+            S = T;
+        }
+    }
+    long long t1 = clock64();
+    out[threadIdx.x] = S + C;
+    if (threadIdx.x == 0) cyc[blockIdx.x] = t1 - t0;
+}
+
 __global__ void indep_add(const double *in, double *out, long long *cyc)
 {
     double a0 = in[threadIdx.x], a1 = a0 + 1, a2 = a0 + 2, a3 = a0 + 3, a4 = a0 + 4, a5 = a0 + 5,
@@ -103,6 +134,25 @@ int main()
     run("dep_mul", dep_mul, 1, din, dout, dcyc, REPS);
     run("kahan4", kahan, 1, din, dout, dcyc, REPS * 4.0);
     run("indep_add", indep_add, 1, din, dout, dcyc, REPS);
+    for (int lanes = 64; lanes >= 1; lanes /= 2) {
+        long long h1[2];
+        hipLaunchKernelGGL(dep_add_lanes, dim3(1), dim3(64), 0, 0, din, dout, dcyc, lanes);
+        hipDeviceSynchronize();
+        hipLaunchKernelGGL(dep_add_lanes, dim3(1), dim3(64), 0, 0, din, dout, dcyc, lanes);
+        hipDeviceSynchronize();
+        hipMemcpy(h1, dcyc, 8, hipMemcpyDeviceToHost);
+        long long h2[2];
+        hipLaunchKernelGGL(kahan_lanes, dim3(1), dim3(64), 0, 0, din, dout, dcyc, lanes);
+        hipDeviceSynchronize();
+        hipLaunchKernelGGL(kahan_lanes, dim3(1), dim3(64), 0, 0, din, dout, dcyc, lanes);
+        hipDeviceSynchronize();
+        hipMemcpy(h2, dcyc, 8, hipMemcpyDeviceToHost);
+        printf("active lanes %2d: dep_add %.2f cyc/op, kahan %.2f cyc/add\n", lanes, h1[0] / (double)REPS,
+               h2[0] / (4.0 * REPS));
+    }
+    // two waves sharing one SIMD (8 waves per WG -> 2 per SIMD)
+    run("dep_add", dep_add, 8, din, dout, dcyc, REPS);
+    run("kahan4", kahan, 8, din, dout, dcyc, REPS * 4.0);
     run("dep_add", dep_add, 4, din, dout, dcyc, REPS);
     run("kahan4", kahan, 4, din, dout, dcyc, REPS * 4.0);
     return 0;
