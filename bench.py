@@ -131,6 +131,7 @@ def main():
     if dist:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    ctx.synchronize()     # raises if a kernel reported a failed hand-off
     if dist:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)

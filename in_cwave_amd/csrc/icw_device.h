@@ -22,13 +22,14 @@ struct IcwK0Args {
     int32_t n_streams, T;
     const long long *pos;          /* [n_streams] reader position (frames into track) */
     const long long *fade;         /* [n_streams][3] n_samples, n_fade_in, n_fade_out */
-    double *xd;                    /* [n_streams][2][x_pitch] faded input, channel-planar */
+    const uint32_t *hq_phase;      /* [n_streams][2] Hilbert phase at block start */
+    double *xd;                    /* [n_chains][x_pitch]: each chain's own filter input sequence */
     size_t x_pitch;
 };
 
 /* Arguments of the IIR state kernel (one lane = one DF-II chain). */
 struct IcwK1Args {
-    const double *xd;              /* K0 output */
+    const double *xd;              /* K0 output: per-chain filter inputs */
     size_t x_pitch;
     uint32_t nch;
     int32_t n_streams, n_chains, T;
@@ -43,6 +44,7 @@ struct IcwK1Args {
     size_t w_pitch;
     uint32_t *info_phase;          /* [n_streams][2] block-start Hilbert phases (for K2) */
     unsigned long long *info_nframe; /* [n_streams] block-start n_frame (for K2) */
+    int *err;                      /* set by a bounded spin that gave up (never in a healthy run) */
     double pc[20];                 /* loop-back coefficients -a[i+1]/a0 */
 };
 

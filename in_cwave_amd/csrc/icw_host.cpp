@@ -23,6 +23,7 @@
 #include "icw_tables.inc"
 
 extern "C" hipError_t icw_launch_unpack(const IcwK0Args *a, hipStream_t st);
+extern "C" hipError_t icw_launch_iir_pair(const IcwK1Args *a, int nord, int kahan, int subn, hipStream_t st);
 extern "C" hipError_t icw_launch_iir_state(const IcwK1Args *a, int nord, int kahan, int subn, hipStream_t st);
 extern "C" hipError_t icw_launch_output(const IcwK2Args *a, int nord, int kahan, hipStream_t st);
 
@@ -50,6 +51,7 @@ struct DevState {
     double *bus = nullptr;                /* [streams][27][4] */
     uint32_t *clips = nullptr;            /* [streams][2] */
     unsigned long long *peak_bits = nullptr; /* [streams][2] */
+    int *err = nullptr;                   /* kernel hand-off timeout flag */
 };
 
 }  // namespace
@@ -84,6 +86,8 @@ struct icw_ctx {
     size_t d_pre_bytes = 0;
     hipStream_t stream = nullptr;
     std::vector<hipEvent_t> ev;
+    int n_cu = 256;
+    bool pair_mode = false;   /* chain+helper wave pairs (few chains per SIMD) vs plain lanes */
     double last_ms[2]{};
     int last_launches[2]{};
     std::mutex mu;
@@ -290,7 +294,7 @@ int grow(void **p, size_t *cur, size_t need)
 void free_all(icw_ctx *c)
 {
     DevState &s = c->st;
-    void *ptrs[] = {s.hist, s.sncnt, s.hq_phase, s.pos, s.fade, s.n_frame, s.bus, s.clips, s.peak_bits,
+    void *ptrs[] = {s.err, s.hist, s.sncnt, s.hq_phase, s.pos, s.fade, s.n_frame, s.bus, s.clips, s.peak_bits,
                     c->d_prog, c->w[0], c->w[1], c->xd[0], c->xd[1], c->info_phase[0], c->info_phase[1],
                     c->info_nframe[0], c->info_nframe[1], c->d_in, c->d_out, c->d_pre};
     for (void *p : ptrs)
@@ -387,6 +391,7 @@ int icw_create(const icw_config *cfg, const icw_node *nodes, int n_nodes, int n_
     rc |= dalloc(&s.bus, S * ICW_N_INPUTS * 4);
     rc |= dalloc(&s.clips, S * 2);
     rc |= dalloc(&s.peak_bits, S * 2);
+    rc |= dalloc(&s.err, 1);
     for (int p = 0; p < 2; ++p) {
         rc |= dalloc(&c->info_phase[p], S * 2);
         rc |= dalloc(&c->info_nframe[p], S);
@@ -407,6 +412,19 @@ int icw_create(const icw_config *cfg, const icw_node *nodes, int n_nodes, int n_
         return rc < 0 ? (rc == ICW_ENOMEM ? ICW_ENOMEM : ICW_EDEVICE) : ICW_EDEVICE;
     }
     c->peak_db.assign(S * 2, ICW_SR_ZERO_SIGNAL_DB);
+    {
+        hipDeviceProp_t prop;
+        if (hipGetDeviceProperties(&prop, c->device) == hipSuccess) c->n_cu = prop.multiProcessorCount;
+        /* the pair kernel holds ~150 KB LDS -> one 64-chain workgroup per CU; beyond that many
+         * chains the plain kernel (several waves per SIMD, throughput-bound) is the better fit */
+        const long wgs = ((long)S * 4 + 63) / 64;
+        /* measured (profiles/r01_*): the pair kernel's hand-off protocol still costs more than the
+         * instructions it removes from the chain wave, so the plain kernel is the default */
+        c->pair_mode = false && wgs <= c->n_cu;
+        const char *m = getenv("ICW_K1_MODE");
+        if (m && !strcmp(m, "plain")) c->pair_mode = false;
+        if (m && !strcmp(m, "pair")) c->pair_mode = true;
+    }
     rc = icw_stream_init(c, 0, n_streams);
     if (rc) { free_all(c); delete c; return rc; }
     *out = c;
@@ -550,12 +568,12 @@ int icw_process_streams(icw_ctx *c, int first, int count, const void *in, size_t
     const int N = c->nord;
     const int Tb = std::min(n_frames, kMaxBlockFrames);
     const size_t w_pitch = (size_t)Tb + N + 1;
-    const size_t x_pitch = ((size_t)Tb + 1) & ~(size_t)1;
+    const size_t x_pitch = ((size_t)Tb + ICW_MAX_IIR_ORDER + 2) & ~(size_t)1;   /* look-ahead pad */
     const int n_blocks = (n_frames + Tb - 1) / Tb;
     const int n_sets = n_blocks > 1 ? 2 : 1;
     for (int p = 0; p < n_sets; ++p) {
         if (grow((void **)&c->w[p], &c->w_bytes[p], S * 4 * w_pitch * sizeof(double))) return ICW_ENOMEM;
-        if (grow((void **)&c->xd[p], &c->xd_bytes[p], S * 2 * x_pitch * sizeof(double))) return ICW_ENOMEM;
+        if (grow((void **)&c->xd[p], &c->xd_bytes[p], S * 4 * x_pitch * sizeof(double))) return ICW_ENOMEM;
     }
     hipStream_t st2 = c->stream2;
     /* second stream starts after everything already queued on st (inputs, previous calls) */
@@ -587,6 +605,7 @@ int icw_process_streams(icw_ctx *c, int first, int count, const void *in, size_t
         a0.T = T;
         a0.pos = ds.pos + f0;
         a0.fade = ds.fade + f0 * 3;
+        a0.hq_phase = ds.hq_phase + f0 * 2;
         a0.xd = c->xd[p];
         a0.x_pitch = x_pitch;
         if (icw_launch_unpack(&a0, st) != hipSuccess) return ICW_EDEVICE;
@@ -604,6 +623,7 @@ int icw_process_streams(icw_ctx *c, int first, int count, const void *in, size_t
         a1.hq_phase = ds.hq_phase + f0 * 2;
         a1.pos = ds.pos + f0;
         a1.n_frame = ds.n_frame + f0;
+        a1.err = ds.err;
         a1.ssr = (unsigned long long)cfg.sample_rate * ICW_HZ_SCALE;
         a1.scaled = cfg.frmod_scaled;
         a1.w = c->w[p];
@@ -614,7 +634,10 @@ int icw_process_streams(icw_ctx *c, int first, int count, const void *in, size_t
         /* w[p]/info[p] were last read by the output kernel of block b-2 */
         if (b >= 2 && hipStreamWaitEvent(st, c->k2done[p], 0) != hipSuccess) return ICW_EDEVICE;
         if (timing) hipEventRecord(c->ev[4 * b], st);
-        if (icw_launch_iir_state(&a1, N, cfg.iir_kahan, cfg.iir_subnorm_reject, st) != hipSuccess) return ICW_EDEVICE;
+        const hipError_t e1 = c->pair_mode
+            ? icw_launch_iir_pair(&a1, N, cfg.iir_kahan, cfg.iir_subnorm_reject, st)
+            : icw_launch_iir_state(&a1, N, cfg.iir_kahan, cfg.iir_subnorm_reject, st);
+        if (e1 != hipSuccess) return ICW_EDEVICE;
         if (timing) hipEventRecord(c->ev[4 * b + 1], st);
         if (hipEventRecord(c->k1done[p], st) != hipSuccess || hipStreamWaitEvent(st2, c->k1done[p], 0) != hipSuccess)
             return ICW_EDEVICE;
@@ -660,6 +683,8 @@ int icw_process_streams(icw_ctx *c, int first, int count, const void *in, size_t
         if (d_pre && hipMemcpyAsync(dbg, d_pre, S * (size_t)n_frames * 2 * sizeof(double), hipMemcpyDeviceToHost, st) != hipSuccess)
             return ICW_EDEVICE;
         if (hipStreamSynchronize(st) != hipSuccess) return ICW_EDEVICE;
+        int e = 0;
+        if (hipMemcpy(&e, ds.err, sizeof(int), hipMemcpyDeviceToHost) != hipSuccess || e) return ICW_EDEVICE;
     }
     if (timing) {
         if (hipStreamSynchronize(st) != hipSuccess) return ICW_EDEVICE;
@@ -689,7 +714,10 @@ int icw_synchronize(icw_ctx *c)
 {
     if (!c) return ICW_EINVAL;
     if (set_dev(c)) return ICW_EDEVICE;
-    return hipStreamSynchronize(c->stream) == hipSuccess ? ICW_OK : ICW_EDEVICE;
+    if (hipStreamSynchronize(c->stream) != hipSuccess) return ICW_EDEVICE;
+    int e = 0;
+    if (hipMemcpy(&e, c->st.err, sizeof(int), hipMemcpyDeviceToHost) != hipSuccess || e) return ICW_EDEVICE;
+    return ICW_OK;
 }
 
 int icw_get_meters(icw_ctx *c, int s, int reset, icw_meters *m)

@@ -26,6 +26,14 @@
 
 #pragma clang fp contract(off)
 
+/* diagnostic build only (tools/k1_probe.hip): s_memtime stamps of workgroup 0, lane 0 */
+#ifdef ICW_STAMPS
+__device__ unsigned long long icw_stamps[8][1024];
+#define ICW_STAMP(k, n) do { if (blockIdx.x == 0 && lane == 0 && (n) < 1024) icw_stamps[k][n] = __builtin_amdgcn_s_memtime(); } while (0)
+#else
+#define ICW_STAMP(k, n) do { } while (0)
+#endif
+
 #define ICW_PI (3.1415926535897932384626433832795029)
 #define ICW_SQRT2 (1.4142135623730950488016887242097)
 
@@ -66,6 +74,13 @@ __device__ __forceinline__ double icw_fade(long long ix, long long ns, long long
     return fade;
 }
 
+/* input of the I (f=0) / Q (f=1) filter for Hilbert phase k (lpf_hilbert_quad.c:133-151):
+ *   I: {x, +0, -x, +0}   Q: {+0, -x, +0, x}   ==  k' = (k+f)&3: {x, +0, -x, +0}[k'] */
+__device__ __forceinline__ double icw_filter_in(double x, unsigned kq)
+{
+    return kq == 0 ? x : (kq == 2 ? -x : 0.0);
+}
+
 /* ------------------------------------------------------------ IIR state kernel (K1) ----- */
 /* One unrolled step of the loop-back sum for sample J of an N-block.  The delay line lives in
  * R[]: at step J the logical z_i (i = 0 most recent) is R[(J-1-i) mod N]; the new w is written
@@ -101,12 +116,6 @@ __device__ __forceinline__ void icw_iir_step(double (&R)[N], double xin, const d
     R[J] = S;
 }
 
-/* input of the I (f=0) / Q (f=1) filter for Hilbert phase k (lpf_hilbert_quad.c:133-151):
- *   I: {x, +0, -x, +0}   Q: {+0, -x, +0, x}   ==  k' = (k+f)&3: {x, +0, -x, +0}[k'] */
-__device__ __forceinline__ double icw_filter_in(double x, unsigned kq)
-{
-    return kq == 0 ? x : (kq == 2 ? -x : 0.0);
-}
 
 template <int N, int J>
 __device__ __forceinline__ void icw_store_hist(const double (&R)[N], double *hist, int g, int n_chains)
@@ -138,30 +147,35 @@ __device__ __forceinline__ void icw_normalise_ring(double (&R)[N], int rem)
 }
 
 template <int N, int J0, bool KAHAN, bool SUBN>
-__device__ __forceinline__ void icw_block_steps(double (&R)[N], const double (&xv)[N], unsigned kq0,
+__device__ __forceinline__ void icw_block_steps(double (&R)[N], const double (&xv)[N],
                                                 const double (&pc)[20], unsigned &cnt, int lim)
 {
     if constexpr (J0 < N) {
         if (J0 < lim) {
-            icw_iir_step<N, KAHAN, SUBN, J0>(R, icw_filter_in(xv[J0], (kq0 + J0) & 3u), pc, cnt);
-            icw_block_steps<N, J0 + 1, KAHAN, SUBN>(R, xv, kq0, pc, cnt, lim);
+            icw_iir_step<N, KAHAN, SUBN, J0>(R, xv[J0], pc, cnt);
+            icw_block_steps<N, J0 + 1, KAHAN, SUBN>(R, xv, pc, cnt, lim);
         }
     }
 }
 
+/* full block of N steps; after step J consumes xv[J], refill it with the input N samples ahead
+ * (rows are padded by >= N doubles, so the last block's look-ahead loads stay in bounds) */
 template <int N, int J0, bool KAHAN, bool SUBN>
-__device__ __forceinline__ void icw_block_steps_full(double (&R)[N], const double (&xv)[N], unsigned kq0,
-                                                     const double (&pc)[20], unsigned &cnt)
+__device__ __forceinline__ void icw_block_steps_pf(double (&R)[N], double (&xv)[N], const double *xnext,
+                                                   const double (&pc)[20], unsigned &cnt)
 {
     if constexpr (J0 < N) {
-        icw_iir_step<N, KAHAN, SUBN, J0>(R, icw_filter_in(xv[J0], (kq0 + J0) & 3u), pc, cnt);
-        icw_block_steps_full<N, J0 + 1, KAHAN, SUBN>(R, xv, kq0, pc, cnt);
+        icw_iir_step<N, KAHAN, SUBN, J0>(R, xv[J0], pc, cnt);
+        xv[J0] = xnext[J0];
+        icw_block_steps_pf<N, J0 + 1, KAHAN, SUBN>(R, xv, xnext, pc, cnt);
     }
 }
 
 /* Input prep (K0): unpack + fade each frame once (xwave_unpack_csample, xwave_reader.c:908-1001)
- * into channel-planar doubles xd[s][ch][t].  Mono input writes plane 0 only; the right-channel
- * chains then read plane 0, which is exactly the reference's reuse of `val` (xwave_reader.c:988). */
+ * and lay out every DF-II chain's own input sequence: the quadrature mix of hq_rp_process
+ * (lpf_hilbert_quad.c:129-156) feeds the I filter {x, +0, -x, +0} and the Q filter {+0, -x, +0, x}
+ * by sample phase.  Mono input feeds the right converter with the left value, exactly the
+ * reference's reuse of `val` (xwave_reader.c:988).  Row g = s*4 + ch*2 + {0:I, 1:Q}. */
 __global__ __launch_bounds__(256) void icw_unpack_frames(IcwK0Args a)
 {
     const int t = blockIdx.x * 256 + threadIdx.x;
@@ -170,14 +184,21 @@ __global__ __launch_bounds__(256) void icw_unpack_frames(IcwK0Args a)
     const unsigned char *fp = a.in + (size_t)s * a.in_stride + (size_t)t * a.fsz;
     const long long ix = a.pos[s] + t;
     const double fd = icw_fade(ix, a.fade[s * 3 + 0], a.fade[s * 3 + 1], a.fade[s * 3 + 2]);
-    double *xs = a.xd + (size_t)s * 2 * a.x_pitch;
-    double v = icw_unpack(fp, a.fmt);
-    if (fd >= 0.0) v *= fd;
-    xs[t] = v;
+    double v[2];
+    v[0] = icw_unpack(fp, a.fmt);
+    if (fd >= 0.0) v[0] *= fd;
     if (a.nch > 1) {
-        v = icw_unpack(fp + a.csz, a.fmt);
-        if (fd >= 0.0) v *= fd;
-        xs[a.x_pitch + t] = v;
+        v[1] = icw_unpack(fp + a.csz, a.fmt);
+        if (fd >= 0.0) v[1] *= fd;
+    } else {
+        v[1] = v[0];
+    }
+    double *xs = a.xd + (size_t)s * 4 * a.x_pitch + t;
+#pragma unroll
+    for (int ch = 0; ch < 2; ++ch) {
+        const unsigned k = (a.hq_phase[s * 2 + ch] + (unsigned)t) & 3u;
+        xs[(size_t)(ch * 2 + 0) * a.x_pitch] = icw_filter_in(v[ch], k);
+        xs[(size_t)(ch * 2 + 1) * a.x_pitch] = icw_filter_in(v[ch], (k + 1u) & 3u);
     }
 }
 
@@ -204,7 +225,7 @@ __global__ __launch_bounds__(64) void icw_iir_state(IcwK1Args a)
     for (int i = 0; i < N; ++i) R[N - 1 - i] = a.hist[(size_t)g * ICW_HIST_PITCH + i];
 
     const unsigned ph0 = a.hq_phase[s * 2 + c];
-    const double *xp = a.xd + ((size_t)s * 2 + (a.nch > 1 ? c : 0)) * a.x_pitch;
+    const double *xp = a.xd + (size_t)g * a.x_pitch;
     double *wrow = a.w + (size_t)g * a.w_pitch;
     /* history rows [0, N): row j = z_{N-1-j} = R[j] */
 #pragma unroll
@@ -214,18 +235,16 @@ __global__ __launch_bounds__(64) void icw_iir_state(IcwK1Args a)
     unsigned cnt = 0;
     int t = 0;
     if (T >= N) {
-        /* software pipeline: the next block's inputs are in flight while this block computes */
-        double xv[N], xn[N];
+        /* xv[j] holds the input of step j of the current block; right after a step consumes it the
+         * same register is refilled with the next block's input, so loads run N samples ahead
+         * with no register copies */
+        double xv[N];
         icw_load_x<N>(xv, xp);
         for (; t + N <= T; t += N) {
-            if (t + 2 * N <= T) icw_load_x<N>(xn, xp + t + N);
-            const unsigned kq0 = (ph0 + (unsigned)t + (unsigned)f) & 3u;
-            icw_block_steps_full<N, 0, KAHAN, SUBN>(R, xv, kq0, pc, cnt);
+            icw_block_steps_pf<N, 0, KAHAN, SUBN>(R, xv, xp + t + N, pc, cnt);
             double *wo = wrow + N + t;
 #pragma unroll
             for (int j = 0; j < N; ++j) wo[j] = R[j];
-#pragma unroll
-            for (int j = 0; j < N; ++j) xv[j] = xn[j];
         }
     }
     const int rem = T - t;
@@ -233,8 +252,7 @@ __global__ __launch_bounds__(64) void icw_iir_state(IcwK1Args a)
         double xv[N];
 #pragma unroll
         for (int j = 0; j < N; ++j) xv[j] = (j < rem) ? xp[t + j] : 0.0;
-        const unsigned kq0 = (ph0 + (unsigned)t + (unsigned)f) & 3u;
-        icw_block_steps<N, 0, KAHAN, SUBN>(R, xv, kq0, pc, cnt, rem);
+        icw_block_steps<N, 0, KAHAN, SUBN>(R, xv, pc, cnt, rem);
         double *wo = wrow + N + t;
 #pragma unroll
         for (int j = 0; j < N; ++j)
@@ -242,6 +260,293 @@ __global__ __launch_bounds__(64) void icw_iir_state(IcwK1Args a)
         icw_normalise_ring<N>(R, rem);
     }
     icw_store_hist<N, 0>(R, a.hist, g, n_chains);
+    a.sncnt[g] += cnt;
+    if (f == 0) {
+        a.info_phase[s * 2 + c] = ph0;
+        a.hq_phase[s * 2 + c] = (ph0 + (unsigned)T) & 3u;
+        if (c == 0) {
+            a.pos[s] += T;
+            const unsigned long long n0 = a.n_frame[s];
+            a.info_nframe[s] = n0;
+            a.n_frame[s] = a.scaled ? (n0 + (unsigned long long)T) % a.ssr : n0 + (unsigned long long)T;
+        }
+    }
+}
+
+/* ---------------------------------------- IIR state kernel, chain+helper wave pair (K1p) ---- */
+/* Latency/issue-bound regime (few chains per SIMD, e.g. BASELINE C2: 1024 chains on 1024 SIMDs).
+ * A single wave issues ~1 FP64 instruction per ~4.7 cycles whether or not the instructions depend
+ * on each other (tools/lat_probe), so a chain's time per sample is its instruction count.  The
+ * workgroup pairs a CHAIN wave with a HELPER wave on another SIMD:
+ *   chain : the loop-back Kahan sum (hblpf.c:1017-1046) -- the 4 products that depend on the
+ *           newest / oldest states, the 73 dependent adds, the subnorm reject -- and nothing else;
+ *   helper: every other product w[m]*c_i (i in [3, N-KT)), the Hilbert input selection, and the
+ *           store of w[] to HBM; it publishes them through an LDS ring indexed by target sample.
+ * Hand-off: the chain writes w[n] to wring and bumps chain_done; the helper bumps help_done once
+ * w[m]'s products are in LDS.  Slot n needs help_done >= n-3; the chain checks the slot of sample
+ * n+1 in the middle of sample n and prefetches it in two halves (after the entries are consumed),
+ * so LDS latency is off the critical path and the helper has ~2 samples of slack. */
+template <int N>
+struct IcwPair {
+    static constexpr int KT = (N >= 20) ? 2 : 1;   /* oldest products computed by the chain */
+    static constexpr int RING = N - KT;            /* product slots, indexed by target % RING */
+    static constexpr int NH = N - KT - 3;          /* helper products i in [3, N-KT) */
+    static constexpr int NE = NH + 1;              /* + the filter input x_in (entry 0) */
+    static constexpr int WR = 8;                   /* w hand-off ring */
+    static constexpr int HALF = 7;                 /* entries [0,HALF) prefetched mid-sample */
+    static constexpr int IMID = 3 + HALF - 1;      /* steps i < IMID consume entries < HALF */
+};
+
+__device__ __forceinline__ int icw_lds_ld(const int *p)
+{
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+/* blocking LDS poll issued by hand: the compiler's own atomic-load lowering placed a
+ * vector-memory drain (s_waitcnt vmcnt(0)) at every poll-loop header, which would wait for the
+ * helper's HBM prefetches each sample */
+__device__ __forceinline__ int icw_poll(unsigned off)
+{
+    int v;
+    asm volatile("ds_read_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(off));
+    return __builtin_amdgcn_readfirstlane(v);
+}
+__device__ __forceinline__ void icw_lds_st(int *p, int v)
+{
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+template <int N, int J, int I>
+__device__ __forceinline__ double icw_pair_prod(const double (&R)[N], const double (&pf)[IcwPair<N>::NE],
+                                                const double (&pc)[20])
+{
+    using P = IcwPair<N>;
+    if constexpr (I < 3 || I >= N - P::KT) return R[(J - 1 - I + 2 * N) % N] * pc[I];
+    else return pf[1 + I - 3];
+}
+
+template <int N, bool KAHAN, int J, int I>
+__device__ __forceinline__ void icw_pair_sum(double &S, double &C, const double (&R)[N],
+                                             const double (&pf)[IcwPair<N>::NE], const double (&pc)[20], int I1)
+{
+    if constexpr (I < N) {
+        if (I < I1) {
+            const double t = icw_pair_prod<N, J, I>(R, pf, pc);
+            if (KAHAN) {
+                const double Y = t - C;
+                const double T = S + Y;
+                C = (T - S) - Y;
+                S = T;
+            } else {
+                S += t;
+            }
+            icw_pair_sum<N, KAHAN, J, I + 1>(S, C, R, pf, pc, I1);
+        }
+    }
+}
+
+/* steps i in [I0, N) starting at template index I0 */
+template <int N, bool KAHAN, int J, int I0>
+__device__ __forceinline__ void icw_pair_range(double &S, double &C, const double (&R)[N],
+                                               const double (&pf)[IcwPair<N>::NE], const double (&pc)[20], int I1)
+{
+    icw_pair_sum<N, KAHAN, J, I0>(S, C, R, pf, pc, I1);
+}
+
+struct IcwPairLds;   /* layout documented in icw_iir_pair */
+
+template <int N, bool KAHAN, bool SUBN, int J>
+__device__ __forceinline__ void icw_pair_sample(double (&R)[N], double (&pf)[IcwPair<N>::NE], const double (&pc)[20],
+                                                unsigned &cnt, const int n, double *prod, double *wring,
+                                                int *chain_done, const int *help_done, const int lane, int *err,
+                                                const unsigned hd_off)
+{
+    using P = IcwPair<N>;
+    /* The poll of help_done is issued by hand at the start of the sample and waited for by hand
+     * in the middle, so its LDS latency hides under the first half of the Kahan chain.  (A plain
+     * load would be sunk by the compiler to its use, with the first half of the sum moved below
+     * the check -- an exposed LDS round trip every sample.)  Extra hand-issued LDS ops only make
+     * the compiler's in-order lgkmcnt waits stronger, never weaker. */
+    int pv;
+    double S = pf[0], C = 0.0;
+    ICW_STAMP(0, n);
+    asm volatile("ds_read_b32 %0, %2" : "=v"(pv), "+v"(S) : "v"(hd_off));
+    icw_pair_range<N, KAHAN, J, 0>(S, C, R, pf, pc, P::IMID);
+    asm volatile("" : "+v"(S), "+v"(C));                       /* first half stays above the check */
+    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(pv) : : "memory");
+    /* mid-sample: slot n+1 must be complete (help_done >= n-2), then prefetch its first half
+     * (x_in and products 3..IMID-1, whose registers were just consumed) */
+    pv = __builtin_amdgcn_readfirstlane(pv);
+    for (int spin = 0; pv < n - 2; ++spin) {          /* bounded: a broken hand-off ends the kernel */
+        if (spin > (1 << 22)) { *err = 1; break; }
+        __builtin_amdgcn_s_sleep(1);
+        pv = icw_poll(hd_off);
+    }
+    ICW_STAMP(1, n);
+    const double *slot = prod + (size_t)((n + 1) % P::RING) * P::NE * 64 + lane;
+#pragma unroll
+    for (int e = 0; e < P::HALF; ++e) pf[e] = slot[e * 64];
+    icw_pair_range<N, KAHAN, J, P::IMID>(S, C, R, pf, pc, N);
+    asm volatile("" : "+v"(S));                                 /* second half above its refill */
+#pragma unroll
+    for (int e = P::HALF; e < P::NE; ++e) pf[e] = slot[e * 64];
+    if (SUBN) {
+        const bool z = fabs(S) < 1.0;
+        cnt += z ? 1u : 0u;
+        S = z ? 0.0 : S;
+    }
+    R[J] = S;
+    /* publish w[n]: LDS operations of one wave are performed in order, so the counter store
+     * cannot overtake the data store; the asm barrier keeps the compiler from reordering them */
+    wring[(n % P::WR) * 64 + lane] = S;
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+    if (lane == 0) icw_lds_st(chain_done, n + 1);
+    ICW_STAMP(2, n);
+}
+
+template <int N, bool KAHAN, bool SUBN, int J0>
+__device__ __forceinline__ void icw_pair_block(double (&R)[N], double (&pf)[IcwPair<N>::NE], const double (&pc)[20],
+                                               unsigned &cnt, const int n0, const int lim, double *prod, double *wring,
+                                               int *chain_done, const int *help_done, const int lane, int *err,
+                                               const unsigned hd_off)
+{
+    if constexpr (J0 < N) {
+        if (J0 < lim) {
+            icw_pair_sample<N, KAHAN, SUBN, J0>(R, pf, pc, cnt, n0 + J0, prod, wring, chain_done, help_done, lane, err,
+                                                hd_off);
+            icw_pair_block<N, KAHAN, SUBN, J0 + 1>(R, pf, pc, cnt, n0, lim, prod, wring, chain_done, help_done, lane,
+                                                   err, hd_off);
+        }
+    }
+}
+
+template <int N, bool KAHAN, bool SUBN>
+__global__ __launch_bounds__(128) void icw_iir_pair(IcwK1Args a)
+{
+    using P = IcwPair<N>;
+    __shared__ double prod[P::RING * P::NE * 64];   /* [slot][entry][lane] */
+    __shared__ double wring[P::WR * 64];             /* [n % WR][lane] */
+    __shared__ int counters[2];                       /* chain_done, help_done */
+    int *chain_done = &counters[0];
+    int *help_done = &counters[1];
+
+    const int lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;
+    const int g0 = blockIdx.x * 64 + lane;
+    const bool valid = g0 < a.n_chains;
+    const int g = valid ? g0 : a.n_chains - 1;
+    const int s = g >> 2, c = (g >> 1) & 1, f = g & 1;
+    const int T = a.T;
+    double pc[20];
+#pragma unroll
+    for (int i = 0; i < 20; ++i) pc[i] = a.pc[i];
+    if (threadIdx.x == 0) {
+        icw_lds_st(chain_done, 0);
+        icw_lds_st(help_done, -0x40000000);
+    }
+    __syncthreads();
+
+    const unsigned ph0 = a.hq_phase[s * 2 + c];
+    if (wave == 1) {
+        /* ------------------------------- helper wave ------------------------------- */
+        const double *xp = a.xd + (size_t)g * a.x_pitch;
+        double *wrow = a.w + (size_t)g * a.w_pitch;
+        double z[N];   /* z[k] = w[-1-k] (history, most recent first) */
+#pragma unroll
+        for (int k = 0; k < N; ++k) z[k] = a.hist[(size_t)g * ICW_HIST_PITCH + k];
+        if (valid) {
+#pragma unroll
+            for (int j = 0; j < N; ++j) wrow[j] = z[N - 1 - j];
+        }
+        /* prefill: products of history w[m] (m = -1-k) for targets n = m+1+i = i-k >= 0 */
+#pragma unroll
+        for (int k = 0; k < N; ++k)
+#pragma unroll
+            for (int i = 3; i < N - P::KT; ++i) {
+                const int n = i - k;
+                if (n >= 0 && n < T) prod[((size_t)(n % P::RING) * P::NE + 1 + i - 3) * 64 + lane] = z[k] * pc[i];
+            }
+#pragma unroll
+        for (int n = 0; n < 4; ++n)
+            if (n < T) prod[((size_t)(n % P::RING) * P::NE) * 64 + lane] = xp[n];
+        __atomic_signal_fence(__ATOMIC_SEQ_CST);
+        if (lane == 0) icw_lds_st(help_done, 0);
+
+        /* All HBM traffic of the helper happens at 16-sample group boundaries (filter inputs
+         * read a group ahead into registers, the group's w[] written back as one 128-B run per
+         * lane), and the per-sample hand-off is branch-free apart from the poll, so the loop
+         * carries no vector-memory waits.  Products for targets >= T land in ring slots whose
+         * previous targets are already consumed, so they are written unconditionally. */
+        constexpr int U = 16;
+        double xa[U], xb[U], wg[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) xa[u] = (4 + u < T) ? xp[4 + u] : 0.0;
+#pragma unroll
+        for (int u = 0; u < U; ++u) xb[u] = (U + 4 + u < T) ? xp[U + 4 + u] : 0.0;
+        int cd = 0;
+        const unsigned cd_off = (unsigned)(uintptr_t)chain_done;
+        for (int m0 = 0; m0 < T; m0 += U) {
+            const int ulim = min(U, T - m0);
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int m = m0 + u;
+                if (u < ulim) {
+                    for (int spin = 0; cd < m + 1; ++spin) {
+                        if (spin > (1 << 24)) { *a.err = 2; return; }
+                        cd = icw_poll(cd_off);
+                    }
+                    ICW_STAMP(3, m);
+                    const double w = wring[(m % P::WR) * 64 + lane];
+                    wg[u] = w;
+                    const int sb = (m + 4) % P::RING;   /* slot of target m+1+i for i = 3 */
+                    double *pb = prod + lane;
+#pragma unroll
+                    for (int i = 3; i < N - P::KT; ++i) {
+                        int sl = sb + (i - 3);
+                        sl = sl >= P::RING ? sl - P::RING : sl;
+                        pb[((size_t)sl * P::NE + 1 + i - 3) * 64] = w * pc[i];
+                    }
+                    pb[((size_t)sb * P::NE) * 64] = xa[u];
+                    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+                    if (lane == 0) icw_lds_st(help_done, m + 1);
+                    ICW_STAMP(4, m);
+                }
+            }
+            if (valid) {
+#pragma unroll
+                for (int u = 0; u < U; ++u)
+                    if (u < ulim) wrow[N + m0 + u] = wg[u];
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) xa[u] = xb[u];
+#pragma unroll
+            for (int u = 0; u < U; ++u) xb[u] = (m0 + 2 * U + 4 + u < T) ? xp[m0 + 2 * U + 4 + u] : 0.0;
+        }
+        return;
+    }
+
+    /* ---------------------------------- chain wave ---------------------------------- */
+    double R[N];
+#pragma unroll
+    for (int i = 0; i < N; ++i) R[N - 1 - i] = a.hist[(size_t)g * ICW_HIST_PITCH + i];
+    for (int spin = 0; __builtin_amdgcn_readfirstlane(icw_lds_ld(help_done)) < 0; ++spin) {
+        if (spin > (1 << 22)) { *a.err = 3; break; }
+        __builtin_amdgcn_s_sleep(1);
+    }
+    double pf[P::NE];
+#pragma unroll
+    for (int e = 0; e < P::NE; ++e) pf[e] = prod[(size_t)e * 64 + lane];
+    const unsigned hd_off = (unsigned)(uintptr_t)help_done;   /* LDS byte offset (flat low bits) */
+    unsigned cnt = 0;
+    int t = 0;
+    for (; t + N <= T; t += N)
+        icw_pair_block<N, KAHAN, SUBN, 0>(R, pf, pc, cnt, t, N, prod, wring, chain_done, help_done, lane, a.err, hd_off);
+    const int rem = T - t;
+    if (rem > 0) {
+        icw_pair_block<N, KAHAN, SUBN, 0>(R, pf, pc, cnt, t, rem, prod, wring, chain_done, help_done, lane, a.err, hd_off);
+        icw_normalise_ring<N>(R, rem);
+    }
+    if (!valid) return;
+    icw_store_hist<N, 0>(R, a.hist, g, a.n_chains);
     a.sncnt[g] += cnt;
     if (f == 0) {
         a.info_phase[s * 2 + c] = ph0;
@@ -560,6 +865,32 @@ static hipError_t launch_k1_t(const IcwK1Args &a, hipStream_t st)
     const int blocks = (a.n_chains + 63) / 64;
     hipLaunchKernelGGL((icw_iir_state<N, K, S>), dim3(blocks), dim3(64), 0, st, a);
     return hipGetLastError();
+}
+
+template <int N, bool K, bool S>
+static hipError_t launch_k1p_t(const IcwK1Args &a, hipStream_t st)
+{
+    const int blocks = (a.n_chains + 63) / 64;
+    hipLaunchKernelGGL((icw_iir_pair<N, K, S>), dim3(blocks), dim3(128), 0, st, a);
+    return hipGetLastError();
+}
+
+template <int N>
+static hipError_t launch_k1p_n(const IcwK1Args &a, bool kahan, bool subn, hipStream_t st)
+{
+    if (kahan) return subn ? launch_k1p_t<N, true, true>(a, st) : launch_k1p_t<N, true, false>(a, st);
+    return subn ? launch_k1p_t<N, false, true>(a, st) : launch_k1p_t<N, false, false>(a, st);
+}
+
+extern "C" hipError_t icw_launch_iir_pair(const IcwK1Args *a, int nord, int kahan, int subn, hipStream_t st)
+{
+    switch (nord) {
+    case 15: return launch_k1p_n<15>(*a, kahan, subn, st);
+    case 18: return launch_k1p_n<18>(*a, kahan, subn, st);
+    case 19: return launch_k1p_n<19>(*a, kahan, subn, st);
+    case 20: return launch_k1p_n<20>(*a, kahan, subn, st);
+    }
+    return hipErrorInvalidValue;
 }
 
 template <int N>

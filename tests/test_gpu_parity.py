@@ -12,6 +12,14 @@ pytestmark = pytest.mark.gpu
 REL_TOL = 1e-6   # north_star: "within 1e-6 relative for the float Hilbert/modulator stages"
 
 
+@pytest.fixture(autouse=True, params=["pair", "plain"])
+def k1_mode(request, monkeypatch):
+    """run every case through both IIR-state kernels: the chain+helper wave pair (few chains per
+    SIMD) and the plain lane-per-chain kernel (throughput regime)"""
+    monkeypatch.setenv("ICW_K1_MODE", request.param)
+    return request.param
+
+
 def run_both(oracle, icw, cfg, nodes, raw, n_frames, blocks=None):
     ctx = icw.Context(cfg, nodes, raw.shape[0])
     if blocks is None:

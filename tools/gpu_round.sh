@@ -13,6 +13,7 @@ step() {   # step <name> <timeout> <cmd...>
 for s in "$@"; do
   case $s in
     probe) step lat_probe 60 ./tools/lat_probe || exit 2 ;;
+    k1probe) step k1_probe 120 ./tools/k1_probe 256 8192 || exit 2 ;;
     test)  step pytest_gpu 900 python -m pytest tests -m gpu -q -x; ok $? || exit 2 ;;
     testall) step pytest_gpu 900 python -m pytest tests -m gpu -q; ok $? || exit 2 ;;
     bench) step bench 600 python bench.py --steps 3 --warmup 1 --no-cpu-baseline || exit 2 ;;
