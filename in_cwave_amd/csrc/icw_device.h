@@ -13,6 +13,7 @@
 #define ICW_MAX_REGS  8      /* value registers: `in`, node outputs, persistent slots */
 #define ICW_K2_TILE   256    /* frames per output-kernel workgroup */
 #define ICW_HIST_PITCH 20    /* doubles per chain in the delay-line state */
+#define ICW_RSTATE    42     /* doubles of render state per channel: prev_rnd, prev_ns_err, E[20], O[20] */
 
 /* Arguments of the input prep kernel (one thread = one frame). */
 struct IcwK0Args {
@@ -81,6 +82,22 @@ struct IcwRenderK {
     int32_t sign_delta, norm_shift, is24;
     int32_t render_type, ns_kind, ns_n;
     double ns_c[40];
+};
+
+/* Arguments of the serial render kernel (one lane = one channel's SOUND_RENDER). */
+struct IcwK3Args {
+    const double *pre;             /* [n_streams][T][2] pre-render values from the output kernel */
+    size_t pre_stride;             /* doubles per stream */
+    int32_t n_streams, T;
+    unsigned char *out;            /* stream s at out + s*out_stride */
+    size_t out_stride;
+    uint32_t *mt;                  /* [624][mt_pitch] MT19937 state words, generator g = s*2 + ch */
+    int32_t *mt_idx;               /* [n_gen] index of the next word (624: twist needed) */
+    double *rs;                    /* [n_gen][ICW_RSTATE]: prev_rnd, prev_ns_err, E[20], O[20] */
+    uint32_t *clips;               /* [n_streams][2] */
+    unsigned long long *peak_bits; /* [n_streams][2] */
+    int32_t n_gen, mt_pitch;
+    IcwRenderK rk;
 };
 
 /* Arguments of the output kernel (frame-parallel: Kahan output sums, unmix, graph, render). */

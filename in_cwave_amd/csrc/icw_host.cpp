@@ -25,6 +25,7 @@
 extern "C" hipError_t icw_launch_unpack(const IcwK0Args *a, hipStream_t st);
 extern "C" hipError_t icw_launch_iir_pair(const IcwK1Args *a, int nord, int kahan, int subn, hipStream_t st);
 extern "C" hipError_t icw_launch_iir_state(const IcwK1Args *a, int nord, int kahan, int subn, hipStream_t st);
+extern "C" hipError_t icw_launch_render(const IcwK3Args *a, hipStream_t st);
 extern "C" hipError_t icw_launch_output(const IcwK2Args *a, int nord, int kahan, hipStream_t st);
 
 #define ICW_PI_H (3.1415926535897932384626433832795029)
@@ -52,6 +53,10 @@ struct DevState {
     uint32_t *clips = nullptr;            /* [streams][2] */
     unsigned long long *peak_bits = nullptr; /* [streams][2] */
     int *err = nullptr;                   /* kernel hand-off timeout flag */
+    /* serial render state (only when the render is not ROUND/flat) */
+    uint32_t *mt = nullptr;               /* [624][2*streams] */
+    int32_t *mt_idx = nullptr;            /* [2*streams] */
+    double *rs = nullptr;                 /* [2*streams][ICW_RSTATE] */
 };
 
 }  // namespace
@@ -84,6 +89,10 @@ struct icw_ctx {
     size_t d_in_bytes = 0, d_out_bytes = 0;
     double *d_pre = nullptr;
     size_t d_pre_bytes = 0;
+    double *rpre = nullptr;               /* per-block pre-render buffer for the serial render */
+    size_t rpre_bytes = 0;
+    bool serial_render = false;
+    uint32_t mt_seed_state[2][624];       /* seeded MT19937 states for L / R (mtrnd_init_seed) */
     hipStream_t stream = nullptr;
     std::vector<hipEvent_t> ev;
     int n_cu = 256;
@@ -294,7 +303,7 @@ int grow(void **p, size_t *cur, size_t need)
 void free_all(icw_ctx *c)
 {
     DevState &s = c->st;
-    void *ptrs[] = {s.err, s.hist, s.sncnt, s.hq_phase, s.pos, s.fade, s.n_frame, s.bus, s.clips, s.peak_bits,
+    void *ptrs[] = {s.mt, s.mt_idx, s.rs, c->rpre, s.err, s.hist, s.sncnt, s.hq_phase, s.pos, s.fade, s.n_frame, s.bus, s.clips, s.peak_bits,
                     c->d_prog, c->w[0], c->w[1], c->xd[0], c->xd[1], c->info_phase[0], c->info_phase[1],
                     c->info_nframe[0], c->info_nframe[1], c->d_in, c->d_out, c->d_pre};
     for (void *p : ptrs)
@@ -374,9 +383,13 @@ int icw_create(const icw_config *cfg, const icw_node *nodes, int n_nodes, int n_
         c->pd[i] = u2d(icw_hb_b[t][i + 1]) / a0;
     }
     render_consts(cfg->render, cfg->need24bits, c->rk);
-    if (!(cfg->render.render_type == ICW_RENDER_ROUND && c->rk.ns_kind == 0)) {
-        delete c;
-        return ICW_EUNSUPPORTED;   /* dithered / noise-shaped render: serial kernel pending */
+    /* ROUND + flat is elementwise (rendered inside the output kernel); every other render keeps
+     * serial per-channel state and runs in the serial render kernel */
+    c->serial_render = !(cfg->render.render_type == ICW_RENDER_ROUND && c->rk.ns_kind == 0);
+    for (int ch = 0; ch < 2; ++ch) {
+        uint32_t *st = c->mt_seed_state[ch];
+        st[0] = ch ? cfg->seed_right : cfg->seed_left;         /* mtrnd_init_seed, mt_jrnd.c:28-47 */
+        for (uint32_t j = 1; j < 624; ++j) st[j] = 1812433253u * (st[j - 1] ^ (st[j - 1] >> 30)) + j;
     }
     c->n_streams = n_streams;
     const size_t S = (size_t)n_streams, C = S * 4;
@@ -392,6 +405,11 @@ int icw_create(const icw_config *cfg, const icw_node *nodes, int n_nodes, int n_
     rc |= dalloc(&s.clips, S * 2);
     rc |= dalloc(&s.peak_bits, S * 2);
     rc |= dalloc(&s.err, 1);
+    if (c->serial_render) {
+        rc |= dalloc(&s.mt, (size_t)624 * S * 2);
+        rc |= dalloc(&s.mt_idx, S * 2);
+        rc |= dalloc(&s.rs, S * 2 * ICW_RSTATE);
+    }
     for (int p = 0; p < 2; ++p) {
         rc |= dalloc(&c->info_phase[p], S * 2);
         rc |= dalloc(&c->info_nframe[p], S);
@@ -463,6 +481,21 @@ int icw_stream_init(icw_ctx *c, int first, int count)
     std::vector<long long> fd(n * 3);
     for (size_t i = 0; i < n; ++i) { fd[i * 3] = (long long)1 << 62; fd[i * 3 + 1] = 0; fd[i * 3 + 2] = 0; }
     ok &= hipMemcpyAsync(s.fade + f * 3, fd.data(), fd.size() * sizeof(long long), hipMemcpyHostToDevice, st) == hipSuccess;
+    /* host sources of async copies live until the synchronize below */
+    std::vector<uint32_t> col;
+    std::vector<int32_t> idx;
+    if (c->serial_render) {
+        /* renders re-seeded (mod_context_init -> sound_render_init, in_cwave.c:69-70) */
+        const size_t G = (size_t)c->n_streams * 2;
+        col.resize((size_t)624 * n * 2);
+        for (int i = 0; i < 624; ++i)
+            for (size_t k = 0; k < n * 2; ++k) col[(size_t)i * n * 2 + k] = c->mt_seed_state[k & 1][i];
+        ok &= hipMemcpy2DAsync(s.mt + f * 2, G * 4, col.data(), n * 2 * 4, n * 2 * 4, 624, hipMemcpyHostToDevice,
+                               st) == hipSuccess;
+        idx.assign(n * 2, 624);
+        ok &= hipMemcpyAsync(s.mt_idx + f * 2, idx.data(), idx.size() * 4, hipMemcpyHostToDevice, st) == hipSuccess;
+        ok &= hipMemsetAsync(s.rs + f * 2 * ICW_RSTATE, 0, n * 2 * ICW_RSTATE * sizeof(double), st) == hipSuccess;
+    }
     ok &= hipStreamSynchronize(st) == hipSuccess;
     for (size_t i = f * 2; i < (f + n) * 2; ++i) c->peak_db[i] = ICW_SR_ZERO_SIGNAL_DB;
     return ok ? ICW_OK : ICW_EDEVICE;
@@ -493,7 +526,10 @@ int icw_stream_open(icw_ctx *c, int s, int64_t n_samples, uint32_t fade_in, uint
         ok &= hipMemset(c->st.sncnt + (size_t)s * 4, 0, 4 * sizeof(unsigned long long)) == hipSuccess;
         ok &= hipMemset(c->st.hq_phase + (size_t)s * 2, 0, 2 * sizeof(uint32_t)) == hipSuccess;
     }
-    /* sound_render_set_outbits -> recalc: ROUND/flat keeps no shaping state on this path */
+    /* sound_render_set_outbits -> sound_render_recalc: prev_rnd, shaper buffers and prev_ns_err
+     * reset, the RNG is not (sound_render.c:527-580) */
+    if (c->serial_render)
+        ok &= hipMemset(c->st.rs + (size_t)s * 2 * ICW_RSTATE, 0, 2 * ICW_RSTATE * sizeof(double)) == hipSuccess;
     return ok ? ICW_OK : ICW_EDEVICE;
 }
 
@@ -575,6 +611,8 @@ int icw_process_streams(icw_ctx *c, int first, int count, const void *in, size_t
         if (grow((void **)&c->w[p], &c->w_bytes[p], S * 4 * w_pitch * sizeof(double))) return ICW_ENOMEM;
         if (grow((void **)&c->xd[p], &c->xd_bytes[p], S * 4 * x_pitch * sizeof(double))) return ICW_ENOMEM;
     }
+    if (c->serial_render && !d_pre && grow((void **)&c->rpre, &c->rpre_bytes, S * (size_t)Tb * 2 * sizeof(double)))
+        return ICW_ENOMEM;
     hipStream_t st2 = c->stream2;
     /* second stream starts after everything already queued on st (inputs, previous calls) */
     if (hipEventRecord(c->join, st) != hipSuccess || hipStreamWaitEvent(st2, c->join, 0) != hipSuccess)
@@ -661,8 +699,11 @@ int icw_process_streams(icw_ctx *c, int first, int count, const void *in, size_t
         if (d_pre) {
             a2.pre = d_pre + (size_t)t0 * 2;
             a2.pre_stride = (size_t)n_frames * 2;
+        } else if (c->serial_render) {
+            a2.pre = c->rpre;
+            a2.pre_stride = (size_t)T * 2;
         }
-        a2.do_render = 1;
+        a2.do_render = c->serial_render ? 0 : 1;
         a2.clips = ds.clips + f0 * 2;
         a2.peak_bits = ds.peak_bits + f0 * 2;
         a2.rk = c->rk;
@@ -671,6 +712,25 @@ int icw_process_streams(icw_ctx *c, int first, int count, const void *in, size_t
         a2.d0 = c->d0;
         if (timing) hipEventRecord(c->ev[4 * b + 2], st2);
         if (icw_launch_output(&a2, N, cfg.iir_kahan, st2) != hipSuccess) return ICW_EDEVICE;
+        if (c->serial_render) {
+            IcwK3Args a3;
+            memset(&a3, 0, sizeof(a3));
+            a3.pre = a2.pre;
+            a3.pre_stride = a2.pre_stride;
+            a3.n_streams = count;
+            a3.T = T;
+            a3.out = a2.out;
+            a3.out_stride = dos;
+            a3.mt = ds.mt + f0 * 2;          /* column offset: [624][G] layout, pitch G */
+            a3.mt_idx = ds.mt_idx + f0 * 2;
+            a3.rs = ds.rs + f0 * 2 * ICW_RSTATE;
+            a3.clips = ds.clips + f0 * 2;
+            a3.peak_bits = ds.peak_bits + f0 * 2;
+            a3.n_gen = count * 2;
+            a3.mt_pitch = c->n_streams * 2;
+            a3.rk = c->rk;
+            if (icw_launch_render(&a3, st2) != hipSuccess) return ICW_EDEVICE;
+        }
         if (timing) hipEventRecord(c->ev[4 * b + 3], st2);
         if (hipEventRecord(c->k2done[p], st2) != hipSuccess) return ICW_EDEVICE;
     }

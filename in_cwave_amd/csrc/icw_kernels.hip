@@ -858,6 +858,153 @@ __global__ __launch_bounds__(ICW_K2_TILE) void icw_output(IcwK2Args a)
     }
 }
 
+/* ------------------------------------------------------ serial render kernel (K3) ------ */
+/* sound_render_value (sound_render.c:691-809) for the dithered / noise-shaped renders, whose
+ * state (MT19937 position, sloped-TPDF memory, noise-shaper feedback) is serial per channel:
+ * one lane per channel, the channel's MT19937 state held in LDS ([624][64] words, 156 KB: the
+ * twist of mt_jrnd.c:99-124 runs in place per lane), shaper history in registers as shift
+ * registers (age 0 = newest, identical sums to the ring of ns_fir/ns_iir, sound_render.c:403-489). */
+__device__ __forceinline__ uint32_t icw_mt_twist_word(uint32_t u, uint32_t v)
+{
+    const uint32_t y = (u & 0x80000000u) | (v & 0x7fffffffu);
+    return (y >> 1) ^ ((v & 1u) ? 0x9908b0dfu : 0u);
+}
+
+__device__ __forceinline__ void icw_mt_regen(uint32_t *mt, int lane)
+{
+    /* in-place generation of the next 624 words (mtrnd_gen_ui32, mt_jrnd.c:105-120) */
+    for (int i = 0; i < 227; ++i)
+        mt[i * 64 + lane] = mt[(i + 397) * 64 + lane] ^ icw_mt_twist_word(mt[i * 64 + lane], mt[(i + 1) * 64 + lane]);
+    for (int i = 227; i < 623; ++i)
+        mt[i * 64 + lane] = mt[(i - 227) * 64 + lane] ^ icw_mt_twist_word(mt[i * 64 + lane], mt[(i + 1) * 64 + lane]);
+    mt[623 * 64 + lane] = mt[396 * 64 + lane] ^ icw_mt_twist_word(mt[623 * 64 + lane], mt[lane]);
+}
+
+__device__ __forceinline__ uint32_t icw_mt_u32(uint32_t *mt, int lane, int &idx)
+{
+    if (idx >= 624) {
+        icw_mt_regen(mt, lane);
+        idx = 0;
+    }
+    uint32_t y = mt[idx * 64 + lane];
+    ++idx;
+    y ^= (y >> 11);
+    y ^= (y << 7) & 0x9d2c5680u;
+    y ^= (y << 15) & 0xefc60000u;
+    y ^= (y >> 18);
+    return y;
+}
+
+/* mtrnd_gen_dsopen (mt_jrnd.c:218-256): (-1, 1) with 53-bit resolution, +-1 rejected */
+__device__ __forceinline__ double icw_mt_dsopen(uint32_t *mt, int lane, int &idx)
+{
+    double r;
+    do {
+        const uint32_t a = icw_mt_u32(mt, lane, idx) >> 5;
+        const uint32_t b = icw_mt_u32(mt, lane, idx) >> 6;
+        r = ((a * 67108864.0 + b) * (1.0 / 9007199254740992.0)) * 2.0 - 1.0;
+    } while (-1.0 == r || 1.0 == r);
+    return r;
+}
+
+#define ICW_SQRT6 (2.4494897427831780981972840747059)
+
+template <int KIND>
+__global__ __launch_bounds__(64) void icw_render_serial(IcwK3Args a)
+{
+    __shared__ uint32_t mt[624 * 64];
+    const int lane = threadIdx.x;
+    const int g0 = blockIdx.x * 64 + lane;
+    const bool valid = g0 < a.n_gen;
+    const int g = valid ? g0 : a.n_gen - 1;
+    const int s = g >> 1, ch = g & 1;
+    for (int i = 0; i < 624; ++i) mt[i * 64 + lane] = a.mt[(size_t)i * a.mt_pitch + g];
+    int idx = a.mt_idx[g];
+    double *rs = a.rs + (size_t)g * ICW_RSTATE;
+    double prev_rnd = rs[0], prev_err = rs[1];
+    constexpr int NM = ICW_MAX_NS_TAPS;
+    double E[NM], O[NM];
+#pragma unroll
+    for (int i = 0; i < NM; ++i) { E[i] = rs[2 + i]; O[i] = rs[2 + NM + i]; }
+    const IcwRenderK &k = a.rk;
+    const int nn = k.ns_n;
+    const int osz = k.is24 ? 3 : 2;
+    const double *pp = a.pre + (size_t)s * a.pre_stride + ch;
+    unsigned char *op = a.out + (size_t)s * a.out_stride + (size_t)ch * osz;
+    unsigned clips = 0;
+    double pk = 0.0;
+    for (int t = 0; t < a.T; ++t) {
+        double input = pp[(size_t)t * 2];
+        double rnd = 0.0, tr;
+        switch (k.render_type) {
+        case ICW_RENDER_RPDF: rnd = icw_mt_dsopen(mt, lane, idx) / ICW_SQRT2; break;
+        case ICW_RENDER_TPDF:
+            rnd = icw_mt_dsopen(mt, lane, idx);
+            rnd += icw_mt_dsopen(mt, lane, idx);
+            rnd /= 2.0;
+            break;
+        case ICW_RENDER_STPDF:
+            rnd = ((tr = icw_mt_dsopen(mt, lane, idx)) - prev_rnd) / 2.0;
+            prev_rnd = tr;
+            break;
+        case ICW_RENDER_GAUSS:
+            rnd = icw_mt_dsopen(mt, lane, idx);
+            for (int i = 1; i < 12; ++i) rnd += icw_mt_dsopen(mt, lane, idx);
+            rnd /= (2.0 * ICW_SQRT6);
+            break;
+        default: break;
+        }
+        input = (input * k.norm_mul) - prev_err;
+        double q = input + (rnd * k.dth_mul);
+        int delta;
+        if (q < 0.0) { q -= k.round_offset; delta = k.sign_delta; }
+        else { q += k.round_offset; delta = 0; }
+        const double aq = fabs(q);
+        pk = aq > pk ? aq : pk;
+        if (q >= k.hi) { q = k.hi - 1.0; ++clips; }
+        if (q <= k.lo) { q = k.lo + 1.0; ++clips; }
+        int val = (isnan(q) ? (int)0x80000000 : (int)q) + delta;
+        /* noise shaping for the next sample (ns_empty / ns_fir / ns_iir) */
+        const double ev = (double)val - input;
+        double res = 0.0;
+        if (KIND == 1) {
+#pragma unroll
+            for (int i = NM - 1; i > 0; --i) E[i] = E[i - 1];
+            E[0] = ev;
+#pragma unroll
+            for (int i = 0; i < NM; ++i)
+                if (i < nn) res += k.ns_c[i] * E[i];
+        } else if (KIND == 2) {
+#pragma unroll
+            for (int i = NM - 1; i > 0; --i) E[i] = E[i - 1];
+            E[0] = ev;
+#pragma unroll
+            for (int i = 0; i < NM; ++i)
+                if (i < nn) res += k.ns_c[i] * E[i] - k.ns_c[i + nn] * O[i];
+#pragma unroll
+            for (int i = NM - 1; i > 0; --i) O[i] = O[i - 1];
+            O[0] = res;
+        }
+        prev_err = res;
+        val <<= k.norm_shift;
+        if (valid) {
+            unsigned char *o = op + (size_t)t * 2 * osz;
+            o[0] = (unsigned char)val;
+            o[1] = (unsigned char)(val >> 8);
+            if (k.is24) o[2] = (unsigned char)(val >> 16);
+        }
+    }
+    if (!valid) return;
+    for (int i = 0; i < 624; ++i) a.mt[(size_t)i * a.mt_pitch + g] = mt[i * 64 + lane];
+    a.mt_idx[g] = idx;
+    rs[0] = prev_rnd;
+    rs[1] = prev_err;
+#pragma unroll
+    for (int i = 0; i < NM; ++i) { rs[2 + i] = E[i]; rs[2 + NM + i] = O[i]; }
+    if (clips) atomicAdd(&a.clips[g], clips);
+    if (pk > 0.0) atomicMax(&a.peak_bits[g], (unsigned long long)__double_as_longlong(pk));
+}
+
 /* ---------------------------------------------------------------- launch wrappers ------- */
 template <int N, bool K, bool S>
 static hipError_t launch_k1_t(const IcwK1Args &a, hipStream_t st)
@@ -923,6 +1070,17 @@ static hipError_t launch_k2_t(const IcwK2Args &a, hipStream_t st)
 {
     dim3 grid((a.T + ICW_K2_TILE - 1) / ICW_K2_TILE, a.n_streams);
     hipLaunchKernelGGL((icw_output<N, K>), grid, dim3(ICW_K2_TILE), 0, st, a);
+    return hipGetLastError();
+}
+
+extern "C" hipError_t icw_launch_render(const IcwK3Args *a, hipStream_t st)
+{
+    const int blocks = (a->n_gen + 63) / 64;
+    switch (a->rk.ns_kind) {
+    case 0: hipLaunchKernelGGL(icw_render_serial<0>, dim3(blocks), dim3(64), 0, st, *a); break;
+    case 1: hipLaunchKernelGGL(icw_render_serial<1>, dim3(blocks), dim3(64), 0, st, *a); break;
+    default: hipLaunchKernelGGL(icw_render_serial<2>, dim3(blocks), dim3(64), 0, st, *a); break;
+    }
     return hipGetLastError();
 }
 

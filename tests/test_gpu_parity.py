@@ -110,3 +110,68 @@ def test_input_formats(oracle, icw, fmt, ch):
     raw = synth.batch_pcm(3, 2000, 44100, channels=ch, fmt=fmt)
     _, out, pre, ro, rp = run_both(oracle, icw, cfg, graph.graph_master_only(), raw, 2000)
     assert_parity(out, pre, ro, rp, 3, exact_pre=True)
+
+
+@pytest.mark.parametrize("rtype", [abi.RENDER_ROUND, abi.RENDER_RPDF, abi.RENDER_TPDF, abi.RENDER_STPDF,
+                                   abi.RENDER_GAUSS])
+@pytest.mark.parametrize("quantz", [abi.QUANTZ_MID_TREAD, abi.QUANTZ_MID_RISER])
+@pytest.mark.parametrize("is24", [False, True])
+def test_render_matrix(oracle, icw, rtype, quantz, is24):
+    """sound_render_value: every render type x quantiser x 16/24 bit, flat and F-weighted shaper"""
+    for ns in (abi.NSHAPE_FLAT, abi.NSHAPE_FW44):
+        cfg = graph.default_config(44100, need24bits=is24)
+        cfg.render.render_type, cfg.render.quantz_type, cfg.render.nshape_type = rtype, quantz, ns
+        cfg.render.dth_bits = 1.5
+        raw = synth.batch_pcm(3, 1500, 44100)
+        ctx, out, pre, ro, rp = run_both(oracle, icw, cfg, graph.graph_master_only(), raw, 1500,
+                                         blocks=[700, 800])
+        assert_parity(out, pre, ro, rp, 3 if is24 else 2, exact_pre=True)
+
+
+@pytest.mark.parametrize("ns", list(range(abi.NSHAPE_MAX + 1)))
+def test_every_noise_shaper(oracle, icw, ns):
+    cfg = graph.default_config(48000, need24bits=(ns % 2 == 1))
+    cfg.render.render_type = abi.RENDER_TPDF
+    cfg.render.nshape_type = ns
+    raw = synth.batch_pcm(2, 1200, 48000)
+    _, out, pre, ro, rp = run_both(oracle, icw, cfg, graph.graph_master_only(), raw, 1200)
+    assert_parity(out, pre, ro, rp, 3 if ns % 2 == 1 else 2, exact_pre=True)
+
+
+@pytest.mark.parametrize("bits", [(16, 2), (16, 11), (24, 18), (24, 5)])
+def test_sign_bits_reduction(oracle, icw, bits):
+    width, sb = bits
+    cfg = graph.default_config(48000, need24bits=(width == 24))
+    if width == 24:
+        cfg.render.sign_bits24 = sb
+    else:
+        cfg.render.sign_bits16 = sb
+    cfg.render.render_type = abi.RENDER_STPDF
+    raw = synth.batch_pcm(2, 1000, 48000)
+    _, out, pre, ro, rp = run_both(oracle, icw, cfg, graph.graph_master_only(), raw, 1000)
+    assert_parity(out, pre, ro, rp, 3 if width == 24 else 2, exact_pre=True)
+
+
+def test_c5_shape_tpdf_mew44_24bit(oracle, icw):
+    """BASELINE C5: 192 kHz float32 stereo, Hilbert + Master, 24-bit TPDF (1 bit) + MEW44 shaper"""
+    cfg = graph.default_config(192000, fmt=abi.FMT_F32, need24bits=True)
+    cfg.render.render_type = abi.RENDER_TPDF
+    cfg.render.nshape_type = abi.NSHAPE_MEW44
+    raw = synth.batch_pcm(4, 3000, 192000, fmt=abi.FMT_F32)
+    ctx, out, pre, ro, rp = run_both(oracle, icw, cfg, graph.graph_master_only(), raw, 3000)
+    assert_parity(out, pre, ro, rp, 3, exact_pre=True)
+
+
+def test_meters_match_oracle(oracle, icw):
+    cfg = graph.default_config(48000)
+    cfg.render.render_type = abi.RENDER_TPDF
+    raw = synth.batch_pcm(3, 2000, 48000)
+    nodes = [graph.master(gain=2.0)]            # drive into clipping
+    ctx = icw.Context(cfg, nodes, 3)
+    ctx.process(raw, 2000)
+    for s in range(3):
+        st = oracle.Stream(cfg, nodes)
+        st.process(raw[s], 2000)
+        m, r = ctx.meters(s), st.meters()
+        assert m["clips"] == r["clips"] and m["desubnorm"] == r["desubnorm"]
+        assert m["peak_db"] == r["peak_db"]
