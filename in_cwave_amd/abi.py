@@ -71,6 +71,16 @@ SIGNATURES = {
     "icw_stream_open": (_i, [_vp, _i, C.c_int64, C.c_uint32, C.c_uint32, C.c_uint32, _i, _i]),
     "icw_stream_reset_hilbert": (_i, [_vp, _i]),
     "icw_stream_reset_framecnt": (_i, [_vp, _i]),
+    "icw_stream_seek": (_i, [_vp, _i, C.c_int64]),
+    "icw_set_input": (_i, [_vp, C.c_uint32, C.c_uint32, C.c_uint32]),
+    "icw_mod_context_create": (_vp, [C.POINTER(Config), C.POINTER(Node), _i, _i, C.POINTER(_i)]),
+    "icw_mod_context_destroy": (None, [_vp]),
+    "icw_mod_context_fopen": (_i, [_vp, C.c_uint32, C.c_uint32, C.c_uint32, C.c_int64, C.c_uint32, C.c_uint32,
+                                   C.c_uint32, _i, _i]),
+    "icw_amod_process_samples": (_i, [_vp, _vp, _vp, _u]),
+    "icw_mod_context_seek": (_i, [_vp, C.c_int64, _i]),
+    "icw_mod_context_out_size": (_i, [_vp]),
+    "icw_mod_context_meters": (_i, [_vp, _i, C.POINTER(Meters)]),
     "icw_process_batch": (_i, [_vp, _vp, _sz, _vp, _sz, _i, _u, _vp, _vp]),
     "icw_process_streams": (_i, [_vp, _i, _i, _vp, _sz, _vp, _sz, _i, _u, _vp, _vp]),
     "icw_synchronize": (_i, [_vp]),

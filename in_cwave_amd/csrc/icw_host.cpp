@@ -552,6 +552,28 @@ int icw_stream_reset_framecnt(icw_ctx *c, int s)
     return hipMemset(c->st.n_frame + s, 0, sizeof(unsigned long long)) == hipSuccess ? ICW_OK : ICW_EDEVICE;
 }
 
+int icw_stream_seek(icw_ctx *c, int s, int64_t frame_pos)
+{
+    if (!c || s < 0 || s >= c->n_streams || frame_pos < 0) return ICW_EINVAL;
+    std::lock_guard<std::mutex> lk(c->mu);
+    if (set_dev(c)) return ICW_EDEVICE;
+    long long v = (long long)frame_pos;
+    bool ok = hipStreamSynchronize(c->stream) == hipSuccess;
+    ok &= hipMemcpy(c->st.pos + s, &v, sizeof(v), hipMemcpyHostToDevice) == hipSuccess;
+    return ok ? ICW_OK : ICW_EDEVICE;
+}
+
+int icw_set_input(icw_ctx *c, uint32_t sample_rate, uint32_t fmt, uint32_t channels)
+{
+    if (!c || sample_rate == 0 || sample_rate > ICW_MAX_FS_SRC || fmt > ICW_FMT_F32 || channels == 0) return ICW_EINVAL;
+    std::lock_guard<std::mutex> lk(c->mu);
+    if (set_dev(c) || hipStreamSynchronize(c->stream) != hipSuccess) return ICW_EDEVICE;
+    c->cfg.sample_rate = sample_rate;
+    c->cfg.in_format = fmt;
+    c->cfg.in_channels = channels;
+    return ICW_OK;
+}
+
 int icw_render_size(const icw_ctx *c) { return c ? (c->cfg.need24bits ? 3 : 2) : ICW_EINVAL; }
 
 int icw_process_streams(icw_ctx *c, int first, int count, const void *in, size_t in_stride, void *out,

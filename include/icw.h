@@ -162,6 +162,12 @@ int icw_stream_open(icw_ctx *ctx, int s, int64_t n_samples, uint32_t fade_in_ms,
                     uint32_t fade_out_ms, uint32_t sec_align, int clr_nframe, int clr_hilb);
 int icw_stream_reset_hilbert(icw_ctx *ctx, int s);
 int icw_stream_reset_framecnt(icw_ctx *ctx, int s);
+/* reader seek (xwave_seek_samples, xwave_reader.c:752-785): frame position inside the track,
+ * virtual tail included, from which fades are evaluated */
+int icw_stream_seek(icw_ctx *ctx, int s, int64_t frame_pos);
+/* input format of the next blocks (a new track, mod_context_fopen): sample rate, ICW_FMT_*,
+ * channels; applies to every stream of the context */
+int icw_set_input(icw_ctx *ctx, uint32_t sample_rate, uint32_t fmt, uint32_t channels);
 
 /* Process n_frames frames of every stream (the batched amod_process_samples).
  *   in  : stream s starts at (char*)in  + s*in_stride_bytes,  frames interleaved by channel
