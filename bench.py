@@ -27,6 +27,14 @@ ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT))
 
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+CLOCK_GHZ = 2.4                # MI355X max engine clock (MI355X_MICROARCH.md chip table)
+# Issue floor of icw_iir_state (DESIGN.md "Roofline"): one wave issues ~one FP64 VALU instruction
+# per 4.7 cycles whether or not they depend on each other (profiles/r01_fp64_latency_probe.txt),
+# and the order-19 Kahan chain costs 19 mul + 73 add + 3 reject + 5 bookkeeping = 100 VALU per
+# sample in the compiled loop (ISA listing) -> ~470 cycles per sample per chain.
+K1_VALU_PER_SAMPLE = 100
+CYC_PER_FP64_VALU = 4.7
+PMC_FILE = ROOT / "profiles" / "r01_c2_pmc.json"
 FP64_PEAK_TFLOPS = 78.6        # MI355X FP64 vector (256 CU x 2.4 GHz x 128 flop/clk), vendor figure
 ALG_BYTES_PER_FRAME = 8        # C2 = 4 B in (2 x int16) + 4 B out (2 x int16)
 
@@ -147,9 +155,21 @@ def main():
     k2_avg_s = k2_ms / 1e3 / max(1, k2_n)
     achieved = ALG_BYTES_PER_FRAME * frames_per_launch / k1_avg_s / 1e9 if k1_avg_s > 0 else None
     flops_per_frame = 4 * 2 * (15 * 19 - 4) / 2    # the recurrence half of 1124 flops/frame
+    traffic = None
+    try:   # HBM bytes per launch of the same kernel/config from the committed PMC passes
+        pmc = json.loads(PMC_FILE.read_text())
+        if int(pmc["frames_per_launch"]) == int(frames_per_launch):
+            traffic = next(v["hbm_bytes_corrected"] for k, v in pmc["kernels"].items() if "icw_iir_state" in k)
+    except Exception:
+        traffic = None
+    samples_per_chain = frames_per_launch / S
+    issue_floor_ms = samples_per_chain * K1_VALU_PER_SAMPLE * CYC_PER_FP64_VALU / (CLOCK_GHZ * 1e6)
     roof = {
         "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-        "frac": (achieved / HBM_PEAK_GBS) if achieved else None, "traffic": None,
+        "frac": (achieved / HBM_PEAK_GBS) if achieved else None, "traffic": traffic,
+        "issue_bound": {"valu_per_sample": K1_VALU_PER_SAMPLE, "cycles_per_valu": CYC_PER_FP64_VALU,
+                        "clock_ghz": CLOCK_GHZ, "floor_ms_per_launch": issue_floor_ms,
+                        "frac": (issue_floor_ms / (k1_avg_s * 1e3)) if k1_avg_s else None},
         "kernel": "icw_iir_state", "alg_bytes_per_frame": ALG_BYTES_PER_FRAME,
         "frames_per_launch": frames_per_launch, "avg_launch_ms": k1_avg_s * 1e3,
         "output_kernel_avg_launch_ms": k2_avg_s * 1e3,

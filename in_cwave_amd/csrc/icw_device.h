@@ -117,6 +117,7 @@ struct IcwK2Args {
     double *pre;                   /* nullable [n_streams][T][2] pre-render doubles */
     size_t pre_stride;             /* in doubles, per stream */
     int32_t do_render;             /* elementwise ROUND/flat render in this kernel */
+    int32_t n_regs;                /* DSP value registers (sizes the dynamic LDS register file) */
     uint32_t *clips;               /* [n_streams][2] */
     unsigned long long *peak_bits; /* [n_streams][2] max |q| as ordered bits */
     IcwRenderK rk;

@@ -726,6 +726,7 @@ int icw_process_streams(icw_ctx *c, int first, int count, const void *in, size_t
             a2.pre_stride = (size_t)T * 2;
         }
         a2.do_render = c->serial_render ? 0 : 1;
+        a2.n_regs = c->prog.n_regs;
         a2.clips = ds.clips + f0 * 2;
         a2.peak_bits = ds.peak_bits + f0 * 2;
         a2.rk = c->rk;
