@@ -49,7 +49,7 @@ def parse():
     ap.add_argument("--fs", type=int, default=48000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-workers", type=int, default=16)
-    ap.add_argument("--cpu-frames", type=int, default=1 << 23)
+    ap.add_argument("--cpu-frames", type=int, default=1 << 25)
     return ap.parse_args()
 
 
