@@ -14,7 +14,11 @@ S_ADD_REIM, S_SUB_REIM, S_RE, S_IM = 0, 1, 2, 3
 XCH_NORMAL, XCH_SWAP, XCH_LEFTONLY, XCH_RIGHTONLY, XCH_MIXLR = 0, 1, 2, 3, 4
 # input formats (HRW_FMT_*)
 FMT_U8, FMT_I16, FMT_I24, FMT_I32, FMT_F32 = 0, 1, 2, 3, 4
-FMT_BYTES = {FMT_U8: 1, FMT_I16: 2, FMT_I24: 3, FMT_I32: 4, FMT_F32: 4}
+# complex CWAVE formats: ICW_FMT_CW_F64 + HCW_FMT_* (cwave.h:70-80), Hilbert bypassed
+FMT_CW_F64, FMT_CW_I16, FMT_CW_I16_F32, FMT_CW_F32 = 5, 6, 7, 8
+FMT_BYTES = {FMT_U8: 1, FMT_I16: 2, FMT_I24: 3, FMT_I32: 4, FMT_F32: 4,
+             FMT_CW_F64: 16, FMT_CW_I16: 4, FMT_CW_I16_F32: 6, FMT_CW_F32: 8}
+CW_FORMATS = (FMT_CW_F64, FMT_CW_I16, FMT_CW_I16_F32, FMT_CW_F32)
 # render (sound_render.h)
 QUANTZ_MID_TREAD, QUANTZ_MID_RISER = 0, 1
 RENDER_ROUND, RENDER_RPDF, RENDER_TPDF, RENDER_STPDF, RENDER_GAUSS = 0, 1, 2, 3, 4

@@ -9,11 +9,14 @@
 #include <stddef.h>
 #include <stdint.h>
 
-#define ICW_MAX_OPS   16     /* compiled DSP ops (nodes) per graph on the device path */
+#define ICW_MAX_OPS   64     /* DSP ops (nodes) per graph on the device path */
+#define ICW_MAX_REG_OPS 16   /* ops of a graph the frame-parallel register program accepts */
 #define ICW_MAX_REGS  8      /* value registers: `in`, node outputs, persistent slots */
 #define ICW_K2_TILE   256    /* frames per output-kernel workgroup */
 #define ICW_HIST_PITCH 20    /* doubles per chain in the delay-line state */
 #define ICW_RSTATE    42     /* doubles of render state per channel: prev_rnd, prev_ns_err, E[20], O[20] */
+
+struct IcwProg;
 
 /* Arguments of the input prep kernel (one thread = one frame). */
 struct IcwK0Args {
@@ -24,8 +27,35 @@ struct IcwK0Args {
     const long long *pos;          /* [n_streams] reader position (frames into track) */
     const long long *fade;         /* [n_streams][3] n_samples, n_fade_in, n_fade_out */
     const uint32_t *hq_phase;      /* [n_streams][2] Hilbert phase at block start */
-    double *xd;                    /* [n_chains][x_pitch]: each chain's own filter input sequence */
+    double *xd;                    /* [n_chains][x_pitch]: each chain's own filter input sequence;
+                                      complex input: rows s*4 + ch*2 + {0: I, 1: Q} hold the samples */
     size_t x_pitch;
+};
+
+/* Arguments of the block bookkeeping kernel for complex input (no Hilbert): one thread per stream. */
+struct IcwAdvArgs {
+    int32_t n_streams, T;
+    const uint32_t *hq_phase;
+    long long *pos;
+    unsigned long long *n_frame;
+    unsigned long long ssr;
+    int32_t scaled;
+    uint32_t *info_phase;
+    unsigned long long *info_nframe;
+};
+
+/* Arguments of the serial graph kernel (bus form; one lane = one stream, loops over frames). */
+struct IcwK4Args {
+    const double *iq;              /* [n_streams][T][4] `in` per frame (lre, lim, rre, rim) */
+    int32_t n_streams, T;
+    const unsigned long long *info_nframe;
+    unsigned long long ssr;
+    int32_t scaled;
+    uint32_t sample_rate;
+    const IcwProg *prog;
+    double *bus;                   /* [n_streams][27][4] */
+    double *pre;                   /* [n_streams][pre_stride] (lOut, rOut) per frame */
+    size_t pre_stride;
 };
 
 /* Arguments of the IIR state kernel (one lane = one DF-II chain). */
@@ -55,6 +85,8 @@ struct IcwOp {
     int32_t n_in;                  /* inputs, in bus-slot order */
     int32_t in_reg[27];            /* value register each input resolves to */
     int32_t out_reg;               /* register the node's output lands in (not MASTER) */
+    uint32_t in_mask;              /* bus-program form: bit k = reads bus slot k */
+    int32_t out_slot;              /* bus-program form: slot written (n_out) */
     int32_t xch, iqinv[2];
     int32_t tout[2];
     int32_t act[2];                /* is_shift / is_pm per channel */
@@ -64,14 +96,19 @@ struct IcwOp {
     double pp[2], lp[2], fa[2];    /* PM: fphase*PI, flevel*PI, fangle */
 };
 
+/* A compiled DSP list.  Register form (frame-parallel output kernel): every slot read resolves at
+ * compile time to `in`, an earlier op of the same frame or a never-written (constant) slot.  Bus
+ * form (serial graph kernel, is_bus = 1): the reference's own bus semantics, for lists that read a
+ * slot before it is written in the frame -- a one-frame delay, feedback included. */
 struct IcwProg {
     int32_t n_ops;
+    int32_t is_bus;
     int32_t n_regs;
     int32_t bypass;                /* am.is_bypass_list: only the Master, on raw `in` */
     int32_t n_persist;             /* slots read before any write in the frame and never written */
     int32_t persist_reg[ICW_MAX_REGS], persist_slot[ICW_MAX_REGS];
     int32_t n_wb;                  /* slots written in the frame: final value -> persistent bus */
-    int32_t wb_reg[ICW_MAX_REGS + ICW_MAX_OPS], wb_slot[ICW_MAX_REGS + ICW_MAX_OPS];
+    int32_t wb_reg[ICW_MAX_REGS + ICW_MAX_REG_OPS], wb_slot[ICW_MAX_REGS + ICW_MAX_REG_OPS];
     IcwOp ops[ICW_MAX_OPS];
 };
 
@@ -122,6 +159,10 @@ struct IcwK2Args {
     unsigned long long *peak_bits; /* [n_streams][2] max |q| as ordered bits */
     IcwRenderK rk;
     double pc[20], pd[20], d0;
+    const double *xin;             /* complex input: K0's I/Q rows (then w is unused) */
+    size_t x_pitch;
+    int32_t cw;
+    double *iq_out;                /* bus-form graph: write `in` here [n_streams][T][4], skip the rest */
 };
 
 #endif

@@ -27,6 +27,8 @@ extern "C" hipError_t icw_launch_iir_pair(const IcwK1Args *a, int nord, int kaha
 extern "C" hipError_t icw_launch_iir_state(const IcwK1Args *a, int nord, int kahan, int subn, hipStream_t st);
 extern "C" hipError_t icw_launch_render(const IcwK3Args *a, hipStream_t st);
 extern "C" hipError_t icw_launch_output(const IcwK2Args *a, int nord, int kahan, hipStream_t st);
+extern "C" hipError_t icw_launch_graph_serial(const IcwK4Args *a, hipStream_t st);
+extern "C" hipError_t icw_launch_advance(const IcwAdvArgs *a, hipStream_t st);
 
 #define ICW_PI_H (3.1415926535897932384626433832795029)
 
@@ -91,6 +93,8 @@ struct icw_ctx {
     size_t d_pre_bytes = 0;
     double *rpre = nullptr;               /* per-block pre-render buffer for the serial render */
     size_t rpre_bytes = 0;
+    double *iq = nullptr;                 /* per-block `in` buffer for the bus-form graph */
+    size_t iq_bytes = 0;
     bool serial_render = false;
     uint32_t mt_seed_state[2][624];       /* seeded MT19937 states for L / R (mtrnd_init_seed) */
     hipStream_t stream = nullptr;
@@ -119,10 +123,11 @@ int dalloc(T **p, size_t n)
     return ICW_OK;
 }
 
+/* bytes per channel sample: HRW_FMT_* (xwave_reader.c:553-580), CWAVE cw_slen (xwave_reader.c:246-252) */
 unsigned fmt_size(unsigned fmt)
 {
-    static const unsigned sz[5] = {1, 2, 3, 4, 4};
-    return fmt < 5 ? sz[fmt] : 0;
+    static const unsigned sz[9] = {1, 2, 3, 4, 4, 16, 4, 6, 8};
+    return fmt < 9 ? sz[fmt] : 0;
 }
 
 /* amod_init (adv_modulator.c:216-331): accept the list only if its head is the one and only
@@ -178,6 +183,60 @@ double scaled_fr(double f) { return (double)((unsigned)(f * ((double)ICW_HZ_SCAL
  * (adv_modulator.c:637).  Each input slot resolves to the value most recently written in the
  * same frame; a slot never written by any node reads its persistent bus value.  A slot read
  * before its writer runs (a one-frame delay, doc 3.1) is not yet on the device path. */
+/* per-op parameters shared by the register and bus forms */
+void op_params(const icw_node &n, IcwOp &op)
+{
+    op.mode = n.mode;
+    op.xch = n.xch_mode;
+    op.iqinv[0] = n.iq_invert[0];
+    op.iqinv[1] = n.iq_invert[1];
+    op.gain[0] = n.gain[0];
+    op.gain[1] = n.gain[1];
+    op.out_slot = n.mode == ICW_MODE_MASTER ? 0 : n.n_out;
+    op.in_mask = 0;
+    for (int k = 0; k < ICW_N_INPUTS; ++k)
+        if (n.inputs[k]) op.in_mask |= 1u << k;
+    for (int c = 0; c < 2; ++c) {
+        op.tout[c] = n.tout[c];
+        if (n.mode == ICW_MODE_SHIFT) {
+            op.act[c] = n.is_shift[c];
+            double f = n.fr_shift[c];
+            op.neg[c] = f < 0.0;
+            if (f < 0.0) f = -f;
+            op.f[c] = f;   /* scaled below if frmod_scaled */
+        } else if (n.mode == ICW_MODE_PM) {
+            op.act[c] = n.is_pm[c];
+            op.f[c] = n.pm_freq[c];
+            op.pp[c] = n.pm_phase[c] * ICW_PI_H;              /* fphase * PI */
+            op.lp[c] = n.pm_level[c] * ICW_PI_H;              /* flevel * PI */
+            op.fa[c] = n.pm_angle[c];
+        }
+    }
+}
+
+/* Bus form: the list as the reference runs it (tail -> head, or the head alone when bypassed) */
+int compile_bus(const std::vector<icw_node> &nodes, int bypass, IcwProg &P)
+{
+    memset(&P, 0, sizeof(P));
+    P.is_bus = 1;
+    P.bypass = bypass;
+    std::vector<int> order;
+    if (bypass) order.push_back(0);
+    else for (int i = (int)nodes.size() - 1; i >= 0; --i) order.push_back(i);
+    if ((int)order.size() > ICW_MAX_OPS) return ICW_EUNSUPPORTED;
+    for (size_t oi = 0; oi < order.size(); ++oi) {
+        const icw_node &n = nodes[order[oi]];
+        if (n.mode != ICW_MODE_MASTER && (n.n_out < 1 || n.n_out >= ICW_N_INPUTS)) return ICW_EGRAPH;
+        op_params(n, P.ops[oi]);
+    }
+    P.n_ops = (int)order.size();
+    P.n_regs = 1;
+    return ICW_OK;
+}
+
+/* Register form for the frame-parallel output kernel; ICW_EUNSUPPORTED when a slot is read
+ * before it is written in the frame (one-frame delay) or the list exceeds the register budget --
+ * the caller then compiles the bus form. */
 int compile_graph(const std::vector<icw_node> &nodes, int bypass, IcwProg &P)
 {
     memset(&P, 0, sizeof(P));
@@ -185,7 +244,7 @@ int compile_graph(const std::vector<icw_node> &nodes, int bypass, IcwProg &P)
     std::vector<int> order;
     if (bypass) order.push_back(0);
     else for (int i = (int)nodes.size() - 1; i >= 0; --i) order.push_back(i);
-    if ((int)order.size() > ICW_MAX_OPS) return ICW_EUNSUPPORTED;
+    if ((int)order.size() > ICW_MAX_REG_OPS) return ICW_EUNSUPPORTED;
 
     bool written_any[ICW_N_INPUTS] = {false};
     for (int i : order)
@@ -218,27 +277,7 @@ int compile_graph(const std::vector<icw_node> &nodes, int bypass, IcwProg &P)
                 op.in_reg[op.n_in++] = r;
             }
         }
-        op.xch = n.xch_mode;
-        op.iqinv[0] = n.iq_invert[0];
-        op.iqinv[1] = n.iq_invert[1];
-        op.gain[0] = n.gain[0];
-        op.gain[1] = n.gain[1];
-        for (int c = 0; c < 2; ++c) {
-            op.tout[c] = n.tout[c];
-            if (n.mode == ICW_MODE_SHIFT) {
-                op.act[c] = n.is_shift[c];
-                double f = n.fr_shift[c];
-                op.neg[c] = f < 0.0;
-                if (f < 0.0) f = -f;
-                op.f[c] = f;   /* scaled below if frmod_scaled */
-            } else if (n.mode == ICW_MODE_PM) {
-                op.act[c] = n.is_pm[c];
-                op.f[c] = n.pm_freq[c];
-                op.pp[c] = n.pm_phase[c] * ICW_PI_H;              /* fphase * PI */
-                op.lp[c] = n.pm_level[c] * ICW_PI_H;              /* flevel * PI */
-                op.fa[c] = n.pm_angle[c];
-            }
-        }
+        op_params(n, op);
         if (n.mode != ICW_MODE_MASTER) {
             if (n_regs >= ICW_MAX_REGS) return ICW_EUNSUPPORTED;
             op.out_reg = n_regs++;
@@ -303,7 +342,7 @@ int grow(void **p, size_t *cur, size_t need)
 void free_all(icw_ctx *c)
 {
     DevState &s = c->st;
-    void *ptrs[] = {s.mt, s.mt_idx, s.rs, c->rpre, s.err, s.hist, s.sncnt, s.hq_phase, s.pos, s.fade, s.n_frame, s.bus, s.clips, s.peak_bits,
+    void *ptrs[] = {s.mt, s.mt_idx, s.rs, c->rpre, c->iq, s.err, s.hist, s.sncnt, s.hq_phase, s.pos, s.fade, s.n_frame, s.bus, s.clips, s.peak_bits,
                     c->d_prog, c->w[0], c->w[1], c->xd[0], c->xd[1], c->info_phase[0], c->info_phase[1],
                     c->info_nframe[0], c->info_nframe[1], c->d_in, c->d_out, c->d_pre};
     for (void *p : ptrs)
@@ -339,7 +378,7 @@ int icw_create(const icw_config *cfg, const icw_node *nodes, int n_nodes, int n_
 {
     if (!cfg || !out || n_streams <= 0 || n_nodes < 0 || (n_nodes > 0 && !nodes)) return ICW_EINVAL;
     *out = nullptr;
-    if (cfg->hilbert_type > 5 || cfg->in_format > ICW_FMT_F32 || cfg->in_channels == 0 ||
+    if (cfg->hilbert_type > 5 || cfg->in_format > ICW_FMT_CW_F32 || cfg->in_channels == 0 ||
         cfg->sample_rate == 0 || cfg->sample_rate > ICW_MAX_FS_SRC)
         return ICW_EINVAL;
     if (cfg->render.sign_bits16 < 2 || cfg->render.sign_bits16 > 16 || cfg->render.sign_bits24 < 2 ||
@@ -368,6 +407,7 @@ int icw_create(const icw_config *cfg, const icw_node *nodes, int n_nodes, int n_
                 }
             }
     int rc = compile_graph(c->nodes, cfg->bypass_list, c->prog);
+    if (rc == ICW_EUNSUPPORTED) rc = compile_bus(c->nodes, cfg->bypass_list, c->prog);
     if (rc) { delete c; return rc; }
     if (cfg->frmod_scaled)
         for (int i = 0; i < c->prog.n_ops; ++i)
@@ -386,6 +426,8 @@ int icw_create(const icw_config *cfg, const icw_node *nodes, int n_nodes, int n_
     /* ROUND + flat is elementwise (rendered inside the output kernel); every other render keeps
      * serial per-channel state and runs in the serial render kernel */
     c->serial_render = !(cfg->render.render_type == ICW_RENDER_ROUND && c->rk.ns_kind == 0);
+    /* the bus-form graph runs frame-serially and hands lOut/rOut to the serial render */
+    if (c->prog.is_bus) c->serial_render = true;
     for (int ch = 0; ch < 2; ++ch) {
         uint32_t *st = c->mt_seed_state[ch];
         st[0] = ch ? cfg->seed_right : cfg->seed_left;         /* mtrnd_init_seed, mt_jrnd.c:28-47 */
@@ -565,7 +607,7 @@ int icw_stream_seek(icw_ctx *c, int s, int64_t frame_pos)
 
 int icw_set_input(icw_ctx *c, uint32_t sample_rate, uint32_t fmt, uint32_t channels)
 {
-    if (!c || sample_rate == 0 || sample_rate > ICW_MAX_FS_SRC || fmt > ICW_FMT_F32 || channels == 0) return ICW_EINVAL;
+    if (!c || sample_rate == 0 || sample_rate > ICW_MAX_FS_SRC || fmt > ICW_FMT_CW_F32 || channels == 0) return ICW_EINVAL;
     std::lock_guard<std::mutex> lk(c->mu);
     if (set_dev(c) || hipStreamSynchronize(c->stream) != hipSuccess) return ICW_EDEVICE;
     c->cfg.sample_rate = sample_rate;
@@ -635,6 +677,9 @@ int icw_process_streams(icw_ctx *c, int first, int count, const void *in, size_t
     }
     if (c->serial_render && !d_pre && grow((void **)&c->rpre, &c->rpre_bytes, S * (size_t)Tb * 2 * sizeof(double)))
         return ICW_ENOMEM;
+    const bool cw = cfg.in_format >= ICW_FMT_CW_F64;
+    const bool bus = c->prog.is_bus;
+    if (bus && grow((void **)&c->iq, &c->iq_bytes, S * (size_t)Tb * 4 * sizeof(double))) return ICW_ENOMEM;
     hipStream_t st2 = c->stream2;
     /* second stream starts after everything already queued on st (inputs, previous calls) */
     if (hipEventRecord(c->join, st) != hipSuccess || hipStreamWaitEvent(st2, c->join, 0) != hipSuccess)
@@ -668,6 +713,8 @@ int icw_process_streams(icw_ctx *c, int first, int count, const void *in, size_t
         a0.hq_phase = ds.hq_phase + f0 * 2;
         a0.xd = c->xd[p];
         a0.x_pitch = x_pitch;
+        /* xd[p], w[p], info[p] were last read by the output kernel of block b-2 */
+        if (b >= 2 && hipStreamWaitEvent(st, c->k2done[p], 0) != hipSuccess) return ICW_EDEVICE;
         if (icw_launch_unpack(&a0, st) != hipSuccess) return ICW_EDEVICE;
 
         IcwK1Args a1;
@@ -691,12 +738,26 @@ int icw_process_streams(icw_ctx *c, int first, int count, const void *in, size_t
         a1.info_phase = c->info_phase[p];
         a1.info_nframe = c->info_nframe[p];
         memcpy(a1.pc, c->pc, sizeof(a1.pc));
-        /* w[p]/info[p] were last read by the output kernel of block b-2 */
-        if (b >= 2 && hipStreamWaitEvent(st, c->k2done[p], 0) != hipSuccess) return ICW_EDEVICE;
         if (timing) hipEventRecord(c->ev[4 * b], st);
-        const hipError_t e1 = c->pair_mode
-            ? icw_launch_iir_pair(&a1, N, cfg.iir_kahan, cfg.iir_subnorm_reject, st)
-            : icw_launch_iir_state(&a1, N, cfg.iir_kahan, cfg.iir_subnorm_reject, st);
+        hipError_t e1;
+        if (cw) {
+            /* complex input: no Hilbert, only the block bookkeeping */
+            IcwAdvArgs av;
+            memset(&av, 0, sizeof(av));
+            av.n_streams = count;
+            av.T = T;
+            av.hq_phase = a1.hq_phase;
+            av.pos = a1.pos;
+            av.n_frame = a1.n_frame;
+            av.ssr = a1.ssr;
+            av.scaled = a1.scaled;
+            av.info_phase = a1.info_phase;
+            av.info_nframe = a1.info_nframe;
+            e1 = icw_launch_advance(&av, st);
+        } else {
+            e1 = c->pair_mode ? icw_launch_iir_pair(&a1, N, cfg.iir_kahan, cfg.iir_subnorm_reject, st)
+                              : icw_launch_iir_state(&a1, N, cfg.iir_kahan, cfg.iir_subnorm_reject, st);
+        }
         if (e1 != hipSuccess) return ICW_EDEVICE;
         if (timing) hipEventRecord(c->ev[4 * b + 1], st);
         if (hipEventRecord(c->k1done[p], st) != hipSuccess || hipStreamWaitEvent(st2, c->k1done[p], 0) != hipSuccess)
@@ -733,8 +794,28 @@ int icw_process_streams(icw_ctx *c, int first, int count, const void *in, size_t
         memcpy(a2.pc, c->pc, sizeof(a2.pc));
         memcpy(a2.pd, c->pd, sizeof(a2.pd));
         a2.d0 = c->d0;
+        a2.cw = cw ? 1 : 0;
+        a2.xin = c->xd[p];
+        a2.x_pitch = x_pitch;
+        if (bus) a2.iq_out = c->iq;
         if (timing) hipEventRecord(c->ev[4 * b + 2], st2);
         if (icw_launch_output(&a2, N, cfg.iir_kahan, st2) != hipSuccess) return ICW_EDEVICE;
+        if (bus) {
+            IcwK4Args a4;
+            memset(&a4, 0, sizeof(a4));
+            a4.iq = c->iq;
+            a4.n_streams = count;
+            a4.T = T;
+            a4.info_nframe = a2.info_nframe;
+            a4.ssr = a2.ssr;
+            a4.scaled = a2.scaled;
+            a4.sample_rate = a2.sample_rate;
+            a4.prog = c->d_prog;
+            a4.bus = a2.bus;
+            a4.pre = a2.pre;
+            a4.pre_stride = a2.pre_stride;
+            if (icw_launch_graph_serial(&a4, st2) != hipSuccess) return ICW_EDEVICE;
+        }
         if (c->serial_render) {
             IcwK3Args a3;
             memset(&a3, 0, sizeof(a3));

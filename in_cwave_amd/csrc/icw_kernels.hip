@@ -63,6 +63,37 @@ __device__ __forceinline__ double icw_unpack(const unsigned char *p, uint32_t fm
     }
 }
 
+/* CWAVE unpackers (xwave_reader.c:171-200): no scaling, values already on the 16-bit scale */
+__device__ __forceinline__ uint32_t icw_le32(const unsigned char *p)
+{
+    return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
+}
+
+__device__ __forceinline__ void icw_unpack_iq(const unsigned char *p, uint32_t fmt, double &vI, double &vQ)
+{
+    switch (fmt) {
+    case ICW_FMT_CW_F64: {
+        const unsigned long long lo = icw_le32(p), hi = icw_le32(p + 4);
+        const unsigned long long lo2 = icw_le32(p + 8), hi2 = icw_le32(p + 12);
+        vI = __longlong_as_double((long long)(lo | (hi << 32)));
+        vQ = __longlong_as_double((long long)(lo2 | (hi2 << 32)));
+        break;
+    }
+    case ICW_FMT_CW_I16:
+        vI = (double)(short)((unsigned)p[0] | ((unsigned)p[1] << 8));
+        vQ = (double)(short)((unsigned)p[2] | ((unsigned)p[3] << 8));
+        break;
+    case ICW_FMT_CW_I16_F32:
+        vI = (double)(short)((unsigned)p[0] | ((unsigned)p[1] << 8));
+        vQ = (double)__uint_as_float(icw_le32(p + 2));
+        break;
+    default:
+        vI = (double)__uint_as_float(icw_le32(p));
+        vQ = (double)__uint_as_float(icw_le32(p + 4));
+        break;
+    }
+}
+
 /* fade factor of xwave_unpack_csample (xwave_reader.c:918-936); < 0 means "no fade" */
 __device__ __forceinline__ double icw_fade(long long ix, long long ns, long long fi, long long fo)
 {
@@ -184,6 +215,22 @@ __global__ __launch_bounds__(256) void icw_unpack_frames(IcwK0Args a)
     const unsigned char *fp = a.in + (size_t)s * a.in_stride + (size_t)t * a.fsz;
     const long long ix = a.pos[s] + t;
     const double fd = icw_fade(ix, a.fade[s * 3 + 0], a.fade[s * 3 + 1], a.fade[s * 3 + 2]);
+    if (a.fmt >= ICW_FMT_CW_F64) {
+        /* complex (CWAVE) sample: I/Q per channel, mono -> R = L, fade on all four
+         * (xwave_reader.c:939-966); rows s*4 + ch*2 + {I, Q} */
+        double q[4];
+        icw_unpack_iq(fp, a.fmt, q[0], q[1]);
+        if (a.nch > 1) icw_unpack_iq(fp + a.csz, a.fmt, q[2], q[3]);
+        else { q[2] = q[0]; q[3] = q[1]; }
+        if (fd >= 0.0) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) q[i] *= fd;
+        }
+        double *xs = a.xd + (size_t)s * 4 * a.x_pitch + t;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) xs[(size_t)i * a.x_pitch] = q[i];
+        return;
+    }
     double v[2];
     v[0] = icw_unpack(fp, a.fmt);
     if (fd >= 0.0) v[0] *= fd;
@@ -646,6 +693,84 @@ __device__ __forceinline__ int icw_render_round(double input, const IcwRenderK &
     return (v + delta) << k.norm_shift;
 }
 
+/* modulator frame counter -> norm_omega of frame t of the block (adv_modulator.c:611-625);
+ * n0 is the block-start counter (< ssr in scaled mode) */
+__device__ __forceinline__ double icw_omega(unsigned long long n0, int t, int scaled, unsigned long long ssr,
+                                            uint32_t sample_rate)
+{
+    if (scaled) {
+        const unsigned long long n = (t == 0) ? n0 : (n0 + (unsigned long long)t) % ssr;
+        return (2.0 * ICW_PI) * ((double)n) / ((double)ssr);
+    }
+    return (2.0 * ICW_PI) * ((double)(n0 + (unsigned long long)t)) / (double)sample_rate;
+}
+
+/* One DSP node on its mixed input d (adv_modulator.c:669-751): channel exchange, I/Q swap,
+ * gains, then Master (-> lOut/rOut) or Shift / PM / Mix (-> o, returns true). */
+__device__ __forceinline__ bool icw_exec_op(const IcwOp &op, IcwLR d, double omega, IcwLR &o, double &lOut,
+                                            double &rOut)
+{
+    double xt;
+    switch (op.xch) {
+    case ICW_XCH_SWAP:
+        xt = d.lre; d.lre = d.rre; d.rre = xt;
+        xt = d.lim; d.lim = d.rim; d.rim = xt;
+        break;
+    case ICW_XCH_LEFTONLY: d.rre = d.lre; d.rim = d.lim; break;
+    case ICW_XCH_RIGHTONLY: d.lre = d.rre; d.lim = d.rim; break;
+    case ICW_XCH_MIXLR:
+        d.lre = d.rre = (d.lre + d.rre) / 2.0;
+        d.lim = d.rim = (d.lim + d.rim) / 2.0;
+        break;
+    default: break;
+    }
+    if (op.iqinv[0]) { xt = d.lre; d.lre = d.lim; d.lim = xt; }
+    if (op.iqinv[1]) { xt = d.rre; d.rre = d.rim; d.rim = xt; }
+    d.lre *= op.gain[0]; d.lim *= op.gain[0];
+    d.rre *= op.gain[1]; d.rim *= op.gain[1];
+    switch (op.mode) {
+    case ICW_MODE_MASTER:
+        lOut = icw_master(op.tout[0], d.lre, d.lim);
+        rOut = icw_master(op.tout[1], d.rre, d.rim);
+        return false;
+    case ICW_MODE_SHIFT: {
+        double cs, sn;
+        if (op.act[0]) {
+            const double ph = fmod(omega * op.f[0], 2.0 * ICW_PI);
+            sincos(ph, &sn, &cs);
+            if (op.neg[0]) sn = -sn;
+            icw_rot(d.lre, d.lim, cs, sn, o.lre, o.lim);
+        } else { o.lre = d.lre; o.lim = d.lim; }
+        if (op.act[1]) {
+            const double ph = fmod(omega * op.f[1], 2.0 * ICW_PI);
+            sincos(ph, &sn, &cs);
+            if (op.neg[1]) sn = -sn;
+            icw_rot(d.rre, d.rim, cs, sn, o.rre, o.rim);
+        } else { o.rre = d.rre; o.rim = d.rim; }
+        return true;
+    }
+    case ICW_MODE_PM: {
+        double cs, sn;
+        if (op.act[0]) {
+            const double ph = fmod(omega * op.f[0], 2.0 * ICW_PI);
+            const double psi = op.lp[0] * (sin(ph + op.pp[0]) + op.fa[0]);
+            sincos(psi, &sn, &cs);
+            icw_rot(d.lre, d.lim, cs, sn, o.lre, o.lim);
+        } else { o.lre = d.lre; o.lim = d.lim; }
+        if (op.act[1]) {
+            const double ph = fmod(omega * op.f[1], 2.0 * ICW_PI);
+            const double psi = op.lp[1] * (sin(ph + op.pp[1]) + op.fa[1]);
+            sincos(psi, &sn, &cs);
+            icw_rot(d.rre, d.rim, cs, sn, o.rre, o.rim);
+        } else { o.rre = d.rre; o.rim = d.rim; }
+        return true;
+    }
+    default: /* MIX */
+        o = d;
+        return true;
+    }
+}
+
 template <int N, bool KAHAN>
 __global__ __launch_bounds__(ICW_K2_TILE) void icw_output(IcwK2Args a)
 {
@@ -658,31 +783,36 @@ __global__ __launch_bounds__(ICW_K2_TILE) void icw_output(IcwK2Args a)
     const int tl = threadIdx.x;
     const int t = t0 + tl;
     const int T = a.T;
-    const int nrow = min(ICW_K2_TILE, T - t0) + N + (KAHAN ? 0 : 1);
 
-    /* stage the w windows of the stream's 4 chains: rows [t0, t0+nrow) */
+    if (!a.cw) {
+        /* stage the w windows of the stream's 4 chains: rows [t0, t0+nrow) */
+        const int nrow = min(ICW_K2_TILE, T - t0) + N + (KAHAN ? 0 : 1);
 #pragma unroll
-    for (int c = 0; c < 4; ++c) {
-        const double *src = a.w + (size_t)(s * 4 + c) * a.w_pitch + t0;
-        for (int r = tl; r < nrow; r += ICW_K2_TILE) lw[c][r] = src[r];
+        for (int c = 0; c < 4; ++c) {
+            const double *src = a.w + (size_t)(s * 4 + c) * a.w_pitch + t0;
+            for (int r = tl; r < nrow; r += ICW_K2_TILE) lw[c][r] = src[r];
+        }
+        __syncthreads();
     }
-    __syncthreads();
-
-    double pc[20], pd[20];
-#pragma unroll
-    for (int i = 0; i < 20; ++i) { pc[i] = a.pc[i]; pd[i] = a.pd[i]; }
 
     unsigned clip_l = 0, clip_r = 0;
     double pk_l = 0.0, pk_r = 0.0;
     if (t < T) {
-        /* filter outputs of the 4 chains (L-I, L-Q, R-I, R-Q) */
-        double y[4];
-#pragma unroll
-        for (int c = 0; c < 4; ++c) y[c] = icw_iir_out<N, KAHAN>(&lw[c][tl], pc, pd, a.d0);
-
-        /* fs/4 un-mix (lpf_hilbert_quad.c:129-156) */
         IcwLR in;
-        {
+        if (a.cw) {
+            /* complex (CWAVE) input: the analytic signal as read (xwave_reader.c:939-966) */
+            const double *xs = a.xin + (size_t)s * 4 * a.x_pitch + t;
+            in.lre = xs[0]; in.lim = xs[a.x_pitch]; in.rre = xs[2 * a.x_pitch]; in.rim = xs[3 * a.x_pitch];
+        } else {
+            double pc[20], pd[20];
+#pragma unroll
+            for (int i = 0; i < 20; ++i) { pc[i] = a.pc[i]; pd[i] = a.pd[i]; }
+            /* filter outputs of the 4 chains (L-I, L-Q, R-I, R-Q) */
+            double y[4];
+#pragma unroll
+            for (int c = 0; c < 4; ++c) y[c] = icw_iir_out<N, KAHAN>(&lw[c][tl], pc, pd, a.d0);
+
+            /* fs/4 un-mix (lpf_hilbert_quad.c:129-156) */
             double oI[2], oQ[2];
 #pragma unroll
             for (int ch = 0; ch < 2; ++ch) {
@@ -698,15 +828,14 @@ __global__ __launch_bounds__(ICW_K2_TILE) void icw_output(IcwK2Args a)
             in.lre = oI[0]; in.lim = oQ[0]; in.rre = oI[1]; in.rim = oQ[1];
         }
 
-        /* modulator frame counter -> norm_omega (adv_modulator.c:611-625) */
-        const unsigned long long n0 = a.info_nframe[s];
-        double omega;
-        if (a.scaled) {
-            const unsigned long long n = (t == 0) ? n0 : (n0 + (unsigned long long)t) % a.ssr;
-            omega = (2.0 * ICW_PI) * ((double)n) / ((double)a.ssr);
-        } else {
-            omega = (2.0 * ICW_PI) * ((double)(n0 + (unsigned long long)t)) / (double)a.sample_rate;
+        if (a.iq_out) {
+            /* bus-form graph: the serial graph kernel takes it from here */
+            double *q = a.iq_out + ((size_t)s * T + t) * 4;
+            q[0] = in.lre; q[1] = in.lim; q[2] = in.rre; q[3] = in.rim;
+            return;   /* do_render == 0 in this mode: no barrier follows */
         }
+
+        const double omega = icw_omega(a.info_nframe[s], t, a.scaled, a.ssr, a.sample_rate);
 
         /* DSP list (adv_modulator.c:637-751) */
         const IcwProg *P = a.prog;
@@ -732,68 +861,8 @@ __global__ __launch_bounds__(ICW_K2_TILE) void icw_output(IcwK2Args a)
                     d.lre += v.lre; d.lim += v.lim; d.rre += v.rre; d.rim += v.rim;
                 }
             }
-            double xt;
-            switch (op.xch) {
-            case ICW_XCH_SWAP:
-                xt = d.lre; d.lre = d.rre; d.rre = xt;
-                xt = d.lim; d.lim = d.rim; d.rim = xt;
-                break;
-            case ICW_XCH_LEFTONLY: d.rre = d.lre; d.rim = d.lim; break;
-            case ICW_XCH_RIGHTONLY: d.lre = d.rre; d.lim = d.rim; break;
-            case ICW_XCH_MIXLR:
-                d.lre = d.rre = (d.lre + d.rre) / 2.0;
-                d.lim = d.rim = (d.lim + d.rim) / 2.0;
-                break;
-            default: break;
-            }
-            if (op.iqinv[0]) { xt = d.lre; d.lre = d.lim; d.lim = xt; }
-            if (op.iqinv[1]) { xt = d.rre; d.rre = d.rim; d.rim = xt; }
-            d.lre *= op.gain[0]; d.lim *= op.gain[0];
-            d.rre *= op.gain[1]; d.rim *= op.gain[1];
             IcwLR o;
-            switch (op.mode) {
-            case ICW_MODE_MASTER:
-                lOut = icw_master(op.tout[0], d.lre, d.lim);
-                rOut = icw_master(op.tout[1], d.rre, d.rim);
-                break;
-            case ICW_MODE_SHIFT: {
-                double cs, sn;
-                if (op.act[0]) {
-                    const double ph = fmod(omega * op.f[0], 2.0 * ICW_PI);
-                    sincos(ph, &sn, &cs);
-                    if (op.neg[0]) sn = -sn;
-                    icw_rot(d.lre, d.lim, cs, sn, o.lre, o.lim);
-                } else { o.lre = d.lre; o.lim = d.lim; }
-                if (op.act[1]) {
-                    const double ph = fmod(omega * op.f[1], 2.0 * ICW_PI);
-                    sincos(ph, &sn, &cs);
-                    if (op.neg[1]) sn = -sn;
-                    icw_rot(d.rre, d.rim, cs, sn, o.rre, o.rim);
-                } else { o.rre = d.rre; o.rim = d.rim; }
-                R.set(op.out_reg, o);
-                break;
-            }
-            case ICW_MODE_PM: {
-                double cs, sn;
-                if (op.act[0]) {
-                    const double ph = fmod(omega * op.f[0], 2.0 * ICW_PI);
-                    const double psi = op.lp[0] * (sin(ph + op.pp[0]) + op.fa[0]);
-                    sincos(psi, &sn, &cs);
-                    icw_rot(d.lre, d.lim, cs, sn, o.lre, o.lim);
-                } else { o.lre = d.lre; o.lim = d.lim; }
-                if (op.act[1]) {
-                    const double ph = fmod(omega * op.f[1], 2.0 * ICW_PI);
-                    const double psi = op.lp[1] * (sin(ph + op.pp[1]) + op.fa[1]);
-                    sincos(psi, &sn, &cs);
-                    icw_rot(d.rre, d.rim, cs, sn, o.rre, o.rim);
-                } else { o.rre = d.rre; o.rim = d.rim; }
-                R.set(op.out_reg, o);
-                break;
-            }
-            default: /* MIX */
-                R.set(op.out_reg, d);
-                break;
-            }
+            if (icw_exec_op(op, d, omega, o, lOut, rOut)) R.set(op.out_reg, o);
         }
 
         if (a.pre) {
@@ -847,6 +916,72 @@ __global__ __launch_bounds__(ICW_K2_TILE) void icw_output(IcwK2Args a)
             if (pm > 0.0) atomicMax(&a.peak_bits[s * 2 + tl], (unsigned long long)__double_as_longlong(pm));
         }
     }
+}
+
+/* ------------------------------------------------------- serial graph kernel (K4) ------ */
+/* Bus form of the DSP list, for lists whose nodes read a slot before it is written in the frame
+ * (a one-frame delay -- feedback loops included): the reference's own per-frame semantics
+ * (adv_modulator.c:636-751) with the 27-slot bus of the stream held in LDS, one lane per stream,
+ * frames in order.  `in` comes from the output kernel (Hilbert or complex input), lOut/rOut go
+ * to the serial render kernel. */
+__global__ __launch_bounds__(64) void icw_graph_serial(IcwK4Args a)
+{
+    __shared__ double bus[ICW_N_INPUTS * 4][64];
+    const int lane = threadIdx.x;
+    const int s = blockIdx.x * 64 + lane;
+    if (s >= a.n_streams) return;
+    double *gb = a.bus + (size_t)s * ICW_N_INPUTS * 4;
+    for (int k = 0; k < ICW_N_INPUTS * 4; ++k) bus[k][lane] = gb[k];
+    const IcwProg *P = a.prog;
+    const unsigned long long n0 = a.info_nframe[s];
+    const double *iq = a.iq + (size_t)s * a.T * 4;
+    double *pre = a.pre + (size_t)s * a.pre_stride;
+    for (int t = 0; t < a.T; ++t) {
+        const double omega = icw_omega(n0, t, a.scaled, a.ssr, a.sample_rate);
+        bus[0][lane] = iq[(size_t)t * 4 + 0];
+        bus[1][lane] = iq[(size_t)t * 4 + 1];
+        bus[2][lane] = iq[(size_t)t * 4 + 2];
+        bus[3][lane] = iq[(size_t)t * 4 + 3];
+        double lOut = 0.0, rOut = 0.0;
+        for (int oi = 0; oi < P->n_ops; ++oi) {
+            const IcwOp &op = P->ops[oi];
+            IcwLR d;
+            if (P->bypass) {
+                d.lre = bus[0][lane]; d.lim = bus[1][lane]; d.rre = bus[2][lane]; d.rim = bus[3][lane];
+            } else {
+                d.lre = d.lim = d.rre = d.rim = 0.0;
+                const uint32_t m = op.in_mask;
+                for (int k = 0; k < ICW_N_INPUTS; ++k) {
+                    if (!((m >> k) & 1u)) continue;
+                    d.lre += bus[k * 4 + 0][lane]; d.lim += bus[k * 4 + 1][lane];
+                    d.rre += bus[k * 4 + 2][lane]; d.rim += bus[k * 4 + 3][lane];
+                }
+            }
+            IcwLR o;
+            if (icw_exec_op(op, d, omega, o, lOut, rOut)) {
+                const int q = op.out_slot * 4;
+                bus[q + 0][lane] = o.lre; bus[q + 1][lane] = o.lim; bus[q + 2][lane] = o.rre; bus[q + 3][lane] = o.rim;
+            }
+        }
+        pre[(size_t)t * 2] = lOut;
+        pre[(size_t)t * 2 + 1] = rOut;
+    }
+    for (int k = 0; k < ICW_N_INPUTS * 4; ++k) gb[k] = bus[k][lane];
+}
+
+/* Block bookkeeping for complex input, where no IIR state kernel runs: the Hilbert phases stay
+ * (the converters are not called for CWAVE samples), the reader position and the modulator
+ * frame counter advance by T, and the block-start snapshot for the output kernel is taken. */
+__global__ __launch_bounds__(64) void icw_advance(IcwAdvArgs a)
+{
+    const int s = blockIdx.x * 64 + threadIdx.x;
+    if (s >= a.n_streams) return;
+    a.info_phase[s * 2 + 0] = a.hq_phase[s * 2 + 0];
+    a.info_phase[s * 2 + 1] = a.hq_phase[s * 2 + 1];
+    a.pos[s] += a.T;
+    const unsigned long long n0 = a.n_frame[s];
+    a.info_nframe[s] = n0;
+    a.n_frame[s] = a.scaled ? (n0 + (unsigned long long)a.T) % a.ssr : n0 + (unsigned long long)a.T;
 }
 
 /* ------------------------------------------------------ serial render kernel (K3) ------ */
@@ -1085,4 +1220,16 @@ extern "C" hipError_t icw_launch_output(const IcwK2Args *a, int nord, int kahan,
     case 20: return kahan ? launch_k2_t<20, true>(*a, st) : launch_k2_t<20, false>(*a, st);
     }
     return hipErrorInvalidValue;
+}
+
+extern "C" hipError_t icw_launch_graph_serial(const IcwK4Args *a, hipStream_t st)
+{
+    hipLaunchKernelGGL(icw_graph_serial, dim3((a->n_streams + 63) / 64), dim3(64), 0, st, *a);
+    return hipGetLastError();
+}
+
+extern "C" hipError_t icw_launch_advance(const IcwAdvArgs *a, hipStream_t st)
+{
+    hipLaunchKernelGGL(icw_advance, dim3((a->n_streams + 63) / 64), dim3(64), 0, st, *a);
+    return hipGetLastError();
 }

@@ -98,6 +98,33 @@ def graph_pm_shift_mix():
             pm(inputs=("in",), out="A")]
 
 
+# ---- lists with one-frame delays (bus form, serial graph kernel) -----------------------------
+def graph_pure_delay():
+    """Master(B) <- Mix(A -> B) <- Shift(in -> A).  Executed tail -> head, the Mix runs first and
+    reads A before the Shift writes it, so B is the shifted signal one frame late."""
+    return [master(inputs=("B",)), shift(inputs=("in",), out="A"), mix(inputs=("A",), out="B")]
+
+
+def graph_leaky_feedback():
+    """C = 0.5 * (in + C[t-1]): a Mix node feeding itself, then Master(C)."""
+    return [master(inputs=("C",)), mix(inputs=("in", "C"), out="C", gain=0.5)]
+
+
+def graph_feedback_pm_shift():
+    """PM and Shift inside a loop: A = PM(0.25 (in + B[t-1])); B = Shift(A); Master(in + B)."""
+    return [master(inputs=("in", "B")), shift(inputs=("A",), out="B"), pm(inputs=("in", "B"), out="A", gain=0.25)]
+
+
+def graph_long_chain(n=24):
+    """More nodes than the register program holds: Master(X) <- n Mix hops from `in`."""
+    slots = "ABCDEFGHIJKLMNOPQRSTUVWX"
+    nodes = [master(inputs=("X",)), mix(inputs=(slots[n - 2],), out="X", gain=1.0)]
+    for i in range(n - 2, 0, -1):
+        nodes.append(mix(inputs=(slots[i - 1],), out=slots[i], gain=1.0))
+    nodes.append(mix(inputs=("in",), out="A", gain=0.999))
+    return nodes
+
+
 def default_config(sample_rate=48000, fmt=abi.FMT_I16, channels=2, need24bits=False, hilbert_type=1):
     """load_config_default hot-path fields (config.c:153-207); NEED24BITS defaults to TRUE in the
     reference, the BASELINE configs C1-C4 use 16-bit output."""

@@ -83,6 +83,11 @@ class Context:
         _check(self._lib.icw_stream_init(self.h, first, self.n_streams - first if count is None else count),
                "icw_stream_init")
 
+    def set_input(self, sample_rate, fmt, channels):
+        """a new track's sample format for every stream (icw_set_input)"""
+        _check(self._lib.icw_set_input(self.h, sample_rate, fmt, channels), "icw_set_input")
+        self.fsz = abi.FMT_BYTES[fmt] * channels
+
     def stream_open(self, s, n_samples, fade_in_ms=0, fade_out_ms=0, sec_align=0, clr_nframe=0, clr_hilb=0):
         _check(self._lib.icw_stream_open(self.h, s, n_samples, fade_in_ms, fade_out_ms, sec_align,
                                          clr_nframe, clr_hilb), "icw_stream_open")

@@ -35,6 +35,41 @@ def stream_pcm(s, n_frames, fs, channels=2, fmt=abi.FMT_I16, seed_base=1000):
     raise ValueError(fmt)
 
 
+def stream_cwave(s, n_frames, fs, channels=2, fmt=abi.FMT_CW_I16, seed_base=2000):
+    """Analytic (complex) test signal in a CWAVE sample format: per channel two complex
+    exponentials (positive and negative frequency, -12 dBFS each) plus complex Gaussian noise at
+    -40 dBFS, on the 16-bit scale the CWAVE formats use (cwave.h:70-80).  Interleaved per frame:
+    Re(L), Im(L)[, Re(R), Im(R)] in the format's own field widths."""
+    rng = np.random.default_rng(seed_base + s)
+    t = np.arange(n_frames, dtype=np.float64) / fs
+    a = 32767.0 * 10 ** (-12 / 20)
+    z = np.zeros((n_frames, channels), dtype=np.complex128)
+    for ch in range(channels):
+        f = rng.uniform(40.0, 0.4 * fs, size=2) * np.array([1.0, -1.0])
+        ph = rng.uniform(0, 2 * np.pi, size=2)
+        z[:, ch] = a * (np.exp(1j * (2 * np.pi * f[0] * t + ph[0])) + np.exp(1j * (2 * np.pi * f[1] * t + ph[1])))
+        z[:, ch] += 32767.0 * 10 ** (-40 / 20) * (rng.standard_normal(n_frames) + 1j * rng.standard_normal(n_frames))
+    re, im = z.real, z.imag
+    if fmt == abi.FMT_CW_F64:
+        dt = np.dtype([("re", "<f8"), ("im", "<f8")])
+    elif fmt == abi.FMT_CW_I16:
+        dt = np.dtype([("re", "<i2"), ("im", "<i2")])
+        re = np.clip(np.round(re), -32768, 32767)
+        im = np.clip(np.round(im), -32768, 32767)
+    elif fmt == abi.FMT_CW_I16_F32:
+        dt = np.dtype([("re", "<i2"), ("im", "<f4")])
+        re = np.clip(np.round(re), -32768, 32767)
+    elif fmt == abi.FMT_CW_F32:
+        dt = np.dtype([("re", "<f4"), ("im", "<f4")])
+    else:
+        raise ValueError(fmt)
+    rec = np.zeros((n_frames, channels), dtype=dt)
+    rec["re"] = re
+    rec["im"] = im
+    return rec.reshape(-1).view(np.uint8)
+
+
 def batch_pcm(n_streams, n_frames, fs, channels=2, fmt=abi.FMT_I16, first=0):
-    rows = [stream_pcm(first + s, n_frames, fs, channels, fmt) for s in range(n_streams)]
+    gen = stream_cwave if fmt in abi.CW_FORMATS else stream_pcm
+    rows = [gen(first + s, n_frames, fs, channels, fmt) for s in range(n_streams)]
     return np.stack(rows)

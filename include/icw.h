@@ -72,6 +72,13 @@ extern "C" {
 #define ICW_FMT_I24  2
 #define ICW_FMT_I32  3
 #define ICW_FMT_F32  4
+/* complex (CWAVE) input sample formats, ICW_FMT_CW_F64 + HCW_FMT_* (cwave.h:70-80).  The analytic
+ * signal is used as read: the Hilbert converters are bypassed and keep their state, fades scale
+ * I and Q alike (xwave_unpack_csample, xwave_reader.c:939-966); mono feeds R with L's I/Q. */
+#define ICW_FMT_CW_F64      5     /* double Re, Im           HCW_FMT_PCM_DBL64 */
+#define ICW_FMT_CW_I16      6     /* int16 Re, Im            HCW_FMT_PCM_INT16 */
+#define ICW_FMT_CW_I16_F32  7     /* int16 Re, float Im      HCW_FMT_PCM_INT16_FLT32 */
+#define ICW_FMT_CW_F32      8     /* float Re, Im            HCW_FMT_PCM_FLT32 */
 /* render (sound_render.h:54-84) */
 #define ICW_QUANTZ_MID_TREAD 0
 #define ICW_QUANTZ_MID_RISER 1

@@ -358,10 +358,50 @@ static double unpack1(const unsigned char *p, unsigned fmt)
     }
 }
 
+/* CWAVE unpackers (xwave_reader.c:171-200; unpack_lsb.h:53-125): I/Q as stored, no scaling */
+static uint32_t le32(const unsigned char *p)
+{
+    return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
+}
+
+static double le_f32(const unsigned char *p)
+{
+    uint32_t u = le32(p);
+    float f;
+    memcpy(&f, &u, 4);
+    return (double)f;
+}
+
+static void unpack_iq(const unsigned char *p, unsigned fmt, double *vI, double *vQ)
+{
+    switch (fmt) {
+    case ICW_FMT_CW_F64: {
+        uint64_t a = (uint64_t)le32(p) | ((uint64_t)le32(p + 4) << 32);
+        uint64_t b = (uint64_t)le32(p + 8) | ((uint64_t)le32(p + 12) << 32);
+        memcpy(vI, &a, 8);
+        memcpy(vQ, &b, 8);
+        break;
+    }
+    case ICW_FMT_CW_I16:
+        *vI = (double)(int16_t)(p[0] | (p[1] << 8));
+        *vQ = (double)(int16_t)(p[2] | (p[3] << 8));
+        break;
+    case ICW_FMT_CW_I16_F32:
+        *vI = (double)(int16_t)(p[0] | (p[1] << 8));
+        *vQ = le_f32(p + 2);
+        break;
+    default:
+        *vI = le_f32(p);
+        *vQ = le_f32(p + 4);
+        break;
+    }
+}
+
+/* HRW_FMT_* sample sizes and CWAVE cw_slen (xwave_reader.c:246-252) */
 static unsigned fmt_size(unsigned fmt)
 {
-    static const unsigned sz[5] = {1, 2, 3, 4, 4};
-    return fmt < 5 ? sz[fmt] : 0;
+    static const unsigned sz[9] = {1, 2, 3, 4, 4, 16, 4, 6, 8};
+    return fmt < 9 ? sz[fmt] : 0;
 }
 
 /* amod_init normalisation (adv_modulator.c:216-331), shared with the product by semantics */
@@ -427,6 +467,14 @@ orc_stream *orc_stream_new(const icw_config *cfg, const icw_node *nodes, int n_n
 }
 
 void orc_stream_free(orc_stream *s) { free(s); }
+
+/* a new track's sample format (mod_context_fopen -> xwave_reader_create, in_cwave.c:207-236) */
+void orc_set_input(orc_stream *s, uint32_t sample_rate, uint32_t fmt, uint32_t channels)
+{
+    s->cfg.sample_rate = sample_rate;
+    s->cfg.in_format = fmt;
+    s->cfg.in_channels = channels;
+}
 
 /* mod_context_fopen + xwave_reader_create fade/tail arithmetic; returns n_tail */
 int64_t orc_stream_open(orc_stream *s, int64_t n_samples, uint32_t fade_in, uint32_t fade_out,
@@ -523,14 +571,23 @@ int orc_process(orc_stream *s, const void *in, unsigned n_frames, void *out, dou
         else if (ix > s->n_samples - s->n_fade_out && ix < s->n_samples)
             fade = ((double)(s->n_samples - ix)) / ((double)s->n_fade_out);
         const unsigned char *fp = ip + (size_t)f * fsz;
-        double val = unpack1(fp, cfg->in_format);
-        if (fade >= 0.0) val *= fade;
-        hq_process(val, &s->bus[0].lre, &s->bus[0].lim, &s->hq[0]);
-        if (nch > 1) {
-            val = unpack1(fp + csz, cfg->in_format);
+        if (cfg->in_format >= ICW_FMT_CW_F64) {
+            /* complex sample: no Hilbert; mono -> R = L; fade on all four (xwave_reader.c:939-966) */
+            lrc *b = &s->bus[0];
+            unpack_iq(fp, cfg->in_format, &b->lre, &b->lim);
+            if (nch > 1) unpack_iq(fp + csz, cfg->in_format, &b->rre, &b->rim);
+            else { b->rre = b->lre; b->rim = b->lim; }
+            if (fade >= 0.0) { b->lre *= fade; b->lim *= fade; b->rre *= fade; b->rim *= fade; }
+        } else {
+            double val = unpack1(fp, cfg->in_format);
             if (fade >= 0.0) val *= fade;
+            hq_process(val, &s->bus[0].lre, &s->bus[0].lim, &s->hq[0]);
+            if (nch > 1) {
+                val = unpack1(fp + csz, cfg->in_format);
+                if (fade >= 0.0) val *= fade;
+            }
+            hq_process(val, &s->bus[0].rre, &s->bus[0].rim, &s->hq[1]);
         }
-        hq_process(val, &s->bus[0].rre, &s->bus[0].rim, &s->hq[1]);
         ++s->pos;
         /* DSP list, tail -> head */
         for (int ni = cfg->bypass_list ? 0 : s->n_nodes - 1; ni >= 0; --ni) {

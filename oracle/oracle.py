@@ -33,6 +33,7 @@ def load():
         lib.orc_stream_new.restype = vp
         lib.orc_stream_new.argtypes = [C.POINTER(abi.Config), C.POINTER(abi.Node), C.c_int, C.POINTER(C.c_int)]
         lib.orc_stream_free.argtypes = [vp]
+        lib.orc_set_input.argtypes = [vp, C.c_uint32, C.c_uint32, C.c_uint32]
         lib.orc_stream_open.restype = C.c_int64
         lib.orc_stream_open.argtypes = [vp, C.c_int64, C.c_uint32, C.c_uint32, C.c_uint32, C.c_int, C.c_int]
         lib.orc_process.restype = C.c_int
@@ -84,6 +85,10 @@ class Stream:
             load().orc_stream_free(self.h)
         except Exception:
             pass
+
+    def set_input(self, sample_rate, fmt, channels):
+        load().orc_set_input(self.h, sample_rate, fmt, channels)
+        self.fsz = abi.FMT_BYTES[fmt] * channels
 
     def open(self, n_samples, fade_in_ms=0, fade_out_ms=0, sec_align=0, clr_nframe=0, clr_hilb=0):
         return load().orc_stream_open(self.h, n_samples, fade_in_ms, fade_out_ms, sec_align, clr_nframe, clr_hilb)

@@ -1,0 +1,110 @@
+"""GPU parity for the second input format and the general DSP-list form.
+
+CWAVE (complex) input, xwave_reader.c:171-200 and 939-966: the analytic signal is used as read.
+The Hilbert converters are bypassed and keep their state across tracks. Fades scale I and Q, and
+mono feeds R with L.
+
+Bus-form graphs, adv_modulator.c:636-751: these lists read a slot before it is written in the
+frame, which is a one-frame delay and includes feedback loops. They run in the serial graph
+kernel with the reference's own bus semantics.
+"""
+import numpy as np
+import pytest
+
+from in_cwave_amd import abi, graph, synth
+
+from test_gpu_parity import assert_parity, run_both
+
+pytestmark = pytest.mark.gpu
+
+CW = [abi.FMT_CW_F64, abi.FMT_CW_I16, abi.FMT_CW_I16_F32, abi.FMT_CW_F32]
+
+
+@pytest.fixture(autouse=True, params=["plain"])
+def k1_mode(request, monkeypatch):
+    monkeypatch.setenv("ICW_K1_MODE", request.param)
+    return request.param
+
+
+@pytest.mark.parametrize("fmt", CW)
+@pytest.mark.parametrize("ch", [1, 2])
+def test_cwave_formats_master_exact(oracle, icw, fmt, ch):
+    cfg = graph.default_config(44100, fmt=fmt, channels=ch, need24bits=True)
+    raw = synth.batch_pcm(3, 2500, 44100, channels=ch, fmt=fmt)
+    _, out, pre, ro, rp = run_both(oracle, icw, cfg, graph.graph_master_only(), raw, 2500)
+    assert_parity(out, pre, ro, rp, 3, exact_pre=True)
+
+
+@pytest.mark.parametrize("fmt", CW)
+def test_cwave_shift_master(oracle, icw, fmt):
+    cfg = graph.default_config(48000, fmt=fmt)
+    raw = synth.batch_pcm(8, 4000, 48000, fmt=fmt)
+    _, out, pre, ro, rp = run_both(oracle, icw, cfg, graph.graph_shift_master(), raw, 4000,
+                                   blocks=[576, 1000, 2424])
+    assert_parity(out, pre, ro, rp, 2, exact_pre=False)
+
+
+def test_cwave_fades_and_tpdf(oracle, icw):
+    cfg = graph.default_config(48000, fmt=abi.FMT_CW_F32)
+    cfg.render.render_type = abi.RENDER_TPDF
+    n = 30000
+    raw = synth.batch_pcm(2, n, 48000, fmt=abi.FMT_CW_F32)
+    ctx = icw.Context(cfg, graph.graph_master_only(), 2)
+    for s in range(2):
+        ctx.stream_open(s, n, fade_in_ms=100, fade_out_ms=200)
+    out, pre = ctx.process(raw, n, want_pre=True)
+    for s in range(2):
+        st = oracle.Stream(cfg, graph.graph_master_only())
+        st.open(n, 100, 200)
+        ro, rp = st.process(raw[s], n, want_pre=True)
+        assert np.array_equal(pre[s].view(np.uint64), rp.view(np.uint64))
+        assert np.array_equal(out[s], ro)
+
+
+def test_track_switch_keeps_hilbert_state(oracle, icw):
+    """WAV track -> CWAVE track -> WAV track in one context: the converters are idle during the
+    CWAVE track, and the second WAV track continues from their state (is_clr_hilb_trk FALSE)"""
+    fs = 48000
+    cfg = graph.default_config(fs)
+    nodes = graph.graph_master_only()
+    tracks = [(abi.FMT_I16, 2, 3000), (abi.FMT_CW_I16_F32, 1, 2000), (abi.FMT_I16, 2, 2500)]
+    ctx = icw.Context(cfg, nodes, 2)
+    sts = [oracle.Stream(cfg, nodes) for _ in range(2)]
+    for i, (fmt, ch, n) in enumerate(tracks):
+        raw = np.stack([synth.batch_pcm(1, n, fs, channels=ch, fmt=fmt, first=10 * i + s)[0] for s in range(2)])
+        ctx.set_input(fs, fmt, ch)
+        for s in range(2):
+            ctx.stream_open(s, n)
+        out, pre = ctx.process(raw, n, want_pre=True)
+        for s in range(2):
+            sts[s].set_input(fs, fmt, ch)
+            sts[s].open(n)
+            ro, rp = sts[s].process(raw[s], n, want_pre=True)
+            assert np.array_equal(pre[s].view(np.uint64), rp.view(np.uint64)), f"track {i} stream {s}"
+            assert np.array_equal(out[s], ro)
+
+
+# ------------------------------------------------------------------ bus-form DSP lists --------
+@pytest.mark.parametrize("mk,exact", [(graph.graph_pure_delay, False), (graph.graph_leaky_feedback, True),
+                                      (graph.graph_feedback_pm_shift, False), (graph.graph_long_chain, True)])
+def test_bus_form_graphs(oracle, icw, mk, exact):
+    cfg = graph.default_config(48000)
+    raw = synth.batch_pcm(6, 3000, 48000)
+    _, out, pre, ro, rp = run_both(oracle, icw, cfg, mk(), raw, 3000, blocks=[576, 1, 1423, 1000])
+    assert_parity(out, pre, ro, rp, 2, exact_pre=exact)
+
+
+def test_bus_form_cwave_gauss(oracle, icw):
+    cfg = graph.default_config(48000, fmt=abi.FMT_CW_F64, need24bits=True)
+    cfg.render.render_type = abi.RENDER_GAUSS
+    cfg.render.nshape_type = abi.NSHAPE_MEW44
+    raw = synth.batch_pcm(3, 2000, 48000, fmt=abi.FMT_CW_F64)
+    _, out, pre, ro, rp = run_both(oracle, icw, cfg, graph.graph_leaky_feedback(), raw, 2000)
+    assert_parity(out, pre, ro, rp, 3, exact_pre=True)
+
+
+def test_bus_form_more_streams_than_a_wave(oracle, icw):
+    cfg = graph.default_config(44100)
+    raw = synth.batch_pcm(70, 700, 44100)
+    _, out, pre, ro, rp = run_both(oracle, icw, cfg, graph.graph_leaky_feedback(), raw, 700)
+    assert_parity(out, pre, ro, rp, 2, exact_pre=True)

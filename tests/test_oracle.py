@@ -217,3 +217,65 @@ def test_graph_normalisation_amod_init(oracle):
     assert np.array_equal(s.process(raw, 500)[0], d.process(raw, 500)[0])
     two = oracle.Stream(cfg, [graph.master(), graph.master()])
     assert not two.accepted
+
+
+# ---------------------------------------------------------------- CWAVE input / bus form -------
+def _cw_config(fmt, ch, fs=48000):
+    return graph.default_config(fs, fmt=fmt, channels=ch)
+
+
+@pytest.mark.parametrize("fmt", [abi.FMT_CW_F64, abi.FMT_CW_I16, abi.FMT_CW_I16_F32, abi.FMT_CW_F32])
+def test_cwave_reads_analytic_signal_as_is(oracle, fmt):
+    """xwave_reader.c:171-200, 939-966: CWAVE samples go to the bus unscaled, without Hilbert;
+    Master S_RE / S_IM with gain 1 returns Re / Im exactly; mono feeds R with L"""
+    for ch in (1, 2):
+        raw = synth.stream_cwave(7, 1000, 48000, channels=ch, fmt=fmt)
+        rec = {abi.FMT_CW_F64: [("re", "<f8"), ("im", "<f8")], abi.FMT_CW_I16: [("re", "<i2"), ("im", "<i2")],
+               abi.FMT_CW_I16_F32: [("re", "<i2"), ("im", "<f4")], abi.FMT_CW_F32: [("re", "<f4"), ("im", "<f4")]}[fmt]
+        v = raw.view(np.dtype(rec)).reshape(1000, ch)
+        re, im = v["re"].astype(np.float64), v["im"].astype(np.float64)
+        if ch == 1:
+            re, im = np.repeat(re, 2, axis=1), np.repeat(im, 2, axis=1)
+        for tout, want in ((abi.S_RE, re), (abi.S_IM, im)):
+            st = oracle.Stream(_cw_config(fmt, ch), [graph.master(tout=tout, gain=1.0)])
+            _, pre = st.process(raw, 1000, want_pre=True)
+            assert np.array_equal(pre.view(np.uint64), want.view(np.uint64))
+
+
+def test_cwave_fade_scales_both_components(oracle):
+    raw = synth.stream_cwave(1, 9600, 48000, fmt=abi.FMT_CW_F32)
+    st = oracle.Stream(_cw_config(abi.FMT_CW_F32, 2), [graph.master(tout=abi.S_IM, gain=1.0)])
+    st.open(9600, fade_in_ms=50)
+    _, pre = st.process(raw, 9600, want_pre=True)
+    im = raw.view(np.dtype([("re", "<f4"), ("im", "<f4")])).reshape(9600, 2)["im"].astype(np.float64)
+    n_in = 50 * 48000 // 1000
+    fade = np.arange(n_in, dtype=np.float64) / n_in
+    # the node's mix starts from 0.0 (adv_modulator.c:655), so a faded -0.0 comes out as +0.0
+    assert np.array_equal(pre[:n_in].view(np.uint64), (0.0 + im[:n_in] * fade[:, None]).view(np.uint64))
+    assert np.array_equal(pre[n_in:].view(np.uint64), (0.0 + im[n_in:]).view(np.uint64))
+
+
+def test_bus_leaky_feedback_recurrence(oracle):
+    """a Mix node reading its own slot sees last frame's value (adv_modulator.c:655-665):
+    C[t] = ((0.0 + in[t]) + C[t-1]) * 0.5, then Master S_RE gain 1"""
+    raw = synth.stream_cwave(2, 800, 48000, fmt=abi.FMT_CW_F64)
+    nodes = [graph.master(inputs=("C",), tout=abi.S_RE, gain=1.0), graph.mix(inputs=("in", "C"), out="C", gain=0.5)]
+    st = oracle.Stream(_cw_config(abi.FMT_CW_F64, 2), nodes)
+    _, pre = st.process(raw, 800, want_pre=True)
+    x = raw.view(np.dtype([("re", "<f8"), ("im", "<f8")])).reshape(800, 2)["re"]
+    c = np.zeros(2)
+    want = np.zeros((800, 2))
+    for t in range(800):
+        c = ((0.0 + x[t]) + c) * 0.5
+        want[t] = c
+    assert np.array_equal(pre.view(np.uint64), want.view(np.uint64))
+
+
+def test_bus_pure_delay_is_one_frame_late(oracle):
+    """Mix(A->B) executes before Shift(in->A): B is last frame's A"""
+    raw = synth.stream_pcm(4, 1500, 48000)
+    cfg = graph.default_config(48000)
+    _, p1 = oracle.Stream(cfg, graph.graph_shift_master()).process(raw, 1500, want_pre=True)
+    _, p2 = oracle.Stream(cfg, graph.graph_pure_delay()).process(raw, 1500, want_pre=True)
+    assert np.all(p2[0] == 0.0)
+    assert np.array_equal(p2[1:].view(np.uint64), p1[:-1].view(np.uint64))

@@ -86,6 +86,14 @@ def e2e():
     imp[0] = imp[1] = 32767
     cases["quirk_impulse"] = (graph.default_config(48000), [graph.master(tout=abi.S_RE, gain=1.0)],
                               imp.view(np.uint8)[None, :])
+    # complex (CWAVE) input and lists with one-frame delays / feedback (bus form)
+    cases["cw_i16f32_shift"] = (graph.default_config(48000, fmt=abi.FMT_CW_I16_F32), graph.graph_shift_master(),
+                                synth.batch_pcm(2, 2400, 48000, fmt=abi.FMT_CW_I16_F32))
+    cases["cw_f64_mono_24"] = (graph.default_config(44100, fmt=abi.FMT_CW_F64, channels=1, need24bits=True),
+                               graph.graph_master_only(), synth.batch_pcm(1, 2205, 44100, channels=1, fmt=abi.FMT_CW_F64))
+    cases["fb_leaky"] = (graph.default_config(48000), graph.graph_leaky_feedback(), synth.batch_pcm(2, 2400, 48000))
+    cases["fb_pm_shift"] = (graph.default_config(48000), graph.graph_feedback_pm_shift(), synth.batch_pcm(2, 2400, 48000))
+    cases["delay_shift"] = (graph.default_config(48000), graph.graph_pure_delay(), synth.batch_pcm(2, 2400, 48000))
     for name, (cfg, nodes, raw) in cases.items():
         fsz = abi.FMT_BYTES[cfg.in_format] * cfg.in_channels
         nf = raw.shape[1] // fsz
