@@ -66,7 +66,16 @@ class Meters(C.Structure):
     _fields_ = [("clips", C.c_uint32 * 2), ("peak_db", C.c_double * 2), ("desubnorm", C.c_uint64)]
 
 
-# every function declared in include/icw.h: name -> (restype, argtypes)
+class CwaveHeader(C.Structure):
+    """icw_cwave_header (include/icw_cwave.h) = HCWAVE_V2 (cwave.h:48-60)"""
+    _fields_ = [("magic", C.c_char * 8), ("hsize", C.c_uint32), ("version", C.c_uint32), ("format", C.c_uint32),
+                ("n_channels", C.c_uint32), ("n_samples", C.c_uint32), ("sample_rate", C.c_uint32),
+                ("k_M", C.c_int32), ("n_crc32", C.c_uint32), ("k_beta", C.c_double)]
+
+
+CWAVE_HEADER_BYTES = 48
+
+# every function declared in include/icw.h, icw_amod.h, icw_cwave.h: name -> (restype, argtypes)
 _vp, _sz, _i, _u = C.c_void_p, C.c_size_t, C.c_int, C.c_uint
 SIGNATURES = {
     "icw_create": (_i, [C.POINTER(Config), C.POINTER(Node), _i, _i, _i, C.POINTER(_vp), C.POINTER(_i)]),
@@ -95,6 +104,12 @@ SIGNATURES = {
     "icw_get_state": (_i, [_vp, _i, _vp, _sz]),
     "icw_set_state": (_i, [_vp, _i, _vp, _sz]),
     "icw_last_timing": (_i, [_vp, C.POINTER(C.c_double), C.POINTER(_i)]),
+    "icw_cwave_parse": (_i, [_vp, _sz, C.c_int64, C.POINTER(CwaveHeader), C.POINTER(C.c_uint32),
+                             C.POINTER(C.c_uint32)]),
+    "icw_crc32_batch": (_i, [_vp, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64), _i, C.POINTER(C.c_uint32),
+                             C.POINTER(C.c_uint32), _u, _i, _vp]),
+    "icw_crc32_combine": (C.c_uint32, [C.c_uint32, C.c_uint32, C.c_uint64]),
+    "icw_cwave_check": (_i, [_vp, C.c_uint64, _u, _i, C.POINTER(C.c_uint32), C.POINTER(_i)]),
     "icw_version": (C.c_char_p, []),
     "icw_strerror": (C.c_char_p, [_i]),
 }

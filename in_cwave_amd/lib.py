@@ -144,3 +144,43 @@ class Context:
         n = (C.c_int * 2)()
         _check(self._lib.icw_last_timing(self.h, ms, n), "icw_last_timing")
         return (ms[0], ms[1]), (n[0], n[1])
+
+
+# ------------------------------------------------------------------ CWAVE files / CRC-32 -------
+def cwave_parse(header, file_size):
+    """icw_cwave_parse: the reference's CWAVE header checks (xwave_reader.c:243-300).  Returns
+    (header struct, ICW_FMT_CW_* format, frame bytes); raises IcwError for a refused file."""
+    lib = load()
+    b = np.frombuffer(bytes(header[:abi.CWAVE_HEADER_BYTES]), dtype=np.uint8).copy()
+    h = abi.CwaveHeader()
+    fmt, fb = C.c_uint32(), C.c_uint32()
+    _check(lib.icw_cwave_parse(_ptr(b), b.size, file_size, C.byref(h), C.byref(fmt), C.byref(fb)), "icw_cwave_parse")
+    return h, fmt.value, fb.value
+
+
+def crc32_batch(base, offsets, lengths, crc_in=None, device_ptrs=False, device=-1, hip_stream=None):
+    """icw_crc32_batch: CRC-32 (crc32.c) of the byte ranges [base+offsets[i], +lengths[i]) on the
+    GPU.  base: numpy uint8 array (host) or a torch uint8 CUDA tensor / int pointer (device_ptrs)."""
+    lib = load()
+    n = len(offsets)
+    off = (C.c_uint64 * max(1, n))(*[int(v) for v in offsets])
+    ln = (C.c_uint64 * max(1, n))(*[int(v) for v in lengths])
+    cin = (C.c_uint32 * max(1, n))(*[int(v) for v in crc_in]) if crc_in is not None else None
+    out = (C.c_uint32 * max(1, n))()
+    flags = abi.F_DEVICE_PTRS if device_ptrs else 0
+    _check(lib.icw_crc32_batch(_ptr(base), off, ln, n, cin, out, flags, device, hip_stream), "icw_crc32_batch")
+    return [int(out[i]) for i in range(n)]
+
+
+def crc32_combine(crc_a, crc_b, len_b):
+    return int(load().icw_crc32_combine(crc_a, crc_b, len_b))
+
+
+def cwave_check(image, device_ptrs=False, device=-1, size=None):
+    """icw_cwave_check: (crc, ok) with ok 1 / 0, or -1 for a V1 file without a stored CRC"""
+    lib = load()
+    size = image.numel() if hasattr(image, "numel") else (len(image) if size is None else size)
+    crc, ok = C.c_uint32(), C.c_int()
+    _check(lib.icw_cwave_check(_ptr(image), size, abi.F_DEVICE_PTRS if device_ptrs else 0, device,
+                               C.byref(crc), C.byref(ok)), "icw_cwave_check")
+    return crc.value, ok.value

@@ -730,3 +730,56 @@ double orc_mt_dclosed(void *m)
     uint32_t a = mt_u32((orc_mt *)m) >> 5, b = mt_u32((orc_mt *)m) >> 6;
     return (a * 67108864.0 + b) * (1.0 / 9007199254740991.0);
 }
+
+/* ------------------------------------------------------------------------ CRC-32 ---------- */
+/* crc32.c restated.  The reference builds the reflected table of POLYNOMIAL 0xEDB88320
+ * (crc32init), feeds the first four data bytes inverted into the register while shifting the
+ * inversion mask out (crc32update, first loop), runs them through four table steps when the mask
+ * empties (ini_), continues byte-wise, and inverts at the end (crc32final, which also finishes
+ * data shorter than four bytes).  Equivalent to the zlib CRC-32 -- tests/test_oracle.py pins it
+ * against zlib and against crc32.c itself compiled by oracle/Makefile. */
+typedef struct { uint32_t xor_mask, reg; } orc_crc;
+
+static uint32_t orc_crc_tab[256];
+
+static uint32_t orc_crc_4steps(uint32_t r)
+{
+    for (int i = 0; i < 4; ++i) r = (r >> 8) ^ orc_crc_tab[r & 255u];
+    return r;
+}
+
+void orc_crc32_init(orc_crc *t)
+{
+    if (!orc_crc_tab[1])
+        for (uint32_t i = 0; i < 256; ++i) {
+            uint32_t r = i;
+            for (int j = 0; j < 8; ++j) r = (r >> 1) ^ ((r & 1u) ? 0xEDB88320u : 0u);
+            orc_crc_tab[i] = r;
+        }
+    t->xor_mask = ~0u;
+    t->reg = 0;
+}
+
+void orc_crc32_update(orc_crc *t, const void *data, size_t len)
+{
+    const uint8_t *p = (const uint8_t *)data;
+    for (; t->xor_mask && len; --len, ++p) {
+        t->reg = (t->reg >> 8) | ((uint32_t)(uint8_t)~*p << 24);
+        t->xor_mask >>= 8;
+        if (!t->xor_mask) t->reg = orc_crc_4steps(t->reg);
+    }
+    for (; len; --len, ++p) t->reg = orc_crc_tab[(t->reg ^ *p) & 255u] ^ (t->reg >> 8);
+}
+
+uint32_t orc_crc32_final(orc_crc *t)
+{
+    return ~(t->xor_mask ? t->xor_mask ^ orc_crc_4steps(t->reg) : t->reg);
+}
+
+uint32_t orc_crc32(const void *data, size_t len)
+{
+    orc_crc t;
+    orc_crc32_init(&t);
+    orc_crc32_update(&t, data, len);
+    return orc_crc32_final(&t);
+}

@@ -59,6 +59,36 @@ def ref_seeds():
     np.savez_compressed(GOLD / "mt_ref_seeds.npz", **out)
 
 
+def crc_ref():
+    """CRC-32 of seeded random data by the REFERENCE crc32.c (oracle/_ref/libref_crc32.so), fed in
+    the block partitions given (crc32update chaining across reads, as check_cwave does)."""
+    lib = C.CDLL(str(ROOT / "oracle/_ref/libref_crc32.so"))
+
+    class Tmp(C.Structure):
+        _fields_ = [("xOr", C.c_uint32), ("temp", C.c_uint32)]
+
+    lib.crc32final.restype = C.c_uint32
+    cases = []
+    rng = np.random.default_rng(32)
+    for n, parts in [(0, [0]), (1, [1]), (3, [1, 2]), (4, [4]), (7, [2, 2, 3]), (9, [9]), (255, [100, 155]),
+                     (4096, [576 * 4, 4096 - 576 * 4]), (65537, [65537]), (100003, [3, 1, 99999])]:
+        data = rng.integers(0, 256, n, dtype=np.uint8).tobytes()
+        t = Tmp()
+        lib.crc32init(C.byref(t))
+        off = 0
+        for k in parts:
+            lib.crc32update(data[off:off + k], C.c_uint(k), C.byref(t))
+            off += k
+        cases.append({"seed_index": len(cases), "n": n, "parts": parts, "crc": int(lib.crc32final(C.byref(t)))})
+    check = b"123456789"
+    t = Tmp()
+    lib.crc32init(C.byref(t))
+    lib.crc32update(check, C.c_uint(9), C.byref(t))
+    doc = {"generator": "numpy.random.default_rng(32).integers(0, 256, n, uint8), cases in order",
+           "cases": cases, "check_123456789": int(lib.crc32final(C.byref(t)))}
+    (GOLD / "crc32_ref.json").write_text(json.dumps(doc, indent=1) + "\n")
+
+
 def e2e():
     from in_cwave_amd import abi, graph, synth
     from oracle import oracle as O
@@ -116,5 +146,6 @@ if __name__ == "__main__":
     if REF.is_dir():
         kat()
         ref_seeds()
+        crc_ref()
     e2e()
     print("golden fixtures written to", GOLD)

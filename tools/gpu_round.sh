@@ -18,6 +18,12 @@ for s in "$@"; do
     testall) step pytest_gpu 900 python -m pytest tests -m gpu -q; ok $? || exit 2 ;;
     bench) step bench 600 python bench.py --steps 3 --warmup 1 --no-cpu-baseline || exit 2 ;;
     benchfull) step bench_full 900 python bench.py || exit 2 ;;
+    crctest) step pytest_crc 600 python -m pytest tests/test_gpu_crc.py tests/test_gpu_cwave_graph.py -q -x; ok $? || exit 2 ;;
+    crcprof)
+      R=$(pwd); export TMPDIR=/tmp
+      ( cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/gpurun_out/crcprof" -o run \
+          -- python3 "$R/tools/bench_crc.py" --gib 4 --iters 5 ) > gpurun_out/crcprof.txt 2>&1
+      rc=$?; echo "[crcprof] rc=$rc" | tee -a gpurun_out/steps.txt; [ $rc -eq 0 ] || exit 2 ;;
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" || exit 2 ;;
     prof)
       R=$(pwd); export TMPDIR=/tmp
