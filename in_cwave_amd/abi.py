@@ -75,6 +75,18 @@ class CwaveHeader(C.Structure):
 
 CWAVE_HEADER_BYTES = 48
 
+CFG_VERSION = 10
+CFG_MAX_NODES = 64
+DSP_NAME_SIZE = 96
+
+
+class FileConfig(C.Structure):
+    """icw_file_config (include/icw_config.h): what an in_cwave.cfg defines"""
+    _fields_ = [("cfg", Config), ("sec_align", C.c_uint32), ("fade_in", C.c_uint32), ("fade_out", C.c_uint32),
+                ("clr_nframe", C.c_int32), ("clr_hilb", C.c_int32), ("subnorm_thr", C.c_double),
+                ("fp_check", C.c_int32), ("ver_config", C.c_uint32), ("n_nodes", C.c_int32),
+                ("nodes", Node * CFG_MAX_NODES), ("names", (C.c_char * DSP_NAME_SIZE) * CFG_MAX_NODES)]
+
 # every function declared in include/icw.h, icw_amod.h, icw_cwave.h: name -> (restype, argtypes)
 _vp, _sz, _i, _u = C.c_void_p, C.c_size_t, C.c_int, C.c_uint
 SIGNATURES = {
@@ -110,6 +122,9 @@ SIGNATURES = {
                              C.POINTER(C.c_uint32), _u, _i, _vp]),
     "icw_crc32_combine": (C.c_uint32, [C.c_uint32, C.c_uint32, C.c_uint64]),
     "icw_cwave_check": (_i, [_vp, C.c_uint64, _u, _i, C.POINTER(C.c_uint32), C.POINTER(_i)]),
+    "icw_config_load": (_i, [C.c_char_p, _sz, C.POINTER(FileConfig), C.POINTER(_i)]),
+    "icw_node_dsp_parse": (_i, [C.c_char_p, C.POINTER(Node), C.c_char_p, _sz]),
+    "icw_node_dsp_format": (_i, [C.POINTER(Node), C.c_char_p, C.c_char_p, _sz]),
     "icw_version": (C.c_char_p, []),
     "icw_strerror": (C.c_char_p, [_i]),
 }

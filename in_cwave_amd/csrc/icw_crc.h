@@ -7,7 +7,6 @@
 #include <stdint.h>
 
 #define ICW_CRC_CELL 65536u      /* bytes per workgroup cell */
-#define ICW_CRC_SEG  256u        /* bytes per lane segment (ICW_CRC_CELL / 256 lanes) */
 
 /* one non-empty byte range [start, end), offsets from the (16 B aligned) base */
 struct IcwCrcBuf {
@@ -24,8 +23,10 @@ struct IcwCrcArgs {
     int32_t n_bufs;
     uint64_t n_chunks;
     const uint32_t *tab;           /* [16][256] slice-by-16 tables */
-    const uint32_t *xseg;          /* [256] x^(8*256*k) mod P */
+    const uint32_t *dstride;       /* [4][256] byte tables of r -> r * x^(8*1024) */
+    const uint32_t *xlane;         /* [256] x^(8 * (16384 (3 - w) + 16 (63 - l))), t = 64 w + l */
     const uint32_t *xcell;         /* [64] x^(8*CELL*2^k) mod P */
+    uint32_t *pw;                  /* [max cells per range] x^(8*CELL*m), filled by icw_crc32_powers */
     uint32_t *raw;                 /* [n] raw CRC (preset 0, no inversion), padded to the cell grid */
 };
 

@@ -14,7 +14,7 @@
 #include "../../include/icw_cwave.h"
 #include "icw_crc.h"
 
-extern "C" hipError_t icw_launch_crc32(const IcwCrcArgs *a, int n_cu, hipStream_t st);
+extern "C" hipError_t icw_launch_crc32(const IcwCrcArgs *a, uint64_t max_cells, int n_cu, hipStream_t st);
 
 namespace {
 
@@ -49,7 +49,8 @@ uint32_t xinv8n(uint64_t n) { return gf_pow(gf_pow(kXinv, 8), n); }      /* x^(-
 
 struct Tables {
     uint32_t tab[16][256];
-    uint32_t xseg[256];
+    uint32_t dstride[4][256];
+    uint32_t xlane[256];
     uint32_t xcell[64];
 };
 
@@ -65,9 +66,12 @@ const Tables &tables()
         }
         for (int k = 1; k < 16; ++k)
             for (int b = 0; b < 256; ++b) t.tab[k][b] = (t.tab[k - 1][b] >> 8) ^ t.tab[0][t.tab[k - 1][b] & 255u];
-        const uint32_t xs = x8n(ICW_CRC_SEG);
-        t.xseg[0] = kOne;
-        for (int k = 1; k < 256; ++k) t.xseg[k] = gf_mul(t.xseg[k - 1], xs);
+        /* r * x^8192 is linear in r: one table per byte of r (bit i of r is x^(31-i)) */
+        const uint32_t k1k = x8n(1024);
+        for (int k = 0; k < 4; ++k)
+            for (uint32_t b = 0; b < 256; ++b) t.dstride[k][b] = gf_mul(b << (8 * k), k1k);
+        for (int w = 0; w < 4; ++w)
+            for (int l = 0; l < 64; ++l) t.xlane[w * 64 + l] = x8n(16384ull * (3 - w) + 16ull * (63 - l));
         t.xcell[0] = x8n(ICW_CRC_CELL);
         for (int k = 1; k < 64; ++k) t.xcell[k] = gf_mul(t.xcell[k - 1], t.xcell[k - 1]);
     });
@@ -165,7 +169,7 @@ int icw_crc32_batch(const void *base, const uint64_t *offsets, const uint64_t *l
         dbase = stage;
     }
     std::vector<IcwCrcBuf> bufs;
-    uint64_t n_chunks = 0;
+    uint64_t n_chunks = 0, max_cells = 0;
     for (int i = 0; i < n; ++i) {
         if (!lengths[i]) continue;
         IcwCrcBuf B;
@@ -177,16 +181,18 @@ int icw_crc32_batch(const void *base, const uint64_t *offsets, const uint64_t *l
         B.first_chunk = n_chunks;
         B.index = (uint32_t)i;
         n_chunks += B.last_cell - B.cell0 + 1;
+        if (B.last_cell - B.cell0 + 1 > max_cells) max_cells = B.last_cell - B.cell0 + 1;
         bufs.push_back(B);
     }
     const Tables &T = tables();
-    /* one device block: tables | raw[n] | bufs */
+    /* one device block: tables | raw[n] | bufs | pw[max_cells] */
     const size_t tab_b = sizeof(Tables), raw_b = (size_t)n * 4, buf_b = bufs.size() * sizeof(IcwCrcBuf);
     const size_t raw_off = (tab_b + 255) & ~(size_t)255, buf_off = (raw_off + raw_b + 255) & ~(size_t)255;
+    const size_t pw_off = (buf_off + buf_b + 255) & ~(size_t)255;
     unsigned char *blk = nullptr;
     int rc = ICW_OK;
     std::vector<uint32_t> raw(n, 0);
-    if (hipMalloc((void **)&blk, buf_off + buf_b + 16) != hipSuccess) rc = ICW_ENOMEM;
+    if (hipMalloc((void **)&blk, pw_off + max_cells * 4 + 16) != hipSuccess) rc = ICW_ENOMEM;
     if (rc == ICW_OK &&
         (hipMemcpyAsync(blk, &T, tab_b, hipMemcpyHostToDevice, st) != hipSuccess ||
          hipMemsetAsync(blk + raw_off, 0, raw_b, st) != hipSuccess ||
@@ -200,10 +206,12 @@ int icw_crc32_batch(const void *base, const uint64_t *offsets, const uint64_t *l
         a.n_bufs = (int32_t)bufs.size();
         a.n_chunks = n_chunks;
         a.tab = (const uint32_t *)(blk + offsetof(Tables, tab));
-        a.xseg = (const uint32_t *)(blk + offsetof(Tables, xseg));
+        a.dstride = (const uint32_t *)(blk + offsetof(Tables, dstride));
+        a.xlane = (const uint32_t *)(blk + offsetof(Tables, xlane));
         a.xcell = (const uint32_t *)(blk + offsetof(Tables, xcell));
+        a.pw = (uint32_t *)(blk + pw_off);
         a.raw = (uint32_t *)(blk + raw_off);
-        if (icw_launch_crc32(&a, n_cu, st) != hipSuccess) rc = ICW_EDEVICE;
+        if (icw_launch_crc32(&a, max_cells, n_cu, st) != hipSuccess) rc = ICW_EDEVICE;
     }
     if (rc == ICW_OK && (hipMemcpyAsync(raw.data(), blk + raw_off, raw_b, hipMemcpyDeviceToHost, st) != hipSuccess ||
                          hipStreamSynchronize(st) != hipSuccess))

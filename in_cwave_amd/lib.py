@@ -22,6 +22,13 @@ def load():
     if _lib is None:
         if not LIB_PATH.exists():
             raise IcwError(f"{LIB_PATH} is missing: run __graft_entry__.build() (no CPU fallback exists)")
+        # PyTorch-ROCm bundles its own HIP runtime; when both live in one process (torch tensors as
+        # device buffers) torch's must come up first, or its later initialisation finds no GPU.
+        try:
+            import torch
+            torch.cuda.is_available()
+        except ImportError:
+            pass
         lib = C.CDLL(str(LIB_PATH))
         for name, (res, args) in abi.SIGNATURES.items():
             fn = getattr(lib, name)
@@ -184,3 +191,37 @@ def cwave_check(image, device_ptrs=False, device=-1, size=None):
     _check(lib.icw_cwave_check(_ptr(image), size, abi.F_DEVICE_PTRS if device_ptrs else 0, device,
                                C.byref(crc), C.byref(ok)), "icw_cwave_check")
     return crc.value, ok.value
+
+
+# ------------------------------------------------------------------ in_cwave.cfg ingestion -----
+def config_load(text, sample_rate=48000, fmt=abi.FMT_I16, channels=2):
+    """icw_config_load on the text of an in_cwave.cfg (load_config, config.c:813-915).
+    Returns (ok, FileConfig, bad_line); on failure the FileConfig holds the defaults, as the
+    reference falls back to them."""
+    data = text.encode() if isinstance(text, str) else bytes(text)
+    fc = abi.FileConfig()
+    fc.cfg.sample_rate, fc.cfg.in_format, fc.cfg.in_channels = sample_rate, fmt, channels
+    bad = C.c_int()
+    rc = load().icw_config_load(data, len(data), C.byref(fc), C.byref(bad))
+    return rc == abi.OK, fc, bad.value
+
+
+def config_nodes(fc):
+    """the DSP list of a loaded config, head first, as icw_create takes it"""
+    return [fc.nodes[i] for i in range(fc.n_nodes)]
+
+
+def node_dsp_parse(args):
+    n = abi.Node()
+    name = C.create_string_buffer(abi.DSP_NAME_SIZE)
+    _check(load().icw_node_dsp_parse(args.encode() if isinstance(args, str) else args, C.byref(n), name,
+                                     abi.DSP_NAME_SIZE), "icw_node_dsp_parse")
+    return n, name.value.decode(errors="replace")
+
+
+def node_dsp_format(node, name=""):
+    buf = C.create_string_buffer(4096)
+    k = load().icw_node_dsp_format(C.byref(node), name.encode(), buf, 4096)
+    if k < 0:
+        _check(k, "icw_node_dsp_format")
+    return buf.value.decode()
