@@ -109,7 +109,9 @@ class Context:
         out = np.zeros((count, n_frames * osz), dtype=np.uint8)
         pre = np.zeros((count, n_frames, 2), dtype=np.float64) if want_pre else None
         flags = abi.F_DEBUG_PRE if want_pre else 0
-        _check(self._lib.icw_process_streams(self.h, first, count, _ptr(inp), inp.strides[0], _ptr(out),
+        # a length-1 leading axis may carry stride 0 (x[None, :]): the row length is the stride then
+        in_stride = inp.strides[0] if count > 1 else inp.shape[1]
+        _check(self._lib.icw_process_streams(self.h, first, count, _ptr(inp), in_stride, _ptr(out),
                                              out.strides[0], n_frames, flags, _ptr(pre), None),
                "icw_process_streams")
         return out, pre
