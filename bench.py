@@ -12,7 +12,10 @@ Metric: rendered output channel-samples per second (2 x frames/s), whole job ove
 Multi-GPU: one process per GPU, streams sharded (weak scaling, no collective on the data path);
 barrier + synchronize around the K timed steps, max elapsed over ranks.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--streams 256] [--frames 1048576]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c2|c3|c4|c5]
+
+--workload picks one of the BASELINE.json configs; the default, c2, is the one the
+headline metric is quoted on.  The others are measured for DESIGN.md, not for the bench line.
 """
 import argparse
 import json
@@ -36,7 +39,34 @@ K1_VALU_PER_SAMPLE = 100
 CYC_PER_FP64_VALU = 4.7
 PMC_FILE = ROOT / "profiles" / "r01_c2_pmc.json"
 FP64_PEAK_TFLOPS = 78.6        # MI355X FP64 vector (256 CU x 2.4 GHz x 128 flop/clk), vendor figure
-ALG_BYTES_PER_FRAME = 8        # C2 = 4 B in (2 x int16) + 4 B out (2 x int16)
+
+
+# SURVEY 8(d) configurations, per GPU: streams, frames per stream per step, fs, input format,
+# channels, DSP list, render, algorithmic bytes per frame (input + output)
+WORKLOADS = {
+    "c2": dict(streams=256, frames=1 << 20, fs=48000, fmt="i16", ch=2, graph="shift_master", render="round16",
+               bytes=8, desc="C2: 256 x 48kHz int16 stereo streams/GPU, Type-1 (order 19) Kahan quadrature "
+                             "Hilbert + Shift(+2/-2 Hz) + Master, 16-bit ROUND"),
+    "c3": dict(streams=4096, frames=1 << 18, fs=96000, fmt="i16", ch=1, graph="master_only", render="round16",
+               bytes=6, desc="C3: 4096 x 96kHz int16 mono streams/GPU, Hilbert + Master, 16-bit ROUND"),
+    "c4": dict(streams=2048, frames=1 << 18, fs=48000, fmt="i16", ch=2, graph="pm_shift_mix", render="round16",
+               bytes=8, desc="C4: 2048 x 48kHz int16 stereo streams/GPU, PM -> Shift -> Mix -> Master, 16-bit ROUND"),
+    "c5": dict(streams=256, frames=1 << 18, fs=192000, fmt="f32", ch=2, graph="master_only", render="tpdf24_mew44",
+               bytes=14, desc="C5: 256 x 192kHz float32 stereo streams/GPU, Hilbert + Master, 24-bit TPDF + "
+                              "MEW44 noise shaping"),
+}
+
+
+def workload_config(w):
+    from in_cwave_amd import abi, graph
+    fmt = {"i16": abi.FMT_I16, "f32": abi.FMT_F32}[w["fmt"]]
+    cfg = graph.default_config(w["fs"], fmt=fmt, channels=w["ch"], need24bits=w["render"].endswith("mew44"))
+    if w["render"] == "tpdf24_mew44":
+        cfg.render.render_type = abi.RENDER_TPDF
+        cfg.render.nshape_type = abi.NSHAPE_MEW44
+    nodes = {"shift_master": graph.graph_shift_master, "master_only": graph.graph_master_only,
+             "pm_shift_mix": graph.graph_pm_shift_mix}[w["graph"]]()
+    return cfg, nodes, fmt
 
 
 def parse():
@@ -44,9 +74,9 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--streams", type=int, default=256, help="streams per GPU (C2: 256)")
-    ap.add_argument("--frames", type=int, default=1 << 20, help="frames per stream per step (C2: 2^20)")
-    ap.add_argument("--fs", type=int, default=48000)
+    ap.add_argument("--workload", default="c2", choices=sorted(WORKLOADS))
+    ap.add_argument("--streams", type=int, default=None, help="streams per GPU (default: the workload's)")
+    ap.add_argument("--frames", type=int, default=None, help="frames per stream per step (default: the workload's)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-workers", type=int, default=16)
     ap.add_argument("--cpu-frames", type=int, default=1 << 25)
@@ -55,30 +85,31 @@ def parse():
 
 def _cpu_worker(args):
     """one CPU core: the oracle restatement (scalar C, -O2 -ffp-contract=off) over one stream"""
-    s, n_frames, fs = args
-    from in_cwave_amd import graph, synth
+    s, n_frames, wname = args
+    from in_cwave_amd import synth
     from oracle import oracle as O
-    cfg = graph.default_config(fs)
-    raw = synth.stream_pcm(s, n_frames, fs)
-    st = O.Stream(cfg, graph.graph_shift_master())
+    w = WORKLOADS[wname]
+    cfg, nodes, fmt = workload_config(w)
+    raw = synth.stream_pcm(s, n_frames, w["fs"], channels=w["ch"], fmt=fmt)
+    st = O.Stream(cfg, nodes)
     t0 = time.perf_counter()
     st.process(raw, n_frames)
     return time.perf_counter() - t0
 
 
-def cpu_baseline(workers, n_frames, fs):
+def cpu_baseline(workers, n_frames, wname):
     import multiprocessing as mp
     from oracle import oracle as O
     O.load()
     ctx = mp.get_context("spawn")
     t0 = time.perf_counter()
     with ctx.Pool(workers) as pool:
-        per = pool.map(_cpu_worker, [(s, n_frames, fs) for s in range(workers)])
+        per = pool.map(_cpu_worker, [(s, n_frames, wname) for s in range(workers)])
     wall = time.perf_counter() - t0
     busy = max(per)
     samples = 2.0 * n_frames * workers
     return {"value": samples / busy / 1e6, "unit": "Msamples/s", "cores": workers, "kind": "port",
-            "sample": f"{workers} streams x {n_frames} frames (C2 shape, oracle C restatement, one process "
+            "sample": f"{workers} streams x {n_frames} frames ({wname} shape, oracle C restatement, one process "
                       f"per core), per-core {2.0 * n_frames / np.mean(per) / 1e6:.3f} Msamples/s, wall {wall:.1f}s"}
 
 
@@ -100,19 +131,24 @@ def main():
     from in_cwave_amd import graph, synth
     from in_cwave_amd import lib as L
 
-    S, T, fs = a.streams, a.frames, a.fs
-    cfg = graph.default_config(fs)
-    ctx = L.Context(cfg, graph.graph_shift_master(), S, device=local)
-    # synthetic input of the C2 shape for this rank's shard of streams (SURVEY 8(d) generator);
-    # 16 distinct generated streams are tiled over the shard to bound setup time
+    W = WORKLOADS[a.workload]
+    S = a.streams or W["streams"]
+    T = a.frames or W["frames"]
+    fs = W["fs"]
+    cfg, nodes, fmt = workload_config(W)
+    ctx = L.Context(cfg, nodes, S, device=local)
+    # synthetic input of the workload's shape for this rank's shard of streams (SURVEY 8(d)
+    # generator); 16 distinct generated streams are tiled over the shard to bound setup time
     n_gen = min(S, 16)
     first = rank * S
-    gen = synth.batch_pcm(n_gen, T, fs, first=first)               # uint8 [n_gen, T*4]
-    d_in = torch.empty((S, T * 4), dtype=torch.uint8, device=dev)
+    gen = synth.batch_pcm(n_gen, T, fs, channels=W["ch"], fmt=fmt, first=first)   # uint8 [n_gen, T*fsz]
+    d_in = torch.empty((S, gen.shape[1]), dtype=torch.uint8, device=dev)
     g = torch.from_numpy(gen).to(dev)
     for s in range(S):
         d_in[s].copy_(g[s % n_gen])
-    d_out = torch.empty((S, T * 4), dtype=torch.uint8, device=dev)
+    del g
+    osz = 2 * ctx.render_size
+    d_out = torch.empty((S, T * osz), dtype=torch.uint8, device=dev)
     torch.cuda.synchronize()
     hip_stream = torch.cuda.current_stream(dev).cuda_stream
 
@@ -153,12 +189,13 @@ def main():
     frames_per_launch = float(S) * T * a.steps / max(1, k1_n)
     k1_avg_s = k1_ms / 1e3 / max(1, k1_n)
     k2_avg_s = k2_ms / 1e3 / max(1, k2_n)
-    achieved = ALG_BYTES_PER_FRAME * frames_per_launch / k1_avg_s / 1e9 if k1_avg_s > 0 else None
+    alg_bytes = W["bytes"]
+    achieved = alg_bytes * frames_per_launch / k1_avg_s / 1e9 if k1_avg_s > 0 else None
     flops_per_frame = 4 * 2 * (15 * 19 - 4) / 2    # the recurrence half of 1124 flops/frame
     traffic = None
     try:   # HBM bytes per launch of the same kernel/config from the committed PMC passes
         pmc = json.loads(PMC_FILE.read_text())
-        if int(pmc["frames_per_launch"]) == int(frames_per_launch):
+        if int(pmc["frames_per_launch"]) == int(frames_per_launch) and a.workload == "c2":
             traffic = next(v["hbm_bytes_corrected"] for k, v in pmc["kernels"].items() if "icw_iir_state" in k)
     except Exception:
         traffic = None
@@ -170,19 +207,19 @@ def main():
         "issue_bound": {"valu_per_sample": K1_VALU_PER_SAMPLE, "cycles_per_valu": CYC_PER_FP64_VALU,
                         "clock_ghz": CLOCK_GHZ, "floor_ms_per_launch": issue_floor_ms,
                         "frac": (issue_floor_ms / (k1_avg_s * 1e3)) if k1_avg_s else None},
-        "kernel": "icw_iir_state", "alg_bytes_per_frame": ALG_BYTES_PER_FRAME,
+        "kernel": "icw_iir_state", "alg_bytes_per_frame": alg_bytes,
         "frames_per_launch": frames_per_launch, "avg_launch_ms": k1_avg_s * 1e3,
         "output_kernel_avg_launch_ms": k2_avg_s * 1e3,
         "fp64_tflops_chain": (1124.0 * frames_per_launch / (k1_avg_s + k2_avg_s) / 1e12) if k1_avg_s else None,
         "fp64_peak_tflops": FP64_PEAK_TFLOPS,
-        "note": "latency-bound serial IIR recurrence: 1024 chains x ~78 dependent FP64 ops/sample (DESIGN.md)",
+        "note": f"issue-bound serial IIR recurrence: {4 * S} chains x ~100 FP64 VALU/sample (DESIGN.md)",
     }
     del flops_per_frame
 
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         try:
-            cpu = cpu_baseline(a.cpu_workers, a.cpu_frames, fs)
+            cpu = cpu_baseline(a.cpu_workers, a.cpu_frames, a.workload)
         except Exception as e:  # reported, never silently replaced
             cpu = {"error": repr(e)}
 
@@ -192,8 +229,7 @@ def main():
             "value": value, "unit": "Msamples/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
             "ms_per_step": ms_per_step, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
             "dtype": "f64", "data": "synthetic",
-            "config": {"workload": "C2: 256 x 48kHz int16 stereo streams/GPU, Type-1 (order 19) Kahan "
-                                   "quadrature Hilbert + Shift(+2/-2 Hz) + Master, 16-bit ROUND",
+            "config": {"workload": W["desc"],
                        "streams_per_gpu": S, "frames_per_stream_per_step": T, "fs": fs,
                        "parallelism": f"stream-shard x{world}"},
             "roofline": roof,

@@ -18,6 +18,10 @@ for s in "$@"; do
     testall) step pytest_gpu 900 python -m pytest tests -m gpu -q; ok $? || exit 2 ;;
     bench) step bench 600 python bench.py --steps 3 --warmup 1 --no-cpu-baseline || exit 2 ;;
     benchfull) step bench_full 900 python bench.py || exit 2 ;;
+    benchall)
+      for w in c2 c3 c4 c5; do
+        step bench_$w 600 python bench.py --workload $w --steps 3 --warmup 1 --no-cpu-baseline || exit 2
+      done ;;
     crctest) step pytest_crc 600 python -m pytest tests/test_gpu_crc.py tests/test_gpu_cwave_graph.py -q -x; ok $? || exit 2 ;;
     crcprof)
       R=$(pwd); export TMPDIR=/tmp
