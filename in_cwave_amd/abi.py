@@ -87,6 +87,26 @@ class FileConfig(C.Structure):
                 ("fp_check", C.c_int32), ("ver_config", C.c_uint32), ("n_nodes", C.c_int32),
                 ("nodes", Node * CFG_MAX_NODES), ("names", (C.c_char * DSP_NAME_SIZE) * CFG_MAX_NODES)]
 
+HTYPE_WFONLY, HTYPE_PCMW, HTYPE_EXT, HTYPE_CWAVE = 0, 1, 2, 3
+
+
+class WavInfo(C.Structure):
+    """icw_wav_info (include/icw_reader.h)"""
+    _fields_ = [("fmt", C.c_uint32), ("channels", C.c_uint32), ("sample_rate", C.c_uint32),
+                ("frame_bytes", C.c_uint32), ("n_samples", C.c_int64), ("data_offset", C.c_int64),
+                ("htype", C.c_uint32), ("reserved_", C.c_uint32)]
+
+
+class BatchOpts(C.Structure):
+    _fields_ = [("fade_in_ms", C.c_uint32), ("fade_out_ms", C.c_uint32), ("sec_align", C.c_uint32),
+                ("block_frames", C.c_int32), ("device", C.c_int32), ("reserved_", C.c_int32)]
+
+
+class BatchStats(C.Structure):
+    _fields_ = [("n_files", C.c_int32), ("n_groups", C.c_int32), ("frames_in", C.c_uint64),
+                ("frames_out", C.c_uint64), ("wall_s", C.c_double), ("io_s", C.c_double)]
+
+
 # every function declared in include/icw.h, icw_amod.h, icw_cwave.h: name -> (restype, argtypes)
 _vp, _sz, _i, _u = C.c_void_p, C.c_size_t, C.c_int, C.c_uint
 SIGNATURES = {
@@ -125,6 +145,10 @@ SIGNATURES = {
     "icw_config_load": (_i, [C.c_char_p, _sz, C.POINTER(FileConfig), C.POINTER(_i)]),
     "icw_node_dsp_parse": (_i, [C.c_char_p, C.POINTER(Node), C.c_char_p, _sz]),
     "icw_node_dsp_format": (_i, [C.POINTER(Node), C.c_char_p, C.c_char_p, _sz]),
+    "icw_wav_parse_file": (_i, [C.c_char_p, C.POINTER(WavInfo)]),
+    "icw_transcode_files": (_i, [C.POINTER(Config), C.POINTER(Node), _i, C.POINTER(C.c_char_p),
+                                 C.POINTER(C.c_char_p), _i, C.POINTER(BatchOpts), C.POINTER(BatchStats),
+                                 C.POINTER(_i)]),
     "icw_version": (C.c_char_p, []),
     "icw_strerror": (C.c_char_p, [_i]),
 }

@@ -227,3 +227,33 @@ def node_dsp_format(node, name=""):
     if k < 0:
         _check(k, "icw_node_dsp_format")
     return buf.value.decode()
+
+
+# ------------------------------------------------------------------ WAV / CWAVE files ---------
+def wav_parse_file(path):
+    """icw_wav_parse_file: the reference's reader acceptance (xwave_reader_create); raises for a
+    refused file"""
+    info = abi.WavInfo()
+    _check(load().icw_wav_parse_file(str(path).encode(), C.byref(info)), "icw_wav_parse_file")
+    return info
+
+
+def transcode_files(cfg, nodes, in_paths, out_paths, fade_in_ms=0, fade_out_ms=0, sec_align=0,
+                    block_frames=0, device=-1):
+    """icw_transcode_files: many files through the GPU path; returns (stats, per-file status)"""
+    n = len(in_paths)
+    ins = (C.c_char_p * max(1, n))(*[str(p).encode() for p in in_paths])
+    outs = (C.c_char_p * max(1, n))(*[str(p).encode() for p in out_paths])
+    arr = graph_nodes(nodes)
+    o = abi.BatchOpts(fade_in_ms, fade_out_ms, sec_align, block_frames, device, 0)
+    st = abi.BatchStats()
+    status = (C.c_int * max(1, n))()
+    rc = load().icw_transcode_files(C.byref(cfg), arr, len(nodes), ins, outs, n, C.byref(o), C.byref(st), status)
+    return rc, st, [status[i] for i in range(n)]
+
+
+def graph_nodes(nodes):
+    arr = (abi.Node * max(1, len(nodes)))()
+    for i, nd in enumerate(nodes):
+        arr[i] = nd
+    return arr
