@@ -135,6 +135,8 @@ struct IcwK3Args {
     unsigned long long *peak_bits; /* [n_streams][2] */
     int32_t n_gen, mt_pitch;
     IcwRenderK rk;
+    double *dith;                  /* [n_gen][dith_pitch] rnd * dth_mul per sample (K3a -> K3b); null: ROUND */
+    size_t dith_pitch;
 };
 
 /* Arguments of the output kernel (frame-parallel: Kahan output sums, unmix, graph, render). */

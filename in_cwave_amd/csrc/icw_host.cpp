@@ -26,6 +26,7 @@ extern "C" hipError_t icw_launch_unpack(const IcwK0Args *a, hipStream_t st);
 extern "C" hipError_t icw_launch_iir_pair(const IcwK1Args *a, int nord, int kahan, int subn, hipStream_t st);
 extern "C" hipError_t icw_launch_iir_state(const IcwK1Args *a, int nord, int kahan, int subn, hipStream_t st);
 extern "C" hipError_t icw_launch_render(const IcwK3Args *a, hipStream_t st);
+extern "C" hipError_t icw_launch_dither(const IcwK3Args *a, hipStream_t st);
 extern "C" hipError_t icw_launch_output(const IcwK2Args *a, int nord, int kahan, hipStream_t st);
 extern "C" hipError_t icw_launch_graph_serial(const IcwK4Args *a, hipStream_t st);
 extern "C" hipError_t icw_launch_advance(const IcwAdvArgs *a, hipStream_t st);
@@ -87,6 +88,11 @@ struct icw_ctx {
     unsigned long long *info_nframe[2] = {nullptr, nullptr};
     hipStream_t stream2 = nullptr;
     hipEvent_t k1done[2] = {nullptr, nullptr}, k2done[2] = {nullptr, nullptr}, join = nullptr;
+    /* dither generation (K3a) runs on its own stream, double-buffered like the block scratch */
+    hipStream_t stream3 = nullptr;
+    hipEvent_t ditdone[2] = {nullptr, nullptr};
+    double *dith[2] = {nullptr, nullptr};
+    size_t dith_bytes[2] = {0, 0};
     unsigned char *d_in = nullptr, *d_out = nullptr;
     size_t d_in_bytes = 0, d_out_bytes = 0;
     double *d_pre = nullptr;
@@ -347,6 +353,11 @@ void free_all(icw_ctx *c)
                     c->info_nframe[0], c->info_nframe[1], c->d_in, c->d_out, c->d_pre};
     for (void *p : ptrs)
         if (p) hipFree(p);
+    for (double *d : {c->dith[0], c->dith[1]})
+        if (d) hipFree(d);
+    for (hipEvent_t e : {c->ditdone[0], c->ditdone[1]})
+        if (e) hipEventDestroy(e);
+    if (c->stream3) hipStreamDestroy(c->stream3);
     for (hipEvent_t e : {c->k1done[0], c->k1done[1], c->k2done[0], c->k2done[1], c->join})
         if (e) hipEventDestroy(e);
     if (c->stream2) hipStreamDestroy(c->stream2);
@@ -461,9 +472,11 @@ int icw_create(const icw_config *cfg, const icw_node *nodes, int n_nodes, int n_
         rc = ICW_EDEVICE;
     if (rc == ICW_OK && hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) rc = ICW_EDEVICE;
     if (rc == ICW_OK && hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking) != hipSuccess) rc = ICW_EDEVICE;
+    if (rc == ICW_OK && hipStreamCreateWithFlags(&c->stream3, hipStreamNonBlocking) != hipSuccess) rc = ICW_EDEVICE;
     for (int p = 0; p < 2 && rc == ICW_OK; ++p)
         if (hipEventCreateWithFlags(&c->k1done[p], hipEventDisableTiming) != hipSuccess ||
-            hipEventCreateWithFlags(&c->k2done[p], hipEventDisableTiming) != hipSuccess)
+            hipEventCreateWithFlags(&c->k2done[p], hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&c->ditdone[p], hipEventDisableTiming) != hipSuccess)
             rc = ICW_EDEVICE;
     if (rc == ICW_OK && hipEventCreateWithFlags(&c->join, hipEventDisableTiming) != hipSuccess) rc = ICW_EDEVICE;
     if (rc != ICW_OK) {
@@ -680,9 +693,14 @@ int icw_process_streams(icw_ctx *c, int first, int count, const void *in, size_t
     const bool cw = cfg.in_format >= ICW_FMT_CW_F64;
     const bool bus = c->prog.is_bus;
     if (bus && grow((void **)&c->iq, &c->iq_bytes, S * (size_t)Tb * 4 * sizeof(double))) return ICW_ENOMEM;
-    hipStream_t st2 = c->stream2;
-    /* second stream starts after everything already queued on st (inputs, previous calls) */
-    if (hipEventRecord(c->join, st) != hipSuccess || hipStreamWaitEvent(st2, c->join, 0) != hipSuccess)
+    hipStream_t st2 = c->stream2, st3 = c->stream3;
+    const bool dither = c->serial_render && cfg.render.render_type != ICW_RENDER_ROUND;
+    if (dither)
+        for (int p = 0; p < n_sets; ++p)
+            if (grow((void **)&c->dith[p], &c->dith_bytes[p], S * 2 * (size_t)Tb * sizeof(double))) return ICW_ENOMEM;
+    /* the other streams start after everything already queued on st (inputs, previous calls) */
+    if (hipEventRecord(c->join, st) != hipSuccess || hipStreamWaitEvent(st2, c->join, 0) != hipSuccess ||
+        hipStreamWaitEvent(st3, c->join, 0) != hipSuccess)
         return ICW_EDEVICE;
 
     DevState &ds = c->st;
@@ -833,6 +851,15 @@ int icw_process_streams(icw_ctx *c, int first, int count, const void *in, size_t
             a3.n_gen = count * 2;
             a3.mt_pitch = c->n_streams * 2;
             a3.rk = c->rk;
+            if (dither) {
+                /* K3a for this block on its own stream: dith[p] was last read by K3b of block b-2 */
+                a3.dith = c->dith[p];
+                a3.dith_pitch = (size_t)Tb;
+                if (b >= 2 && hipStreamWaitEvent(st3, c->k2done[p], 0) != hipSuccess) return ICW_EDEVICE;
+                if (icw_launch_dither(&a3, st3) != hipSuccess || hipEventRecord(c->ditdone[p], st3) != hipSuccess ||
+                    hipStreamWaitEvent(st2, c->ditdone[p], 0) != hipSuccess)
+                    return ICW_EDEVICE;
+            }
             if (icw_launch_render(&a3, st2) != hipSuccess) return ICW_EDEVICE;
         }
         if (timing) hipEventRecord(c->ev[4 * b + 3], st2);

@@ -1035,98 +1035,174 @@ __device__ __forceinline__ double icw_mt_dsopen(uint32_t *mt, int lane, int &idx
 
 #define ICW_SQRT6 (2.4494897427831780981972840747059)
 
-template <int KIND>
-__global__ __launch_bounds__(64) void icw_render_serial(IcwK3Args a)
+/* Dither generation (K3a): the random term rnd * dth_mul of sound_render_value
+ * (sound_render.c:711-756) for every sample of the block.  It depends only on the channel's MT19937
+ * state and the sloped-TPDF memory, never on the audio, so it runs on its own stream ahead of /
+ * beside the Hilbert and output kernels; one lane per render channel, MT words in LDS. */
+template <int RT>
+__global__ __launch_bounds__(64) void icw_dither_gen(IcwK3Args a)
 {
     __shared__ uint32_t mt[624 * 64];
     const int lane = threadIdx.x;
     const int g0 = blockIdx.x * 64 + lane;
     const bool valid = g0 < a.n_gen;
     const int g = valid ? g0 : a.n_gen - 1;
-    const int s = g >> 1, ch = g & 1;
     for (int i = 0; i < 624; ++i) mt[i * 64 + lane] = a.mt[(size_t)i * a.mt_pitch + g];
     int idx = a.mt_idx[g];
     double *rs = a.rs + (size_t)g * ICW_RSTATE;
-    double prev_rnd = rs[0], prev_err = rs[1];
-    constexpr int NM = ICW_MAX_NS_TAPS;
-    double E[NM], O[NM];
-#pragma unroll
-    for (int i = 0; i < NM; ++i) { E[i] = rs[2 + i]; O[i] = rs[2 + NM + i]; }
-    const IcwRenderK &k = a.rk;
-    const int nn = k.ns_n;
-    const int osz = k.is24 ? 3 : 2;
-    const double *pp = a.pre + (size_t)s * a.pre_stride + ch;
-    unsigned char *op = a.out + (size_t)s * a.out_stride + (size_t)ch * osz;
-    unsigned clips = 0;
-    double pk = 0.0;
+    double prev_rnd = rs[0];
+    const double dth_mul = a.rk.dth_mul;
+    double *dd = a.dith + (size_t)g * a.dith_pitch;
     for (int t = 0; t < a.T; ++t) {
-        double input = pp[(size_t)t * 2];
-        double rnd = 0.0, tr;
-        switch (k.render_type) {
-        case ICW_RENDER_RPDF: rnd = icw_mt_dsopen(mt, lane, idx) / ICW_SQRT2; break;
-        case ICW_RENDER_TPDF:
+        double rnd, tr;
+        if (RT == ICW_RENDER_RPDF) {
+            rnd = icw_mt_dsopen(mt, lane, idx) / ICW_SQRT2;
+        } else if (RT == ICW_RENDER_TPDF) {
             rnd = icw_mt_dsopen(mt, lane, idx);
             rnd += icw_mt_dsopen(mt, lane, idx);
             rnd /= 2.0;
-            break;
-        case ICW_RENDER_STPDF:
+        } else if (RT == ICW_RENDER_STPDF) {
             rnd = ((tr = icw_mt_dsopen(mt, lane, idx)) - prev_rnd) / 2.0;
             prev_rnd = tr;
-            break;
-        case ICW_RENDER_GAUSS:
+        } else {
             rnd = icw_mt_dsopen(mt, lane, idx);
             for (int i = 1; i < 12; ++i) rnd += icw_mt_dsopen(mt, lane, idx);
             rnd /= (2.0 * ICW_SQRT6);
-            break;
-        default: break;
         }
-        input = (input * k.norm_mul) - prev_err;
-        double q = input + (rnd * k.dth_mul);
-        int delta;
-        if (q < 0.0) { q -= k.round_offset; delta = k.sign_delta; }
-        else { q += k.round_offset; delta = 0; }
-        const double aq = fabs(q);
-        pk = aq > pk ? aq : pk;
-        if (q >= k.hi) { q = k.hi - 1.0; ++clips; }
-        if (q <= k.lo) { q = k.lo + 1.0; ++clips; }
-        int val = (isnan(q) ? (int)0x80000000 : (int)q) + delta;
-        /* noise shaping for the next sample (ns_empty / ns_fir / ns_iir) */
-        const double ev = (double)val - input;
-        double res = 0.0;
-        if (KIND == 1) {
-#pragma unroll
-            for (int i = NM - 1; i > 0; --i) E[i] = E[i - 1];
-            E[0] = ev;
-#pragma unroll
-            for (int i = 0; i < NM; ++i)
-                if (i < nn) res += k.ns_c[i] * E[i];
-        } else if (KIND == 2) {
-#pragma unroll
-            for (int i = NM - 1; i > 0; --i) E[i] = E[i - 1];
-            E[0] = ev;
-#pragma unroll
-            for (int i = 0; i < NM; ++i)
-                if (i < nn) res += k.ns_c[i] * E[i] - k.ns_c[i + nn] * O[i];
-#pragma unroll
-            for (int i = NM - 1; i > 0; --i) O[i] = O[i - 1];
-            O[0] = res;
-        }
-        prev_err = res;
-        val <<= k.norm_shift;
-        if (valid) {
-            unsigned char *o = op + (size_t)t * 2 * osz;
-            o[0] = (unsigned char)val;
-            o[1] = (unsigned char)(val >> 8);
-            if (k.is24) o[2] = (unsigned char)(val >> 16);
-        }
+        if (valid) dd[t] = rnd * dth_mul;
     }
     if (!valid) return;
     for (int i = 0; i < 624; ++i) a.mt[(size_t)i * a.mt_pitch + g] = mt[i * 64 + lane];
     a.mt_idx[g] = idx;
     rs[0] = prev_rnd;
+}
+
+/* Shaper history as a ring of R values (R = ICW_MAX_NS_TAPS for the FIR shapers, 4 for the
+ * order-4 IIR shapers; R divides the unroll length ICW_MAX_NS_TAPS): at unrolled step J the newest
+ * value goes to slot J mod R, so age i lives in slot (J - i) mod R -- compile-time indices, no
+ * register moves (the reference's ring with a decrementing write pointer, sound_render.c:403-489). */
+template <int R>
+__device__ __forceinline__ void icw_ring_rotate1(double (&X)[R])
+{
+    const double r0 = X[0];
+#pragma unroll
+    for (int k = 0; k < R - 1; ++k) X[k] = X[k + 1];
+    X[R - 1] = r0;
+}
+
+/* One sample of sound_render_value after the dither term (sound_render.c:754-809). */
+template <int KIND, int R, int J>
+__device__ __forceinline__ int icw_render_step(double input, double d, double &prev_err, double (&E)[R],
+                                               double (&O)[R], const IcwRenderK &k, int nn, unsigned &clips,
+                                               double &pk)
+{
+    input = (input * k.norm_mul) - prev_err;
+    double q = input + d;
+    int delta;
+    if (q < 0.0) { q -= k.round_offset; delta = k.sign_delta; }
+    else { q += k.round_offset; delta = 0; }
+    const double aq = fabs(q);
+    pk = aq > pk ? aq : pk;
+    if (q >= k.hi) { q = k.hi - 1.0; ++clips; }
+    if (q <= k.lo) { q = k.lo + 1.0; ++clips; }
+    int val = (isnan(q) ? (int)0x80000000 : (int)q) + delta;
+    /* noise shaping for the next sample (ns_empty / ns_fir / ns_iir) */
+    const double ev = (double)val - input;
+    double res = 0.0;
+    if (KIND == 1) {
+        E[J % R] = ev;
+#pragma unroll
+        for (int i = 0; i < R; ++i)
+            if (i < nn) res += k.ns_c[i] * E[(J - i + 2 * R) % R];
+    } else if (KIND == 2) {
+        E[J % R] = ev;
+#pragma unroll
+        for (int i = 0; i < R; ++i)
+            if (i < nn) res += k.ns_c[i] * E[(J - i + 2 * R) % R] - k.ns_c[i + nn] * O[(J - 1 - i + 2 * R) % R];
+        O[J % R] = res;
+    }
+    prev_err = res;
+    return val << k.norm_shift;
+}
+
+template <int KIND, int R, int J0>
+__device__ __forceinline__ void icw_render_block(const double (&xin)[ICW_MAX_NS_TAPS], const double (&dv)[ICW_MAX_NS_TAPS],
+                                                 double &prev_err, double (&E)[R], double (&O)[R], const IcwRenderK &k,
+                                                 int nn, unsigned &clips, double &pk, unsigned char *o, int osz, int lim,
+                                                 bool valid)
+{
+    if constexpr (J0 < ICW_MAX_NS_TAPS) {
+        if (J0 < lim) {
+            const int val = icw_render_step<KIND, R, J0>(xin[J0], dv[J0], prev_err, E, O, k, nn, clips, pk);
+            if (valid) {
+                unsigned char *q = o + (size_t)J0 * 2 * osz;
+                q[0] = (unsigned char)val;
+                q[1] = (unsigned char)(val >> 8);
+                if (osz == 3) q[2] = (unsigned char)(val >> 16);
+            }
+            icw_render_block<KIND, R, J0 + 1>(xin, dv, prev_err, E, O, k, nn, clips, pk, o, osz, lim, valid);
+        }
+    }
+}
+
+/* Render (K3b): the serial remainder of sound_render_value -- scale, error feedback, rounding,
+ * clips, peak, noise shaper -- with the dither term from K3a.  One lane per channel, samples in
+ * blocks of ICW_MAX_NS_TAPS (a multiple of the ring period): the block's inputs are loaded
+ * before use.  rs keeps the shaper history by age (0 = newest), 20 + 20 slots. */
+template <int KIND, int R>
+__global__ __launch_bounds__(64) void icw_render_serial(IcwK3Args a)
+{
+    constexpr int NM = ICW_MAX_NS_TAPS;
+    static_assert(NM % R == 0, "ring period must divide the unroll");
+    const int lane = threadIdx.x;
+    const int g0 = blockIdx.x * 64 + lane;
+    const bool valid = g0 < a.n_gen;
+    const int g = valid ? g0 : a.n_gen - 1;
+    const int s = g >> 1, ch = g & 1;
+    double *rs = a.rs + (size_t)g * ICW_RSTATE;
+    double prev_err = rs[1];
+    double E[R], O[R];
+    /* block start: age i sits in slot (-1 - i) mod R */
+#pragma unroll
+    for (int i = 0; i < R; ++i) { E[(R - 1 - i) % R] = rs[2 + i]; O[(R - 1 - i) % R] = rs[2 + NM + i]; }
+    const IcwRenderK &k = a.rk;
+    const int nn = k.ns_n;
+    const int osz = k.is24 ? 3 : 2;
+    const double *pp = a.pre + (size_t)s * a.pre_stride + ch;
+    const double *dp = a.dith ? a.dith + (size_t)g * a.dith_pitch : nullptr;
+    unsigned char *op = a.out + (size_t)s * a.out_stride + (size_t)ch * osz;
+    unsigned clips = 0;
+    double pk = 0.0;
+    const int T = a.T;
+    int t = 0;
+    double xin[NM], dv[NM];
+    for (; t + NM <= T; t += NM) {
+#pragma unroll
+        for (int j = 0; j < NM; ++j) {
+            xin[j] = pp[(size_t)(t + j) * 2];
+            dv[j] = dp ? dp[t + j] : 0.0;   /* ROUND: rnd * dth_mul == 0.0 * dth_mul */
+        }
+        icw_render_block<KIND, R, 0>(xin, dv, prev_err, E, O, k, nn, clips, pk, op + (size_t)t * 2 * osz, osz, NM,
+                                     valid);
+    }
+    const int rem = T - t;
+    if (rem > 0) {
+#pragma unroll
+        for (int j = 0; j < NM; ++j) {
+            xin[j] = j < rem ? pp[(size_t)(t + j) * 2] : 0.0;
+            dv[j] = (j < rem && dp) ? dp[t + j] : 0.0;
+        }
+        icw_render_block<KIND, R, 0>(xin, dv, prev_err, E, O, k, nn, clips, pk, op + (size_t)t * 2 * osz, osz, rem,
+                                     valid);
+        /* back to the block-start mapping: rotate left by rem mod R */
+#pragma unroll
+        for (int r = 1; r < NM; ++r)
+            if (r <= rem) { icw_ring_rotate1<R>(E); icw_ring_rotate1<R>(O); }
+    }
+    if (!valid) return;
     rs[1] = prev_err;
 #pragma unroll
-    for (int i = 0; i < NM; ++i) { rs[2 + i] = E[i]; rs[2 + NM + i] = O[i]; }
+    for (int i = 0; i < R; ++i) { rs[2 + i] = E[(R - 1 - i) % R]; rs[2 + NM + i] = O[(R - 1 - i) % R]; }
     if (clips) atomicAdd(&a.clips[g], clips);
     if (pk > 0.0) atomicMax(&a.peak_bits[g], (unsigned long long)__double_as_longlong(pk));
 }
@@ -1200,13 +1276,29 @@ static hipError_t launch_k2_t(const IcwK2Args &a, hipStream_t st)
     return hipGetLastError();
 }
 
+extern "C" hipError_t icw_launch_dither(const IcwK3Args *a, hipStream_t st)
+{
+    const int blocks = (a->n_gen + 63) / 64;
+    switch (a->rk.render_type) {
+    case ICW_RENDER_RPDF: hipLaunchKernelGGL(icw_dither_gen<ICW_RENDER_RPDF>, dim3(blocks), dim3(64), 0, st, *a); break;
+    case ICW_RENDER_TPDF: hipLaunchKernelGGL(icw_dither_gen<ICW_RENDER_TPDF>, dim3(blocks), dim3(64), 0, st, *a); break;
+    case ICW_RENDER_STPDF: hipLaunchKernelGGL(icw_dither_gen<ICW_RENDER_STPDF>, dim3(blocks), dim3(64), 0, st, *a); break;
+    case ICW_RENDER_GAUSS: hipLaunchKernelGGL(icw_dither_gen<ICW_RENDER_GAUSS>, dim3(blocks), dim3(64), 0, st, *a); break;
+    default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
 extern "C" hipError_t icw_launch_render(const IcwK3Args *a, hipStream_t st)
 {
     const int blocks = (a->n_gen + 63) / 64;
     switch (a->rk.ns_kind) {
-    case 0: hipLaunchKernelGGL(icw_render_serial<0>, dim3(blocks), dim3(64), 0, st, *a); break;
-    case 1: hipLaunchKernelGGL(icw_render_serial<1>, dim3(blocks), dim3(64), 0, st, *a); break;
-    default: hipLaunchKernelGGL(icw_render_serial<2>, dim3(blocks), dim3(64), 0, st, *a); break;
+    case 0: hipLaunchKernelGGL((icw_render_serial<0, 1>), dim3(blocks), dim3(64), 0, st, *a); break;
+    case 1: hipLaunchKernelGGL((icw_render_serial<1, ICW_MAX_NS_TAPS>), dim3(blocks), dim3(64), 0, st, *a); break;
+    default:
+        if (a->rk.ns_n > 4) return hipErrorInvalidValue;   /* the IIR shapers are order 4 */
+        hipLaunchKernelGGL((icw_render_serial<2, 4>), dim3(blocks), dim3(64), 0, st, *a);
+        break;
     }
     return hipGetLastError();
 }
