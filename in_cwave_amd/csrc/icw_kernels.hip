@@ -998,12 +998,41 @@ __device__ __forceinline__ uint32_t icw_mt_twist_word(uint32_t u, uint32_t v)
 
 __device__ __forceinline__ void icw_mt_regen(uint32_t *mt, int lane)
 {
-    /* in-place generation of the next 624 words (mtrnd_gen_ui32, mt_jrnd.c:105-120) */
-    for (int i = 0; i < 227; ++i)
-        mt[i * 64 + lane] = mt[(i + 397) * 64 + lane] ^ icw_mt_twist_word(mt[i * 64 + lane], mt[(i + 1) * 64 + lane]);
-    for (int i = 227; i < 623; ++i)
-        mt[i * 64 + lane] = mt[(i - 227) * 64 + lane] ^ icw_mt_twist_word(mt[i * 64 + lane], mt[(i + 1) * 64 + lane]);
-    mt[623 * 64 + lane] = mt[396 * 64 + lane] ^ icw_mt_twist_word(mt[623 * 64 + lane], mt[lane]);
+    /* in-place generation of the next 624 words (mtrnd_gen_ui32, mt_jrnd.c:105-120), 8 words per
+     * batch: a batch's LDS reads are independent of its writes (they read words >= i and, in the
+     * second part, words written >= 220 positions earlier), so its loads issue back to back */
+    uint32_t *m = mt + lane;
+    int i = 0;
+    for (; i + 8 <= 227; i += 8) {
+        uint32_t u[9], f[8];
+#pragma unroll
+        for (int j = 0; j < 9; ++j) u[j] = m[(i + j) * 64];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) f[j] = m[(i + j + 397) * 64];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) m[(i + j) * 64] = f[j] ^ icw_mt_twist_word(u[j], u[j + 1]);
+    }
+    for (; i < 227; ++i) m[i * 64] = m[(i + 397) * 64] ^ icw_mt_twist_word(m[i * 64], m[(i + 1) * 64]);
+    for (; i + 8 <= 623; i += 8) {
+        uint32_t u[9], f[8];
+#pragma unroll
+        for (int j = 0; j < 9; ++j) u[j] = m[(i + j) * 64];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) f[j] = m[(i + j - 227) * 64];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) m[(i + j) * 64] = f[j] ^ icw_mt_twist_word(u[j], u[j + 1]);
+    }
+    for (; i < 623; ++i) m[i * 64] = m[(i - 227) * 64] ^ icw_mt_twist_word(m[i * 64], m[(i + 1) * 64]);
+    m[623 * 64] = m[396 * 64] ^ icw_mt_twist_word(m[623 * 64], m[0]);
+}
+
+__device__ __forceinline__ uint32_t icw_mt_temper(uint32_t y)
+{
+    y ^= (y >> 11);
+    y ^= (y << 7) & 0x9d2c5680u;
+    y ^= (y << 15) & 0xefc60000u;
+    y ^= (y >> 18);
+    return y;
 }
 
 __device__ __forceinline__ uint32_t icw_mt_u32(uint32_t *mt, int lane, int &idx)
@@ -1012,13 +1041,9 @@ __device__ __forceinline__ uint32_t icw_mt_u32(uint32_t *mt, int lane, int &idx)
         icw_mt_regen(mt, lane);
         idx = 0;
     }
-    uint32_t y = mt[idx * 64 + lane];
+    const uint32_t y = mt[idx * 64 + lane];
     ++idx;
-    y ^= (y >> 11);
-    y ^= (y << 7) & 0x9d2c5680u;
-    y ^= (y << 15) & 0xefc60000u;
-    y ^= (y >> 18);
-    return y;
+    return icw_mt_temper(y);
 }
 
 /* mtrnd_gen_dsopen (mt_jrnd.c:218-256): (-1, 1) with 53-bit resolution, +-1 rejected */
@@ -1039,9 +1064,76 @@ __device__ __forceinline__ double icw_mt_dsopen(uint32_t *mt, int lane, int &idx
  * (sound_render.c:711-756) for every sample of the block.  It depends only on the channel's MT19937
  * state and the sloped-TPDF memory, never on the audio, so it runs on its own stream ahead of /
  * beside the Hilbert and output kernels; one lane per render channel, MT words in LDS. */
+/* dsopen from two tempered words (mtrnd_gen_dsopen, mt_jrnd.c:218-256) without the rejection */
+__device__ __forceinline__ double icw_dsopen2(uint32_t ua, uint32_t ub)
+{
+    const uint32_t a = ua >> 5, b = ub >> 6;
+    return ((a * 67108864.0 + b) * (1.0 / 9007199254740992.0)) * 2.0 - 1.0;
+}
+
+template <int RT>
+struct IcwDith {
+    static constexpr int W = RT == ICW_RENDER_GAUSS ? 24 : (RT == ICW_RENDER_TPDF ? 4 : 2);   /* words/sample */
+    static constexpr int C = RT == ICW_RENDER_GAUSS ? 2 : (RT == ICW_RENDER_TPDF ? 8 : 16);  /* samples/chunk */
+};
+
+/* the dither of one sample from its words (no rejection among them) */
+template <int RT>
+__device__ __forceinline__ double icw_dith_from_words(const uint32_t *u, double &prev_rnd)
+{
+    double rnd, tr;
+    if (RT == ICW_RENDER_RPDF) {
+        rnd = icw_dsopen2(u[0], u[1]) / ICW_SQRT2;
+    } else if (RT == ICW_RENDER_TPDF) {
+        rnd = icw_dsopen2(u[0], u[1]);
+        rnd += icw_dsopen2(u[2], u[3]);
+        rnd /= 2.0;
+    } else if (RT == ICW_RENDER_STPDF) {
+        rnd = ((tr = icw_dsopen2(u[0], u[1])) - prev_rnd) / 2.0;
+        prev_rnd = tr;
+    } else {
+        rnd = icw_dsopen2(u[0], u[1]);
+#pragma unroll
+        for (int i = 1; i < 12; ++i) rnd += icw_dsopen2(u[2 * i], u[2 * i + 1]);
+        rnd /= (2.0 * ICW_SQRT6);
+    }
+    return rnd;
+}
+
+/* the reference's sequential form, rejection and twist included */
+template <int RT>
+__device__ __forceinline__ double icw_dith_slow(uint32_t *mt, int lane, int &idx, double &prev_rnd)
+{
+    double rnd, tr;
+    if (RT == ICW_RENDER_RPDF) {
+        rnd = icw_mt_dsopen(mt, lane, idx) / ICW_SQRT2;
+    } else if (RT == ICW_RENDER_TPDF) {
+        rnd = icw_mt_dsopen(mt, lane, idx);
+        rnd += icw_mt_dsopen(mt, lane, idx);
+        rnd /= 2.0;
+    } else if (RT == ICW_RENDER_STPDF) {
+        rnd = ((tr = icw_mt_dsopen(mt, lane, idx)) - prev_rnd) / 2.0;
+        prev_rnd = tr;
+    } else {
+        rnd = icw_mt_dsopen(mt, lane, idx);
+        for (int i = 1; i < 12; ++i) rnd += icw_mt_dsopen(mt, lane, idx);
+        rnd /= (2.0 * ICW_SQRT6);
+    }
+    return rnd;
+}
+
+/* Dither generation (K3a): the random term rnd * dth_mul of sound_render_value
+ * (sound_render.c:711-756) for every sample of the block.  It depends only on the channel's MT19937
+ * state and the sloped-TPDF memory, never on the audio, so it runs on its own stream beside the
+ * Hilbert and output kernels; one lane per render channel, MT words in LDS.  Fast path: a chunk of
+ * C samples whose W*C words are all left before the next twist is read as one batch of
+ * independent LDS loads; a chunk that would hit a rejected draw (probability ~2^-53 per draw) or
+ * the twist runs through the sequential form instead. */
 template <int RT>
 __global__ __launch_bounds__(64) void icw_dither_gen(IcwK3Args a)
 {
+    using D = IcwDith<RT>;
+    constexpr int NW = D::W * D::C;
     __shared__ uint32_t mt[624 * 64];
     const int lane = threadIdx.x;
     const int g0 = blockIdx.x * 64 + lane;
@@ -1053,23 +1145,33 @@ __global__ __launch_bounds__(64) void icw_dither_gen(IcwK3Args a)
     double prev_rnd = rs[0];
     const double dth_mul = a.rk.dth_mul;
     double *dd = a.dith + (size_t)g * a.dith_pitch;
-    for (int t = 0; t < a.T; ++t) {
-        double rnd, tr;
-        if (RT == ICW_RENDER_RPDF) {
-            rnd = icw_mt_dsopen(mt, lane, idx) / ICW_SQRT2;
-        } else if (RT == ICW_RENDER_TPDF) {
-            rnd = icw_mt_dsopen(mt, lane, idx);
-            rnd += icw_mt_dsopen(mt, lane, idx);
-            rnd /= 2.0;
-        } else if (RT == ICW_RENDER_STPDF) {
-            rnd = ((tr = icw_mt_dsopen(mt, lane, idx)) - prev_rnd) / 2.0;
-            prev_rnd = tr;
-        } else {
-            rnd = icw_mt_dsopen(mt, lane, idx);
-            for (int i = 1; i < 12; ++i) rnd += icw_mt_dsopen(mt, lane, idx);
-            rnd /= (2.0 * ICW_SQRT6);
+    const int T = a.T;
+    int t = 0;
+    while (t < T) {
+        if (t + D::C <= T && idx + NW <= 624) {
+            uint32_t u[NW];
+#pragma unroll
+            for (int j = 0; j < NW; ++j) u[j] = icw_mt_temper(mt[(idx + j) * 64 + lane]);
+            bool rej = false;
+#pragma unroll
+            for (int j = 0; j < NW; j += 2) rej |= ((u[j] >> 5) == 0u) && ((u[j + 1] >> 6) == 0u);
+            if (!rej) {
+                double pr = prev_rnd;
+#pragma unroll
+                for (int c = 0; c < D::C; ++c) {
+                    const double rnd = icw_dith_from_words<RT>(u + c * D::W, pr);
+                    if (valid) dd[t + c] = rnd * dth_mul;
+                }
+                prev_rnd = pr;
+                idx += NW;
+                t += D::C;
+                continue;
+            }
         }
+        /* one sample the sequential way (twists, rejections) */
+        const double rnd = icw_dith_slow<RT>(mt, lane, idx, prev_rnd);
         if (valid) dd[t] = rnd * dth_mul;
+        ++t;
     }
     if (!valid) return;
     for (int i = 0; i < 624; ++i) a.mt[(size_t)i * a.mt_pitch + g] = mt[i * 64 + lane];
