@@ -135,7 +135,7 @@ struct IcwK3Args {
     unsigned long long *peak_bits; /* [n_streams][2] */
     int32_t n_gen, mt_pitch;
     IcwRenderK rk;
-    double *dith;                  /* [n_gen][dith_pitch] rnd * dth_mul per sample (K3a -> K3b); null: ROUND */
+    double *dith;                  /* [T][dith_pitch] rnd * dth_mul per sample, time-major (K3a -> K3b); null: ROUND */
     size_t dith_pitch;
 };
 

@@ -854,7 +854,7 @@ int icw_process_streams(icw_ctx *c, int first, int count, const void *in, size_t
             if (dither) {
                 /* K3a for this block on its own stream: dith[p] was last read by K3b of block b-2 */
                 a3.dith = c->dith[p];
-                a3.dith_pitch = (size_t)Tb;
+                a3.dith_pitch = (size_t)count * 2;    /* time-major [T][count*2] */
                 if (b >= 2 && hipStreamWaitEvent(st3, c->k2done[p], 0) != hipSuccess) return ICW_EDEVICE;
                 if (icw_launch_dither(&a3, st3) != hipSuccess || hipEventRecord(c->ditdone[p], st3) != hipSuccess ||
                     hipStreamWaitEvent(st2, c->ditdone[p], 0) != hipSuccess)

@@ -1144,7 +1144,8 @@ __global__ __launch_bounds__(64) void icw_dither_gen(IcwK3Args a)
     double *rs = a.rs + (size_t)g * ICW_RSTATE;
     double prev_rnd = rs[0];
     const double dth_mul = a.rk.dth_mul;
-    double *dd = a.dith + (size_t)g * a.dith_pitch;
+    double *dd = a.dith + g;            /* time-major [t][dith_pitch]: one store per sample is coalesced */
+    const size_t dp = a.dith_pitch;
     const int T = a.T;
     int t = 0;
     while (t < T) {
@@ -1160,7 +1161,7 @@ __global__ __launch_bounds__(64) void icw_dither_gen(IcwK3Args a)
 #pragma unroll
                 for (int c = 0; c < D::C; ++c) {
                     const double rnd = icw_dith_from_words<RT>(u + c * D::W, pr);
-                    if (valid) dd[t + c] = rnd * dth_mul;
+                    if (valid) dd[(size_t)(t + c) * dp] = rnd * dth_mul;
                 }
                 prev_rnd = pr;
                 idx += NW;
@@ -1170,7 +1171,7 @@ __global__ __launch_bounds__(64) void icw_dither_gen(IcwK3Args a)
         }
         /* one sample the sequential way (twists, rejections) */
         const double rnd = icw_dith_slow<RT>(mt, lane, idx, prev_rnd);
-        if (valid) dd[t] = rnd * dth_mul;
+        if (valid) dd[(size_t)t * dp] = rnd * dth_mul;
         ++t;
     }
     if (!valid) return;
@@ -1230,19 +1231,31 @@ __device__ __forceinline__ int icw_render_step(double input, double d, double &p
 template <int KIND, int R, int J0>
 __device__ __forceinline__ void icw_render_block(const double (&xin)[ICW_MAX_NS_TAPS], const double (&dv)[ICW_MAX_NS_TAPS],
                                                  double &prev_err, double (&E)[R], double (&O)[R], const IcwRenderK &k,
-                                                 int nn, unsigned &clips, double &pk, unsigned char *o, int osz, int lim,
-                                                 bool valid)
+                                                 int nn, unsigned &clips, double &pk, int *vrow, int lim)
 {
     if constexpr (J0 < ICW_MAX_NS_TAPS) {
         if (J0 < lim) {
-            const int val = icw_render_step<KIND, R, J0>(xin[J0], dv[J0], prev_err, E, O, k, nn, clips, pk);
-            if (valid) {
-                unsigned char *q = o + (size_t)J0 * 2 * osz;
-                q[0] = (unsigned char)val;
-                q[1] = (unsigned char)(val >> 8);
-                if (osz == 3) q[2] = (unsigned char)(val >> 16);
-            }
-            icw_render_block<KIND, R, J0 + 1>(xin, dv, prev_err, E, O, k, nn, clips, pk, o, osz, lim, valid);
+            vrow[J0] = icw_render_step<KIND, R, J0>(xin[J0], dv[J0], prev_err, E, O, k, nn, clips, pk);
+            icw_render_block<KIND, R, J0 + 1>(xin, dv, prev_err, E, O, k, nn, clips, pk, vrow, lim);
+        }
+    }
+}
+
+/* Write frames [f0, f1) of a block: the lane pair (L = even lane, R = odd lane) of a stream owns
+ * the interleaved L,R frames; values come from the pair's LDS rows.  16-bit frames are one dword;
+ * 24-bit frames are three 16-bit words (2-byte aligned for every stride). */
+__device__ __forceinline__ void icw_put_frames(const int *vl, const int *vr, unsigned char *o, int osz, int f0, int f1)
+{
+    if (osz == 2) {
+        for (int f = f0; f < f1; ++f)
+            *(uint32_t *)(o + (size_t)f * 4) = ((uint32_t)vl[f] & 0xffffu) | ((uint32_t)vr[f] << 16);
+    } else {
+        for (int f = f0; f < f1; ++f) {
+            const uint32_t l = (uint32_t)vl[f], r = (uint32_t)vr[f];
+            uint16_t *q = (uint16_t *)(o + (size_t)f * 6);
+            q[0] = (uint16_t)(l & 0xffffu);
+            q[1] = (uint16_t)(((l >> 16) & 0xffu) | ((r & 0xffu) << 8));
+            q[2] = (uint16_t)((r >> 8) & 0xffffu);
         }
     }
 }
@@ -1256,6 +1269,7 @@ __global__ __launch_bounds__(64) void icw_render_serial(IcwK3Args a)
 {
     constexpr int NM = ICW_MAX_NS_TAPS;
     static_assert(NM % R == 0, "ring period must divide the unroll");
+    __shared__ int vals[64][NM + 1];    /* the block's rendered values, one row per lane */
     const int lane = threadIdx.x;
     const int g0 = blockIdx.x * 64 + lane;
     const bool valid = g0 < a.n_gen;
@@ -1271,8 +1285,12 @@ __global__ __launch_bounds__(64) void icw_render_serial(IcwK3Args a)
     const int nn = k.ns_n;
     const int osz = k.is24 ? 3 : 2;
     const double *pp = a.pre + (size_t)s * a.pre_stride + ch;
-    const double *dp = a.dith ? a.dith + (size_t)g * a.dith_pitch : nullptr;
-    unsigned char *op = a.out + (size_t)s * a.out_stride + (size_t)ch * osz;
+    const double *dp = a.dith ? a.dith + g : nullptr;         /* time-major [t][dith_pitch] */
+    const size_t dpitch = a.dith_pitch;
+    unsigned char *op = a.out + (size_t)s * a.out_stride;     /* the stream's frames */
+    int *vrow = vals[lane];
+    const int *vl = vals[lane & ~1], *vr = vals[lane | 1];
+    const int half = (lane & 1) * (NM / 2);
     unsigned clips = 0;
     double pk = 0.0;
     const int T = a.T;
@@ -1282,20 +1300,24 @@ __global__ __launch_bounds__(64) void icw_render_serial(IcwK3Args a)
 #pragma unroll
         for (int j = 0; j < NM; ++j) {
             xin[j] = pp[(size_t)(t + j) * 2];
-            dv[j] = dp ? dp[t + j] : 0.0;   /* ROUND: rnd * dth_mul == 0.0 * dth_mul */
+            dv[j] = dp ? dp[(size_t)(t + j) * dpitch] : 0.0;   /* ROUND: rnd * dth_mul == 0.0 * dth_mul */
         }
-        icw_render_block<KIND, R, 0>(xin, dv, prev_err, E, O, k, nn, clips, pk, op + (size_t)t * 2 * osz, osz, NM,
-                                     valid);
+        icw_render_block<KIND, R, 0>(xin, dv, prev_err, E, O, k, nn, clips, pk, vrow, NM);
+        __builtin_amdgcn_wave_barrier();
+        if (valid) icw_put_frames(vl, vr, op + (size_t)t * 2 * osz, osz, half, half + NM / 2);
+        __builtin_amdgcn_wave_barrier();
     }
     const int rem = T - t;
     if (rem > 0) {
 #pragma unroll
         for (int j = 0; j < NM; ++j) {
             xin[j] = j < rem ? pp[(size_t)(t + j) * 2] : 0.0;
-            dv[j] = (j < rem && dp) ? dp[t + j] : 0.0;
+            dv[j] = (j < rem && dp) ? dp[(size_t)(t + j) * dpitch] : 0.0;
         }
-        icw_render_block<KIND, R, 0>(xin, dv, prev_err, E, O, k, nn, clips, pk, op + (size_t)t * 2 * osz, osz, rem,
-                                     valid);
+        icw_render_block<KIND, R, 0>(xin, dv, prev_err, E, O, k, nn, clips, pk, vrow, rem);
+        __builtin_amdgcn_wave_barrier();
+        const int h = (rem + 1) / 2;
+        if (valid) icw_put_frames(vl, vr, op + (size_t)t * 2 * osz, osz, (lane & 1) ? h : 0, (lane & 1) ? rem : h);
         /* back to the block-start mapping: rotate left by rem mod R */
 #pragma unroll
         for (int r = 1; r < NM; ++r)

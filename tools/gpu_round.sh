@@ -34,6 +34,11 @@ for s in "$@"; do
       ( cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/gpurun_out/prof" -o run \
           -- python3 "$R/bench.py" --steps 3 --warmup 1 --no-cpu-baseline ) > gpurun_out/prof.txt 2>&1
       rc=$?; echo "[prof] rc=$rc" | tee -a gpurun_out/steps.txt; [ $rc -eq 0 ] || exit 2 ;;
+    profw)   # kernel stats of one workload: WL=c5 bash tools/gpu_round.sh profw
+      R=$(pwd); export TMPDIR=/tmp
+      ( cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/gpurun_out/prof_$WL" -o run \
+          -- python3 "$R/bench.py" --workload "$WL" --steps 2 --warmup 1 --no-cpu-baseline ) > gpurun_out/prof_$WL.txt 2>&1
+      rc=$?; echo "[prof_$WL] rc=$rc" | tee -a gpurun_out/steps.txt; [ $rc -eq 0 ] || exit 2 ;;
     pmc)
       R=$(pwd); export TMPDIR=/tmp
       ( cd /tmp && timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$R/gpurun_out/pmc_fetch" -o run \
