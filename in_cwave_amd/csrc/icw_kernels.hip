@@ -1193,11 +1193,12 @@ __device__ __forceinline__ void icw_ring_rotate1(double (&X)[R])
     X[R - 1] = r0;
 }
 
-/* One sample of sound_render_value after the dither term (sound_render.c:754-809). */
-template <int KIND, int R, int J>
+/* One sample of sound_render_value after the dither term (sound_render.c:754-809).  NN is the
+ * shaper's tap count (a template parameter: a runtime count would predicate all 20 taps). */
+template <int KIND, int R, int NN, int J>
 __device__ __forceinline__ int icw_render_step(double input, double d, double &prev_err, double (&E)[R],
-                                               double (&O)[R], const IcwRenderK &k, int nn, unsigned &clips,
-                                               double &pk)
+                                               double (&O)[R], const IcwRenderK &k, const double (&cf)[2 * NN + 1],
+                                               unsigned &clips, double &pk)
 {
     input = (input * k.norm_mul) - prev_err;
     double q = input + d;
@@ -1215,29 +1216,47 @@ __device__ __forceinline__ int icw_render_step(double input, double d, double &p
     if (KIND == 1) {
         E[J % R] = ev;
 #pragma unroll
-        for (int i = 0; i < R; ++i)
-            if (i < nn) res += k.ns_c[i] * E[(J - i + 2 * R) % R];
+        for (int i = 0; i < NN; ++i) res += cf[i] * E[(J - i + 2 * R) % R];
     } else if (KIND == 2) {
         E[J % R] = ev;
 #pragma unroll
-        for (int i = 0; i < R; ++i)
-            if (i < nn) res += k.ns_c[i] * E[(J - i + 2 * R) % R] - k.ns_c[i + nn] * O[(J - 1 - i + 2 * R) % R];
+        for (int i = 0; i < NN; ++i) res += cf[i] * E[(J - i + 2 * R) % R] - cf[i + NN] * O[(J - 1 - i + 2 * R) % R];
         O[J % R] = res;
     }
     prev_err = res;
     return val << k.norm_shift;
 }
 
-template <int KIND, int R, int J0>
+template <int KIND, int R, int NN, int J0>
 __device__ __forceinline__ void icw_render_block(const double (&xin)[ICW_MAX_NS_TAPS], const double (&dv)[ICW_MAX_NS_TAPS],
                                                  double &prev_err, double (&E)[R], double (&O)[R], const IcwRenderK &k,
-                                                 int nn, unsigned &clips, double &pk, int *vrow, int lim)
+                                                 const double (&cf)[2 * NN + 1], unsigned &clips, double &pk, int *vrow,
+                                                 int lim)
 {
     if constexpr (J0 < ICW_MAX_NS_TAPS) {
         if (J0 < lim) {
-            vrow[J0] = icw_render_step<KIND, R, J0>(xin[J0], dv[J0], prev_err, E, O, k, nn, clips, pk);
-            icw_render_block<KIND, R, J0 + 1>(xin, dv, prev_err, E, O, k, nn, clips, pk, vrow, lim);
+            vrow[J0] = icw_render_step<KIND, R, NN, J0>(xin[J0], dv[J0], prev_err, E, O, k, cf, clips, pk);
+            icw_render_block<KIND, R, NN, J0 + 1>(xin, dv, prev_err, E, O, k, cf, clips, pk, vrow, lim);
         }
+    }
+}
+
+/* a full block whose step J refills xin[J] / dv[J] with the next block's sample right after
+ * consuming it, so the loads run a block ahead of use (clamped indices stay in bounds) */
+template <int KIND, int R, int NN, int J0>
+__device__ __forceinline__ void icw_render_block_pf(double (&xin)[ICW_MAX_NS_TAPS], double (&dv)[ICW_MAX_NS_TAPS],
+                                                    double &prev_err, double (&E)[R], double (&O)[R],
+                                                    const IcwRenderK &k, const double (&cf)[2 * NN + 1],
+                                                    unsigned &clips, double &pk, int *vrow, const double *pp,
+                                                    const double *dp, size_t dpitch, int tn, int tmax)
+{
+    if constexpr (J0 < ICW_MAX_NS_TAPS) {
+        vrow[J0] = icw_render_step<KIND, R, NN, J0>(xin[J0], dv[J0], prev_err, E, O, k, cf, clips, pk);
+        const int tj = min(tn + J0, tmax);
+        xin[J0] = pp[(size_t)tj * 2];
+        dv[J0] = dp ? dp[(size_t)tj * dpitch] : 0.0;
+        icw_render_block_pf<KIND, R, NN, J0 + 1>(xin, dv, prev_err, E, O, k, cf, clips, pk, vrow, pp, dp, dpitch, tn,
+                                                 tmax);
     }
 }
 
@@ -1264,7 +1283,7 @@ __device__ __forceinline__ void icw_put_frames(const int *vl, const int *vr, uns
  * clips, peak, noise shaper -- with the dither term from K3a.  One lane per channel, samples in
  * blocks of ICW_MAX_NS_TAPS (a multiple of the ring period): the block's inputs are loaded
  * before use.  rs keeps the shaper history by age (0 = newest), 20 + 20 slots. */
-template <int KIND, int R>
+template <int KIND, int R, int NN>
 __global__ __launch_bounds__(64) void icw_render_serial(IcwK3Args a)
 {
     constexpr int NM = ICW_MAX_NS_TAPS;
@@ -1282,7 +1301,10 @@ __global__ __launch_bounds__(64) void icw_render_serial(IcwK3Args a)
 #pragma unroll
     for (int i = 0; i < R; ++i) { E[(R - 1 - i) % R] = rs[2 + i]; O[(R - 1 - i) % R] = rs[2 + NM + i]; }
     const IcwRenderK &k = a.rk;
-    const int nn = k.ns_n;
+    double cf[2 * NN + 1];                                    /* shaper coefficients in registers */
+#pragma unroll
+    for (int i = 0; i < 2 * NN; ++i) cf[i] = k.ns_c[i];
+    cf[2 * NN] = 0.0;
     const int osz = k.is24 ? 3 : 2;
     const double *pp = a.pre + (size_t)s * a.pre_stride + ch;
     const double *dp = a.dith ? a.dith + g : nullptr;         /* time-major [t][dith_pitch] */
@@ -1296,13 +1318,16 @@ __global__ __launch_bounds__(64) void icw_render_serial(IcwK3Args a)
     const int T = a.T;
     int t = 0;
     double xin[NM], dv[NM];
-    for (; t + NM <= T; t += NM) {
+    if (T >= NM) {
 #pragma unroll
         for (int j = 0; j < NM; ++j) {
-            xin[j] = pp[(size_t)(t + j) * 2];
-            dv[j] = dp ? dp[(size_t)(t + j) * dpitch] : 0.0;   /* ROUND: rnd * dth_mul == 0.0 * dth_mul */
+            xin[j] = pp[(size_t)j * 2];
+            dv[j] = dp ? dp[(size_t)j * dpitch] : 0.0;         /* ROUND: rnd * dth_mul == 0.0 * dth_mul */
         }
-        icw_render_block<KIND, R, 0>(xin, dv, prev_err, E, O, k, nn, clips, pk, vrow, NM);
+    }
+    for (; t + NM <= T; t += NM) {
+        icw_render_block_pf<KIND, R, NN, 0>(xin, dv, prev_err, E, O, k, cf, clips, pk, vrow, pp, dp, dpitch, t + NM,
+                                            T - 1);
         __builtin_amdgcn_wave_barrier();
         if (valid) icw_put_frames(vl, vr, op + (size_t)t * 2 * osz, osz, half, half + NM / 2);
         __builtin_amdgcn_wave_barrier();
@@ -1314,7 +1339,7 @@ __global__ __launch_bounds__(64) void icw_render_serial(IcwK3Args a)
             xin[j] = j < rem ? pp[(size_t)(t + j) * 2] : 0.0;
             dv[j] = (j < rem && dp) ? dp[(size_t)(t + j) * dpitch] : 0.0;
         }
-        icw_render_block<KIND, R, 0>(xin, dv, prev_err, E, O, k, nn, clips, pk, vrow, rem);
+        icw_render_block<KIND, R, NN, 0>(xin, dv, prev_err, E, O, k, cf, clips, pk, vrow, rem);
         __builtin_amdgcn_wave_barrier();
         const int h = (rem + 1) / 2;
         if (valid) icw_put_frames(vl, vr, op + (size_t)t * 2 * osz, osz, (lane & 1) ? h : 0, (lane & 1) ? rem : h);
@@ -1416,13 +1441,22 @@ extern "C" hipError_t icw_launch_dither(const IcwK3Args *a, hipStream_t st)
 extern "C" hipError_t icw_launch_render(const IcwK3Args *a, hipStream_t st)
 {
     const int blocks = (a->n_gen + 63) / 64;
-    switch (a->rk.ns_kind) {
-    case 0: hipLaunchKernelGGL((icw_render_serial<0, 1>), dim3(blocks), dim3(64), 0, st, *a); break;
-    case 1: hipLaunchKernelGGL((icw_render_serial<1, ICW_MAX_NS_TAPS>), dim3(blocks), dim3(64), 0, st, *a); break;
-    default:
-        if (a->rk.ns_n > 4) return hipErrorInvalidValue;   /* the IIR shapers are order 4 */
-        hipLaunchKernelGGL((icw_render_serial<2, 4>), dim3(blocks), dim3(64), 0, st, *a);
-        break;
+    /* the tap counts of the canned shapers (sound_render.c:75-235): FIR 5, 9, 15, 16, 20; IIR 4 */
+    const int nn = a->rk.ns_n;
+    if (a->rk.ns_kind == 0) {
+        hipLaunchKernelGGL((icw_render_serial<0, 1, 0>), dim3(blocks), dim3(64), 0, st, *a);
+    } else if (a->rk.ns_kind == 1) {
+        switch (nn) {
+        case 5: hipLaunchKernelGGL((icw_render_serial<1, ICW_MAX_NS_TAPS, 5>), dim3(blocks), dim3(64), 0, st, *a); break;
+        case 9: hipLaunchKernelGGL((icw_render_serial<1, ICW_MAX_NS_TAPS, 9>), dim3(blocks), dim3(64), 0, st, *a); break;
+        case 15: hipLaunchKernelGGL((icw_render_serial<1, ICW_MAX_NS_TAPS, 15>), dim3(blocks), dim3(64), 0, st, *a); break;
+        case 16: hipLaunchKernelGGL((icw_render_serial<1, ICW_MAX_NS_TAPS, 16>), dim3(blocks), dim3(64), 0, st, *a); break;
+        case 20: hipLaunchKernelGGL((icw_render_serial<1, ICW_MAX_NS_TAPS, 20>), dim3(blocks), dim3(64), 0, st, *a); break;
+        default: return hipErrorInvalidValue;
+        }
+    } else {
+        if (nn != 4) return hipErrorInvalidValue;
+        hipLaunchKernelGGL((icw_render_serial<2, 4, 4>), dim3(blocks), dim3(64), 0, st, *a);
     }
     return hipGetLastError();
 }
