@@ -88,6 +88,16 @@ class FileConfig(C.Structure):
                 ("nodes", Node * CFG_MAX_NODES), ("names", (C.c_char * DSP_NAME_SIZE) * CFG_MAX_NODES)]
 
 HTYPE_WFONLY, HTYPE_PCMW, HTYPE_EXT, HTYPE_CWAVE = 0, 1, 2, 3
+RSTATE = 42
+
+
+class StateBlob(C.Structure):
+    """the per-stream state blob of icw_get_state / icw_set_state"""
+    _fields_ = [("magic", C.c_uint64), ("n_frame", C.c_uint64), ("pos", C.c_int64), ("n_samples", C.c_int64),
+                ("n_fade_in", C.c_int64), ("n_fade_out", C.c_int64), ("hq_phase", C.c_uint32 * 2),
+                ("nord", C.c_uint32), ("has_render", C.c_uint32), ("hist", (C.c_double * 20) * 4),
+                ("sncnt", C.c_uint64 * 4), ("bus", (C.c_double * 4) * N_INPUTS),
+                ("mt", (C.c_uint32 * 624) * 2), ("mt_idx", C.c_int32 * 2), ("rs", (C.c_double * RSTATE) * 2)]
 
 
 class WavInfo(C.Structure):

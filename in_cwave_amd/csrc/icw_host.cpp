@@ -27,6 +27,7 @@ extern "C" hipError_t icw_launch_iir_pair(const IcwK1Args *a, int nord, int kaha
 extern "C" hipError_t icw_launch_iir_state(const IcwK1Args *a, int nord, int kahan, int subn, hipStream_t st);
 extern "C" hipError_t icw_launch_render(const IcwK3Args *a, hipStream_t st);
 extern "C" hipError_t icw_launch_dither(const IcwK3Args *a, hipStream_t st);
+extern "C" hipError_t icw_launch_dither_lane(const IcwK3Args *a, hipStream_t st);
 extern "C" hipError_t icw_launch_output(const IcwK2Args *a, int nord, int kahan, hipStream_t st);
 extern "C" hipError_t icw_launch_graph_serial(const IcwK4Args *a, hipStream_t st);
 extern "C" hipError_t icw_launch_advance(const IcwAdvArgs *a, hipStream_t st);
@@ -107,6 +108,7 @@ struct icw_ctx {
     std::vector<hipEvent_t> ev;
     int n_cu = 256;
     bool pair_mode = false;   /* chain+helper wave pairs (few chains per SIMD) vs plain lanes */
+    bool dither_lane = false; /* ICW_DITHER=lane: lane-per-channel dither generator (A/B only) */
     double last_ms[2]{};
     int last_launches[2]{};
     std::mutex mu;
@@ -497,6 +499,8 @@ int icw_create(const icw_config *cfg, const icw_node *nodes, int n_nodes, int n_
         const char *m = getenv("ICW_K1_MODE");
         if (m && !strcmp(m, "plain")) c->pair_mode = false;
         if (m && !strcmp(m, "pair")) c->pair_mode = true;
+        const char *d = getenv("ICW_DITHER");
+        c->dither_lane = d && !strcmp(d, "lane");
     }
     rc = icw_stream_init(c, 0, n_streams);
     if (rc) { free_all(c); delete c; return rc; }
@@ -856,7 +860,8 @@ int icw_process_streams(icw_ctx *c, int first, int count, const void *in, size_t
                 a3.dith = c->dith[p];
                 a3.dith_pitch = (size_t)count * 2;    /* time-major [T][count*2] */
                 if (b >= 2 && hipStreamWaitEvent(st3, c->k2done[p], 0) != hipSuccess) return ICW_EDEVICE;
-                if (icw_launch_dither(&a3, st3) != hipSuccess || hipEventRecord(c->ditdone[p], st3) != hipSuccess ||
+                const hipError_t ed = c->dither_lane ? icw_launch_dither_lane(&a3, st3) : icw_launch_dither(&a3, st3);
+                if (ed != hipSuccess || hipEventRecord(c->ditdone[p], st3) != hipSuccess ||
                     hipStreamWaitEvent(st2, c->ditdone[p], 0) != hipSuccess)
                     return ICW_EDEVICE;
             }
@@ -959,11 +964,17 @@ int icw_n_frame(icw_ctx *c, int s, uint64_t *nf)
 struct IcwBlob {
     uint64_t magic, n_frame;
     int64_t pos, n_samples, n_fade_in, n_fade_out;
-    uint32_t hq_phase[2], nord, pad;
+    uint32_t hq_phase[2], nord, has_render;
     double hist[4][ICW_HIST_PITCH];
     uint64_t sncnt[4];
     double bus[ICW_N_INPUTS][4];
+    /* serial render state per channel (dithered / noise-shaped renders only, else zero):
+     * MT19937 words and next index (624: twist due), prev_rnd, prev_ns_err, shaper history by age */
+    uint32_t mt[2][624];
+    int32_t mt_idx[2];
+    double rs[2][ICW_RSTATE];
 };
+constexpr uint64_t kBlobMagic = 0x32574349ull;   /* "ICW2" */
 
 size_t icw_state_size(const icw_ctx *c) { return c ? sizeof(IcwBlob) : 0; }
 
@@ -974,8 +985,9 @@ int icw_get_state(icw_ctx *c, int s, void *blob, size_t size)
     if (set_dev(c)) return ICW_EDEVICE;
     IcwBlob b;
     memset(&b, 0, sizeof(b));
-    b.magic = 0x31574349ull;
+    b.magic = kBlobMagic;
     b.nord = (uint32_t)c->nord;
+    b.has_render = c->serial_render ? 1u : 0u;
     long long fd[3];
     bool ok = hipStreamSynchronize(c->stream) == hipSuccess;
     ok &= hipMemcpy(&b.n_frame, c->st.n_frame + s, 8, hipMemcpyDeviceToHost) == hipSuccess;
@@ -985,6 +997,13 @@ int icw_get_state(icw_ctx *c, int s, void *blob, size_t size)
     ok &= hipMemcpy(b.hist, c->st.hist + (size_t)s * 4 * ICW_HIST_PITCH, sizeof(b.hist), hipMemcpyDeviceToHost) == hipSuccess;
     ok &= hipMemcpy(b.sncnt, c->st.sncnt + (size_t)s * 4, sizeof(b.sncnt), hipMemcpyDeviceToHost) == hipSuccess;
     ok &= hipMemcpy(b.bus, c->st.bus + (size_t)s * ICW_N_INPUTS * 4, sizeof(b.bus), hipMemcpyDeviceToHost) == hipSuccess;
+    if (c->serial_render) {
+        const size_t G = (size_t)c->n_streams * 2;
+        for (int ch = 0; ch < 2; ++ch)
+            ok &= hipMemcpy2D(b.mt[ch], 4, c->st.mt + (size_t)s * 2 + ch, G * 4, 4, 624, hipMemcpyDeviceToHost) == hipSuccess;
+        ok &= hipMemcpy(b.mt_idx, c->st.mt_idx + (size_t)s * 2, sizeof(b.mt_idx), hipMemcpyDeviceToHost) == hipSuccess;
+        ok &= hipMemcpy(b.rs, c->st.rs + (size_t)s * 2 * ICW_RSTATE, sizeof(b.rs), hipMemcpyDeviceToHost) == hipSuccess;
+    }
     b.n_samples = fd[0]; b.n_fade_in = fd[1]; b.n_fade_out = fd[2];
     if (!ok) return ICW_EDEVICE;
     memcpy(blob, &b, sizeof(b));
@@ -996,7 +1015,8 @@ int icw_set_state(icw_ctx *c, int s, const void *blob, size_t size)
     if (!c || !blob || size < sizeof(IcwBlob) || s < 0 || s >= c->n_streams) return ICW_EINVAL;
     IcwBlob b;
     memcpy(&b, blob, sizeof(b));
-    if (b.magic != 0x31574349ull || b.nord != (uint32_t)c->nord) return ICW_EINVAL;
+    if (b.magic != kBlobMagic || b.nord != (uint32_t)c->nord || b.has_render != (c->serial_render ? 1u : 0u))
+        return ICW_EINVAL;
     std::lock_guard<std::mutex> lk(c->mu);
     if (set_dev(c)) return ICW_EDEVICE;
     long long fd[3] = {b.n_samples, b.n_fade_in, b.n_fade_out};
@@ -1008,6 +1028,13 @@ int icw_set_state(icw_ctx *c, int s, const void *blob, size_t size)
     ok &= hipMemcpy(c->st.hist + (size_t)s * 4 * ICW_HIST_PITCH, b.hist, sizeof(b.hist), hipMemcpyHostToDevice) == hipSuccess;
     ok &= hipMemcpy(c->st.sncnt + (size_t)s * 4, b.sncnt, sizeof(b.sncnt), hipMemcpyHostToDevice) == hipSuccess;
     ok &= hipMemcpy(c->st.bus + (size_t)s * ICW_N_INPUTS * 4, b.bus, sizeof(b.bus), hipMemcpyHostToDevice) == hipSuccess;
+    if (c->serial_render) {
+        const size_t G = (size_t)c->n_streams * 2;
+        for (int ch = 0; ch < 2; ++ch)
+            ok &= hipMemcpy2D(c->st.mt + (size_t)s * 2 + ch, G * 4, b.mt[ch], 4, 4, 624, hipMemcpyHostToDevice) == hipSuccess;
+        ok &= hipMemcpy(c->st.mt_idx + (size_t)s * 2, b.mt_idx, sizeof(b.mt_idx), hipMemcpyHostToDevice) == hipSuccess;
+        ok &= hipMemcpy(c->st.rs + (size_t)s * 2 * ICW_RSTATE, b.rs, sizeof(b.rs), hipMemcpyHostToDevice) == hipSuccess;
+    }
     return ok ? ICW_OK : ICW_EDEVICE;
 }
 

@@ -1180,6 +1180,158 @@ __global__ __launch_bounds__(64) void icw_dither_gen(IcwK3Args a)
     rs[0] = prev_rnd;
 }
 
+/* Cooperative dither generation (K3a): one wave per render channel.  The random term of
+ * sound_render_value (sound_render.c:711-756) depends only on the channel's MT19937 stream, so the
+ * stream is produced 624 words at a time by the whole wave:
+ *   twist     the 624-word regeneration (mt_jrnd.c:105-120) in three dependency phases
+ *             ([0,227) from old words; [227,454) and [454,623) from words new by then; then 623);
+ *   window    words idx..623 tempered in parallel; word pairs -> dsopen values (mt_jrnd.c:218-256);
+ *             a rejected pair (+-1.0) yields no value -- the reference just draws the next pair --
+ *             so accepted values are compacted with a ballot prefix count;
+ *   samples   V consecutive values per sample (RPDF 1, TPDF 2, STPDF 1 + the previous, GAUSS 12),
+ *             one lane per sample.
+ * A pair or a sample may straddle windows (one carried word, < V carried values).  The block ends
+ * exactly after its last sample, so idx is where the reference's would be. */
+__device__ __forceinline__ void icw_coop_twist(uint32_t *mt, int lane)
+{
+    uint32_t r[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const int i = lane + 64 * q;
+        if (i < 227) r[q] = mt[i + 397] ^ icw_mt_twist_word(mt[i], mt[i + 1]);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const int i = lane + 64 * q;
+        if (i < 227) mt[i] = r[q];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const int i = 227 + lane + 64 * q;
+        if (i < 454) r[q] = mt[i - 227] ^ icw_mt_twist_word(mt[i], mt[i + 1]);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const int i = 227 + lane + 64 * q;
+        if (i < 454) mt[i] = r[q];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+        const int i = 454 + lane + 64 * q;
+        if (i < 623) r[q] = mt[i - 227] ^ icw_mt_twist_word(mt[i], mt[i + 1]);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+        const int i = 454 + lane + 64 * q;
+        if (i < 623) mt[i] = r[q];
+    }
+    __syncthreads();
+    if (lane == 0) mt[623] = mt[396] ^ icw_mt_twist_word(mt[623], mt[0]);
+    __syncthreads();
+}
+
+template <int RT>
+__global__ __launch_bounds__(64) void icw_dither_coop(IcwK3Args a)
+{
+    constexpr int V = RT == ICW_RENDER_GAUSS ? 12 : (RT == ICW_RENDER_TPDF ? 2 : 1);
+    __shared__ uint32_t mt[624];
+    __shared__ uint32_t tw[626];           /* the window's word list: [carried word] + tempered mt[idx..623] */
+    __shared__ double vals[313 + 16];      /* [carried values] + the window's accepted values */
+    __shared__ short pidx[313];            /* pair index of each accepted value of the window */
+    const int lane = threadIdx.x;
+    const int g = blockIdx.x;              /* one wave per generator: everything below is wave-uniform */
+    for (int i = lane; i < 624; i += 64) mt[i] = a.mt[(size_t)i * a.mt_pitch + g];
+    int idx = a.mt_idx[g];
+    double *rs = a.rs + (size_t)g * ICW_RSTATE;
+    double prev_rnd = rs[0];
+    const double dth_mul = a.rk.dth_mul;
+    double *dd = a.dith + g;
+    const size_t dp = a.dith_pitch;
+    const int T = a.T;
+    int t = 0, k = 0, c = 0;               /* samples done, carried values, carried word (0/1) */
+    uint32_t cword = 0;
+    __syncthreads();
+    while (t < T) {
+        if (idx >= 624) {
+            icw_coop_twist(mt, lane);
+            idx = 0;
+        }
+        const int nw = 624 - idx, nl = nw + c, np = nl >> 1;
+        for (int j = lane; j < nw; j += 64) tw[c + j] = icw_mt_temper(mt[idx + j]);
+        if (lane == 0 && c) tw[0] = cword;
+        __syncthreads();
+        int nacc = 0;
+        for (int p0 = 0; p0 < np; p0 += 64) {
+            const int pp = p0 + lane;
+            bool acc = false;
+            double d = 0.0;
+            if (pp < np) {
+                const uint32_t ua = tw[2 * pp] >> 5, ub = tw[2 * pp + 1] >> 6;
+                acc = !(ua == 0u && ub == 0u);                  /* dsopen rejects exactly -1.0 */
+                d = ((ua * 67108864.0 + ub) * (1.0 / 9007199254740992.0)) * 2.0 - 1.0;
+            }
+            const unsigned long long m = __ballot(acc);
+            const int pos = nacc + __popcll(m & ((1ull << lane) - 1ull));
+            if (acc) { vals[k + pos] = d; pidx[pos] = (short)pp; }
+            nacc += __popcll(m);
+        }
+        __syncthreads();
+        const int nv = k + nacc;
+        const int ns = min(nv / V, T - t);
+        for (int sm = lane; sm < ns; sm += 64) {
+            const double *v = vals + sm * V;
+            double rnd;
+            if (RT == ICW_RENDER_RPDF) {
+                rnd = v[0] / ICW_SQRT2;
+            } else if (RT == ICW_RENDER_TPDF) {
+                rnd = v[0];
+                rnd += v[1];
+                rnd /= 2.0;
+            } else if (RT == ICW_RENDER_STPDF) {
+                rnd = (v[0] - (sm == 0 ? prev_rnd : v[-1])) / 2.0;
+            } else {
+                rnd = v[0];
+#pragma unroll
+                for (int i = 1; i < 12; ++i) rnd += v[i];
+                rnd /= (2.0 * ICW_SQRT6);
+            }
+            dd[(size_t)(t + sm) * dp] = rnd * dth_mul;
+        }
+        if (RT == ICW_RENDER_STPDF && ns > 0) prev_rnd = vals[ns - 1];
+        t += ns;
+        if (t >= T) {
+            /* the block ends inside this window: consume exactly through its last value's pair */
+            const int need = ns * V - k;                        /* >= 1: carried values are < V */
+            const int plast = pidx[need - 1];
+            idx += 2 * (plast + 1) - c;
+            c = 0;
+        } else {
+            /* everything consumed; carry the partial sample's values and an odd last word */
+            const int kn = nv - ns * V;
+            __syncthreads();
+            double cv = 0.0;
+            if (lane < kn) cv = vals[ns * V + lane];
+            __syncthreads();
+            if (lane < kn) vals[lane] = cv;
+            k = kn;
+            if (nl & 1) { cword = tw[nl - 1]; c = 1; }
+            else c = 0;
+            idx = 624;
+        }
+        __syncthreads();
+    }
+    for (int i = lane; i < 624; i += 64) a.mt[(size_t)i * a.mt_pitch + g] = mt[i];
+    if (lane == 0) {
+        a.mt_idx[g] = idx;
+        rs[0] = prev_rnd;
+    }
+}
+
 /* Shaper history as a ring of R values (R = ICW_MAX_NS_TAPS for the FIR shapers, 4 for the
  * order-4 IIR shapers; R divides the unroll length ICW_MAX_NS_TAPS): at unrolled step J the newest
  * value goes to slot J mod R, so age i lives in slot (J - i) mod R -- compile-time indices, no
@@ -1426,6 +1578,20 @@ static hipError_t launch_k2_t(const IcwK2Args &a, hipStream_t st)
 }
 
 extern "C" hipError_t icw_launch_dither(const IcwK3Args *a, hipStream_t st)
+{
+    const int blocks = a->n_gen;           /* one wave per render channel */
+    switch (a->rk.render_type) {
+    case ICW_RENDER_RPDF: hipLaunchKernelGGL(icw_dither_coop<ICW_RENDER_RPDF>, dim3(blocks), dim3(64), 0, st, *a); break;
+    case ICW_RENDER_TPDF: hipLaunchKernelGGL(icw_dither_coop<ICW_RENDER_TPDF>, dim3(blocks), dim3(64), 0, st, *a); break;
+    case ICW_RENDER_STPDF: hipLaunchKernelGGL(icw_dither_coop<ICW_RENDER_STPDF>, dim3(blocks), dim3(64), 0, st, *a); break;
+    case ICW_RENDER_GAUSS: hipLaunchKernelGGL(icw_dither_coop<ICW_RENDER_GAUSS>, dim3(blocks), dim3(64), 0, st, *a); break;
+    default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+/* the lane-per-channel generator, kept for A/B timing (ICW_DITHER=lane) */
+extern "C" hipError_t icw_launch_dither_lane(const IcwK3Args *a, hipStream_t st)
 {
     const int blocks = (a->n_gen + 63) / 64;
     switch (a->rk.render_type) {

@@ -468,6 +468,16 @@ orc_stream *orc_stream_new(const icw_config *cfg, const icw_node *nodes, int n_n
 
 void orc_stream_free(orc_stream *s) { free(s); }
 
+/* raw MT19937 state of render channel ch (test hook): 624 words and the index of the next word
+ * (624: the next draw twists first), the device's representation */
+void orc_set_mt(orc_stream *s, int ch, const uint32_t *words, int idx)
+{
+    orc_mt *m = &s->rd[ch].mt;
+    memcpy(m->st, words, sizeof(m->st));
+    m->next = idx >= MT_N ? 0 : idx;
+    m->left = idx >= MT_N ? 1 : MT_N + 1 - idx;
+}
+
 /* a new track's sample format (mod_context_fopen -> xwave_reader_create, in_cwave.c:207-236) */
 void orc_set_input(orc_stream *s, uint32_t sample_rate, uint32_t fmt, uint32_t channels)
 {

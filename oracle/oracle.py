@@ -34,6 +34,7 @@ def load():
         lib.orc_stream_new.argtypes = [C.POINTER(abi.Config), C.POINTER(abi.Node), C.c_int, C.POINTER(C.c_int)]
         lib.orc_stream_free.argtypes = [vp]
         lib.orc_set_input.argtypes = [vp, C.c_uint32, C.c_uint32, C.c_uint32]
+        lib.orc_set_mt.argtypes = [vp, C.c_int, vp, C.c_int]
         lib.orc_stream_open.restype = C.c_int64
         lib.orc_stream_open.argtypes = [vp, C.c_int64, C.c_uint32, C.c_uint32, C.c_uint32, C.c_int, C.c_int]
         lib.orc_process.restype = C.c_int
@@ -85,6 +86,10 @@ class Stream:
             load().orc_stream_free(self.h)
         except Exception:
             pass
+
+    def set_mt(self, ch, words, idx):
+        w = np.ascontiguousarray(words, dtype=np.uint32)
+        load().orc_set_mt(self.h, ch, w.ctypes.data, idx)
 
     def set_input(self, sample_rate, fmt, channels):
         load().orc_set_input(self.h, sample_rate, fmt, channels)

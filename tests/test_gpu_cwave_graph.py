@@ -108,3 +108,43 @@ def test_bus_form_more_streams_than_a_wave(oracle, icw):
     raw = synth.batch_pcm(70, 700, 44100)
     _, out, pre, ro, rp = run_both(oracle, icw, cfg, graph.graph_leaky_feedback(), raw, 700)
     assert_parity(out, pre, ro, rp, 2, exact_pre=True)
+
+
+# ------------------------------------------------------- dither rejections, state round trip ----
+@pytest.mark.parametrize("rtype", [abi.RENDER_TPDF, abi.RENDER_STPDF, abi.RENDER_GAUSS, abi.RENDER_RPDF])
+@pytest.mark.parametrize("where", ["mid", "edge"])
+def test_dither_rejected_draws_and_state_round_trip(oracle, icw, rtype, where):
+    """mtrnd_gen_dsopen rejects a draw of exactly -1.0 and draws again (mt_jrnd.c:245-256).  A raw
+    MT word 0 tempers to 0, so zeroed words force rejected pairs; the state blob carries the
+    render state, so the same words go into the GPU context and the oracle stream."""
+    import ctypes as C
+    cfg = graph.default_config(48000, need24bits=True)
+    cfg.render.render_type = rtype
+    cfg.render.nshape_type = abi.NSHAPE_FW44 if rtype != abi.RENDER_RPDF else abi.NSHAPE_FLAT
+    nodes = graph.graph_master_only()
+    raw = synth.batch_pcm(2, 3000, 48000)
+    ctx = icw.Context(cfg, nodes, 2)
+    o1, _ = ctx.process(raw[:, :700 * 4], 700)
+    blob = abi.StateBlob.from_buffer_copy(ctx.get_state(1))
+    assert blob.has_render == 1
+    words, idx = [], []
+    for ch in range(2):
+        w = np.frombuffer(bytes(blob.mt[ch]), dtype=np.uint32).copy()
+        i0 = blob.mt_idx[ch]
+        start = i0 + 5 if where == "mid" else 621            # a pair straddling the next twist
+        w[min(start, 623):min(start + 6, 624)] = 0
+        if where == "mid" and i0 + 5 >= 624:
+            w[:6] = 0
+        words.append(w)
+        idx.append(i0)
+        C.memmove(C.addressof(blob.mt[ch]), w.ctypes.data, 624 * 4)
+    ctx.set_state(1, bytes(blob))
+    o2, p2 = ctx.process(np.ascontiguousarray(raw[:, 700 * 4:]), 2300, want_pre=True)
+    st = oracle.Stream(cfg, nodes)
+    r1, _ = st.process(raw[1, :700 * 4], 700)
+    assert np.array_equal(o1[1], r1)
+    for ch in range(2):
+        st.set_mt(ch, words[ch], idx[ch])
+    r2, rp2 = st.process(raw[1, 700 * 4:], 2300, want_pre=True)
+    assert np.array_equal(p2[1].view(np.uint64), rp2.view(np.uint64))
+    assert np.array_equal(o2[1], r2)
