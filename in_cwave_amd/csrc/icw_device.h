@@ -30,6 +30,9 @@ struct IcwK0Args {
     double *xd;                    /* [n_chains][x_pitch]: each chain's own filter input sequence;
                                       complex input: rows s*4 + ch*2 + {0: I, 1: Q} hold the samples */
     size_t x_pitch;
+    const double *hist;            /* [n_chains][ICW_HIST_PITCH] delay lines at block start */
+    int32_t nord;
+    uint32_t *mono_dup;            /* [n_streams] out: 1 if the right converters will reproduce the left */
 };
 
 /* Arguments of the block bookkeeping kernel for complex input (no Hilbert): one thread per stream. */
@@ -161,6 +164,7 @@ struct IcwK2Args {
     unsigned long long *peak_bits; /* [n_streams][2] max |q| as ordered bits */
     IcwRenderK rk;
     double pc[20], pd[20], d0;
+    const uint32_t *mono_dup;      /* [n_streams] K0's flag: right outputs == left outputs this block */
     const double *xin;             /* complex input: K0's I/Q rows (then w is unused) */
     size_t x_pitch;
     int32_t cw;

@@ -86,6 +86,7 @@ struct icw_ctx {
     double *xd[2] = {nullptr, nullptr};
     size_t xd_bytes[2] = {0, 0};
     uint32_t *info_phase[2] = {nullptr, nullptr};
+    uint32_t *mono_dup[2] = {nullptr, nullptr};
     unsigned long long *info_nframe[2] = {nullptr, nullptr};
     hipStream_t stream2 = nullptr;
     hipEvent_t k1done[2] = {nullptr, nullptr}, k2done[2] = {nullptr, nullptr}, join = nullptr;
@@ -351,7 +352,7 @@ void free_all(icw_ctx *c)
 {
     DevState &s = c->st;
     void *ptrs[] = {s.mt, s.mt_idx, s.rs, c->rpre, c->iq, s.err, s.hist, s.sncnt, s.hq_phase, s.pos, s.fade, s.n_frame, s.bus, s.clips, s.peak_bits,
-                    c->d_prog, c->w[0], c->w[1], c->xd[0], c->xd[1], c->info_phase[0], c->info_phase[1],
+                    c->d_prog, c->mono_dup[0], c->mono_dup[1], c->w[0], c->w[1], c->xd[0], c->xd[1], c->info_phase[0], c->info_phase[1],
                     c->info_nframe[0], c->info_nframe[1], c->d_in, c->d_out, c->d_pre};
     for (void *p : ptrs)
         if (p) hipFree(p);
@@ -467,6 +468,7 @@ int icw_create(const icw_config *cfg, const icw_node *nodes, int n_nodes, int n_
     }
     for (int p = 0; p < 2; ++p) {
         rc |= dalloc(&c->info_phase[p], S * 2);
+        rc |= dalloc(&c->mono_dup[p], S);
         rc |= dalloc(&c->info_nframe[p], S);
     }
     rc |= dalloc(&c->d_prog, 1);
@@ -735,6 +737,9 @@ int icw_process_streams(icw_ctx *c, int first, int count, const void *in, size_t
         a0.hq_phase = ds.hq_phase + f0 * 2;
         a0.xd = c->xd[p];
         a0.x_pitch = x_pitch;
+        a0.hist = ds.hist + f0 * 4 * ICW_HIST_PITCH;
+        a0.nord = N;
+        a0.mono_dup = c->mono_dup[p];
         /* xd[p], w[p], info[p] were last read by the output kernel of block b-2 */
         if (b >= 2 && hipStreamWaitEvent(st, c->k2done[p], 0) != hipSuccess) return ICW_EDEVICE;
         if (icw_launch_unpack(&a0, st) != hipSuccess) return ICW_EDEVICE;
@@ -817,6 +822,7 @@ int icw_process_streams(icw_ctx *c, int first, int count, const void *in, size_t
         memcpy(a2.pd, c->pd, sizeof(a2.pd));
         a2.d0 = c->d0;
         a2.cw = cw ? 1 : 0;
+        a2.mono_dup = c->mono_dup[p];
         a2.xin = c->xd[p];
         a2.x_pitch = x_pitch;
         if (bus) a2.iq_out = c->iq;

@@ -211,6 +211,16 @@ __global__ __launch_bounds__(256) void icw_unpack_frames(IcwK0Args a)
 {
     const int t = blockIdx.x * 256 + threadIdx.x;
     const int s = blockIdx.y;
+    if (t == 0 && a.mono_dup) {
+        /* Mono input feeds both converters the same samples, so if their delay lines and phases
+         * are bit-identical now, the right converters reproduce the left ones through the whole
+         * block and the output kernel may copy instead of recomputing. */
+        uint32_t same = (a.nch == 1 && a.fmt < ICW_FMT_CW_F64 && a.hq_phase[s * 2] == a.hq_phase[s * 2 + 1]) ? 1u : 0u;
+        const double *hl = a.hist + (size_t)s * 4 * ICW_HIST_PITCH;
+        for (int i = 0; same && i < 2 * ICW_HIST_PITCH; ++i)
+            if (__double_as_longlong(hl[i]) != __double_as_longlong(hl[2 * ICW_HIST_PITCH + i])) same = 0u;
+        a.mono_dup[s] = same;
+    }
     if (t >= a.T) return;
     const unsigned char *fp = a.in + (size_t)s * a.in_stride + (size_t)t * a.fsz;
     const long long ix = a.pos[s] + t;
@@ -807,10 +817,18 @@ __global__ __launch_bounds__(ICW_K2_TILE) void icw_output(IcwK2Args a)
             double pc[20], pd[20];
 #pragma unroll
             for (int i = 0; i < 20; ++i) { pc[i] = a.pc[i]; pd[i] = a.pd[i]; }
-            /* filter outputs of the 4 chains (L-I, L-Q, R-I, R-Q) */
+            /* filter outputs of the 4 chains (L-I, L-Q, R-I, R-Q); the right pair is a copy when the
+             * converters are provably identical this block (mono, equal state: K0's flag) */
             double y[4];
-#pragma unroll
-            for (int c = 0; c < 4; ++c) y[c] = icw_iir_out<N, KAHAN>(&lw[c][tl], pc, pd, a.d0);
+            y[0] = icw_iir_out<N, KAHAN>(&lw[0][tl], pc, pd, a.d0);
+            y[1] = icw_iir_out<N, KAHAN>(&lw[1][tl], pc, pd, a.d0);
+            if (a.mono_dup && a.mono_dup[s]) {
+                y[2] = y[0];
+                y[3] = y[1];
+            } else {
+                y[2] = icw_iir_out<N, KAHAN>(&lw[2][tl], pc, pd, a.d0);
+                y[3] = icw_iir_out<N, KAHAN>(&lw[3][tl], pc, pd, a.d0);
+            }
 
             /* fs/4 un-mix (lpf_hilbert_quad.c:129-156) */
             double oI[2], oQ[2];

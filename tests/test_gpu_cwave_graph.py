@@ -148,3 +148,29 @@ def test_dither_rejected_draws_and_state_round_trip(oracle, icw, rtype, where):
     r2, rp2 = st.process(raw[1, 700 * 4:], 2300, want_pre=True)
     assert np.array_equal(p2[1].view(np.uint64), rp2.view(np.uint64))
     assert np.array_equal(o2[1], r2)
+
+
+def test_mono_after_stereo_track(oracle, icw):
+    """a mono track right after a stereo one: the converters' states differ, so the right outputs
+    must be computed, not copied (the output kernel's mono shortcut needs identical state)"""
+    fs = 48000
+    cfg = graph.default_config(fs)
+    nodes = graph.graph_shift_master()
+    ctx = icw.Context(cfg, nodes, 3)
+    sts = [oracle.Stream(cfg, nodes) for _ in range(3)]
+    for i, (ch, n) in enumerate([(2, 1500), (1, 4000), (1, 2000)]):
+        raw = synth.batch_pcm(3, n, fs, channels=ch, first=5 * i)
+        ctx.set_input(fs, abi.FMT_I16, ch)
+        out, pre = ctx.process(raw, n, want_pre=True)
+        for s in range(3):
+            sts[s].set_input(fs, abi.FMT_I16, ch)
+            ro, rp = sts[s].process(raw[s], n, want_pre=True)
+            rel = np.abs(pre[s] - rp) / np.maximum(np.abs(rp), 1.0)
+            assert rel.max() <= 1e-6, (i, s)
+            same = pre[s].view(np.uint64) == rp.view(np.uint64)
+            assert np.array_equal(out[s].reshape(n, 2, 2)[same], ro.reshape(n, 2, 2)[same])
+    # the mono tracks after a fresh start do take the shortcut: left == right exactly
+    ctx2 = icw.Context(graph.default_config(fs, channels=1), graph.graph_master_only(), 2)
+    raw = synth.batch_pcm(2, 3000, fs, channels=1)
+    _, pre = ctx2.process(raw, 3000, want_pre=True)
+    assert np.array_equal(pre[:, :, 0].view(np.uint64), pre[:, :, 1].view(np.uint64))
