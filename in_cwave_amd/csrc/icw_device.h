@@ -24,34 +24,34 @@ struct IcwK0Args {
     size_t in_stride;
     uint32_t fmt, csz, fsz, nch;   /* sample format, channel/frame bytes, channels */
     int32_t n_streams, T;
-    const long long *pos;          /* [n_streams] reader position (frames into track) */
+    long long t0;                  /* block offset into the call */
+    const long long *pos;          /* [n_streams] reader position at the call's start */
     const long long *fade;         /* [n_streams][3] n_samples, n_fade_in, n_fade_out */
-    const uint32_t *hq_phase;      /* [n_streams][2] Hilbert phase at block start */
+    const uint32_t *hq_phase;      /* [n_streams][2] Hilbert phase at the call's start */
     double *xd;                    /* [n_chains][x_pitch]: each chain's own filter input sequence;
                                       complex input: rows s*4 + ch*2 + {0: I, 1: Q} hold the samples */
     size_t x_pitch;
-    const double *hist;            /* [n_chains][ICW_HIST_PITCH] delay lines at block start */
-    int32_t nord;
-    uint32_t *mono_dup;            /* [n_streams] out: 1 if the right converters will reproduce the left */
 };
 
-/* Arguments of the block bookkeeping kernel for complex input (no Hilbert): one thread per stream. */
+/* Arguments of the call-end bookkeeping kernel: one thread per stream.  During a call every
+ * kernel reads the call-start position / phases / frame counter and adds its block offset; this
+ * kernel advances them once, after the last block. */
 struct IcwAdvArgs {
-    int32_t n_streams, T;
-    const uint32_t *hq_phase;
+    int32_t n_streams, cw;
+    long long n;                   /* frames processed by the call */
+    uint32_t *hq_phase;
     long long *pos;
     unsigned long long *n_frame;
     unsigned long long ssr;
     int32_t scaled;
-    uint32_t *info_phase;
-    unsigned long long *info_nframe;
 };
 
 /* Arguments of the serial graph kernel (bus form; one lane = one stream, loops over frames). */
 struct IcwK4Args {
     const double *iq;              /* [n_streams][T][4] `in` per frame (lre, lim, rre, rim) */
     int32_t n_streams, T;
-    const unsigned long long *info_nframe;
+    long long t0;
+    const unsigned long long *n_frame;   /* call-start frame counters */
     unsigned long long ssr;
     int32_t scaled;
     uint32_t sample_rate;
@@ -69,15 +69,10 @@ struct IcwK1Args {
     int32_t n_streams, n_chains, T;
     double *hist;                  /* [n_chains][ICW_HIST_PITCH], index 0 = most recent w */
     unsigned long long *sncnt;     /* [n_chains] subnorm rejections */
-    uint32_t *hq_phase;            /* [n_streams][2] Hilbert sample phase (sampe_ix) */
-    long long *pos;                /* [n_streams] reader position, advanced by T */
-    unsigned long long *n_frame;   /* [n_streams] modulator frame counter */
-    unsigned long long ssr;        /* sample_rate * HZ_SCALE (scaled mode) */
-    int32_t scaled;
     double *w;                     /* [n_chains][w_pitch]: rows [0,N) history, [N,N+T) block */
     size_t w_pitch;
-    uint32_t *info_phase;          /* [n_streams][2] block-start Hilbert phases (for K2) */
-    unsigned long long *info_nframe; /* [n_streams] block-start n_frame (for K2) */
+    uint32_t *lr_equal;            /* [n_streams] left and right converters bit-identical (state) */
+    uint32_t *info_dup;            /* [n_streams] lr_equal at this block's start (for K2) */
     int *err;                      /* set by a bounded spin that gave up (never in a healthy run) */
     double pc[20];                 /* loop-back coefficients -a[i+1]/a0 */
 };
@@ -146,9 +141,10 @@ struct IcwK3Args {
 struct IcwK2Args {
     const double *w;               /* [n_chains][w_pitch] */
     size_t w_pitch;
-    int32_t n_streams, T, n_chains;
-    const uint32_t *info_phase;
-    const unsigned long long *info_nframe;
+    int32_t n_streams, T, n_chains, nch;
+    long long t0;                  /* block offset into the call */
+    const uint32_t *hq_phase;      /* [n_streams][2] call-start Hilbert phases */
+    const unsigned long long *n_frame;   /* [n_streams] call-start frame counters */
     unsigned long long ssr;
     int32_t scaled;
     uint32_t sample_rate;
@@ -164,7 +160,7 @@ struct IcwK2Args {
     unsigned long long *peak_bits; /* [n_streams][2] max |q| as ordered bits */
     IcwRenderK rk;
     double pc[20], pd[20], d0;
-    const uint32_t *mono_dup;      /* [n_streams] K0's flag: right outputs == left outputs this block */
+    const uint32_t *info_dup;      /* [n_streams] K1's flag: the converters were identical at block start */
     const double *xin;             /* complex input: K0's I/Q rows (then w is unused) */
     size_t x_pitch;
     int32_t cw;

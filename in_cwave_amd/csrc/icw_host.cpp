@@ -61,6 +61,14 @@ struct DevState {
     uint32_t *mt = nullptr;               /* [624][2*streams] */
     int32_t *mt_idx = nullptr;            /* [2*streams] */
     double *rs = nullptr;                 /* [2*streams][ICW_RSTATE] */
+    uint32_t *lr_equal = nullptr;         /* [streams] right converters bit-identical to left ones */
+};
+
+/* streams confined to disjoint CU sets: K1 on k1_cus CUs spread over the device, the rest on
+ * the other CUs (hipExtStreamCreateWithCUMask) */
+struct CuSplit {
+    int k1_cus = 0;
+    hipStream_t k1 = nullptr, rest = nullptr, dith = nullptr;
 };
 
 }  // namespace
@@ -85,11 +93,13 @@ struct icw_ctx {
     size_t w_bytes[2] = {0, 0};
     double *xd[2] = {nullptr, nullptr};
     size_t xd_bytes[2] = {0, 0};
-    uint32_t *info_phase[2] = {nullptr, nullptr};
-    uint32_t *mono_dup[2] = {nullptr, nullptr};
-    unsigned long long *info_nframe[2] = {nullptr, nullptr};
+    uint32_t *info_dup[2] = {nullptr, nullptr};
     hipStream_t stream2 = nullptr;
     hipEvent_t k1done[2] = {nullptr, nullptr}, k2done[2] = {nullptr, nullptr}, join = nullptr;
+    hipEvent_t k0done[2] = {nullptr, nullptr};
+    std::vector<CuSplit> splits;          /* cached CU-partitioned stream sets, by K1 CU count */
+    bool cu_split = true;                 /* ICW_CU_SPLIT=0 disables the partition */
+    int k1_wpc = 4;                       /* ICW_K1_WPC: K1 waves per CU (one per SIMD) */
     /* dither generation (K3a) runs on its own stream, double-buffered like the block scratch */
     hipStream_t stream3 = nullptr;
     hipEvent_t ditdone[2] = {nullptr, nullptr};
@@ -110,6 +120,7 @@ struct icw_ctx {
     int n_cu = 256;
     bool pair_mode = false;   /* chain+helper wave pairs (few chains per SIMD) vs plain lanes */
     bool dither_lane = false; /* ICW_DITHER=lane: lane-per-channel dither generator (A/B only) */
+    bool serialize = false;   /* ICW_SERIALIZE=1: every kernel on the caller's stream (profiling) */
     double last_ms[2]{};
     int last_launches[2]{};
     std::mutex mu;
@@ -348,12 +359,44 @@ int grow(void **p, size_t *cur, size_t need)
     return ICW_OK;
 }
 
+/* The stream set for a K1 of k1_cus CUs: K1's CUs are spread evenly over the device (every
+ * n_cu / k1_cus-th CU, so each XCD gets its share), the other streams get the remaining CUs. */
+/* wait for every kernel and copy of the context (they run on several streams, the caller's among
+ * them); host-side state changes and reads happen only between calls */
+hipError_t quiesce(icw_ctx *c)
+{
+    (void)c;
+    return hipDeviceSynchronize();
+}
+
+const CuSplit *cu_split(icw_ctx *c, int k1_cus)
+{
+    for (auto &x : c->splits)
+        if (x.k1_cus == k1_cus) return &x;
+    const int n = c->n_cu, words = (n + 31) / 32;
+    std::vector<uint32_t> mk(words, 0u), mr(words, 0u);
+    std::vector<char> used(n, 0);
+    for (int i = 0; i < k1_cus; ++i) used[(int)((long)i * n / k1_cus)] = 1;
+    for (int cu = 0; cu < n; ++cu) (used[cu] ? mk : mr)[cu / 32] |= 1u << (cu % 32);
+    CuSplit x;
+    x.k1_cus = k1_cus;
+    if (hipExtStreamCreateWithCUMask(&x.k1, (uint32_t)words, mk.data()) != hipSuccess ||
+        hipExtStreamCreateWithCUMask(&x.rest, (uint32_t)words, mr.data()) != hipSuccess ||
+        hipExtStreamCreateWithCUMask(&x.dith, (uint32_t)words, mr.data()) != hipSuccess) {
+        for (hipStream_t q : {x.k1, x.rest, x.dith})
+            if (q) hipStreamDestroy(q);
+        return nullptr;
+    }
+    c->splits.push_back(x);
+    return &c->splits.back();
+}
+
 void free_all(icw_ctx *c)
 {
     DevState &s = c->st;
-    void *ptrs[] = {s.mt, s.mt_idx, s.rs, c->rpre, c->iq, s.err, s.hist, s.sncnt, s.hq_phase, s.pos, s.fade, s.n_frame, s.bus, s.clips, s.peak_bits,
-                    c->d_prog, c->mono_dup[0], c->mono_dup[1], c->w[0], c->w[1], c->xd[0], c->xd[1], c->info_phase[0], c->info_phase[1],
-                    c->info_nframe[0], c->info_nframe[1], c->d_in, c->d_out, c->d_pre};
+    void *ptrs[] = {s.mt, s.mt_idx, s.rs, s.lr_equal, c->rpre, c->iq, s.err, s.hist, s.sncnt, s.hq_phase, s.pos, s.fade,
+                    s.n_frame, s.bus, s.clips, s.peak_bits, c->d_prog, c->info_dup[0], c->info_dup[1], c->w[0], c->w[1],
+                    c->xd[0], c->xd[1], c->d_in, c->d_out, c->d_pre};
     for (void *p : ptrs)
         if (p) hipFree(p);
     for (double *d : {c->dith[0], c->dith[1]})
@@ -361,8 +404,11 @@ void free_all(icw_ctx *c)
     for (hipEvent_t e : {c->ditdone[0], c->ditdone[1]})
         if (e) hipEventDestroy(e);
     if (c->stream3) hipStreamDestroy(c->stream3);
-    for (hipEvent_t e : {c->k1done[0], c->k1done[1], c->k2done[0], c->k2done[1], c->join})
+    for (hipEvent_t e : {c->k1done[0], c->k1done[1], c->k2done[0], c->k2done[1], c->k0done[0], c->k0done[1], c->join})
         if (e) hipEventDestroy(e);
+    for (auto &x : c->splits)
+        for (hipStream_t q : {x.k1, x.rest, x.dith})
+            if (q) hipStreamDestroy(q);
     if (c->stream2) hipStreamDestroy(c->stream2);
     for (auto e : c->ev) hipEventDestroy(e);
     if (c->stream) hipStreamDestroy(c->stream);
@@ -466,11 +512,8 @@ int icw_create(const icw_config *cfg, const icw_node *nodes, int n_nodes, int n_
         rc |= dalloc(&s.mt_idx, S * 2);
         rc |= dalloc(&s.rs, S * 2 * ICW_RSTATE);
     }
-    for (int p = 0; p < 2; ++p) {
-        rc |= dalloc(&c->info_phase[p], S * 2);
-        rc |= dalloc(&c->mono_dup[p], S);
-        rc |= dalloc(&c->info_nframe[p], S);
-    }
+    rc |= dalloc(&s.lr_equal, S);
+    for (int p = 0; p < 2; ++p) rc |= dalloc(&c->info_dup[p], S);
     rc |= dalloc(&c->d_prog, 1);
     if (rc == ICW_OK && hipMemcpy(c->d_prog, &c->prog, sizeof(IcwProg), hipMemcpyHostToDevice) != hipSuccess)
         rc = ICW_EDEVICE;
@@ -480,7 +523,8 @@ int icw_create(const icw_config *cfg, const icw_node *nodes, int n_nodes, int n_
     for (int p = 0; p < 2 && rc == ICW_OK; ++p)
         if (hipEventCreateWithFlags(&c->k1done[p], hipEventDisableTiming) != hipSuccess ||
             hipEventCreateWithFlags(&c->k2done[p], hipEventDisableTiming) != hipSuccess ||
-            hipEventCreateWithFlags(&c->ditdone[p], hipEventDisableTiming) != hipSuccess)
+            hipEventCreateWithFlags(&c->ditdone[p], hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&c->k0done[p], hipEventDisableTiming) != hipSuccess)
             rc = ICW_EDEVICE;
     if (rc == ICW_OK && hipEventCreateWithFlags(&c->join, hipEventDisableTiming) != hipSuccess) rc = ICW_EDEVICE;
     if (rc != ICW_OK) {
@@ -503,6 +547,12 @@ int icw_create(const icw_config *cfg, const icw_node *nodes, int n_nodes, int n_
         if (m && !strcmp(m, "pair")) c->pair_mode = true;
         const char *d = getenv("ICW_DITHER");
         c->dither_lane = d && !strcmp(d, "lane");
+        const char *z = getenv("ICW_SERIALIZE");
+        c->serialize = z && !strcmp(z, "1");
+        const char *cs = getenv("ICW_CU_SPLIT");
+        if (cs && !strcmp(cs, "0")) c->cu_split = false;
+        const char *wpc = getenv("ICW_K1_WPC");
+        if (wpc && atoi(wpc) >= 1 && atoi(wpc) <= 8) c->k1_wpc = atoi(wpc);
     }
     rc = icw_stream_init(c, 0, n_streams);
     if (rc) { free_all(c); delete c; return rc; }
@@ -514,7 +564,7 @@ int icw_destroy(icw_ctx *c)
 {
     if (!c) return ICW_EINVAL;
     set_dev(c);
-    hipStreamSynchronize(c->stream);
+    quiesce(c);
     free_all(c);
     delete c;
     return ICW_OK;
@@ -533,6 +583,7 @@ int icw_stream_init(icw_ctx *c, int first, int count)
     ok &= hipMemsetAsync(s.hist + f * 4 * ICW_HIST_PITCH, 0, n * 4 * ICW_HIST_PITCH * sizeof(double), st) == hipSuccess;
     ok &= hipMemsetAsync(s.sncnt + f * 4, 0, n * 4 * sizeof(unsigned long long), st) == hipSuccess;
     ok &= hipMemsetAsync(s.hq_phase + f * 2, 0, n * 2 * sizeof(uint32_t), st) == hipSuccess;
+    ok &= hipMemsetD32Async((hipDeviceptr_t)(s.lr_equal + f), 1, n, st) == hipSuccess;
     ok &= hipMemsetAsync(s.pos + f, 0, n * sizeof(long long), st) == hipSuccess;
     ok &= hipMemsetAsync(s.n_frame + f, 0, n * sizeof(unsigned long long), st) == hipSuccess;
     ok &= hipMemsetAsync(s.bus + f * ICW_N_INPUTS * 4, 0, n * ICW_N_INPUTS * 4 * sizeof(double), st) == hipSuccess;
@@ -579,13 +630,15 @@ int icw_stream_open(icw_ctx *c, int s, int64_t n_samples, uint32_t fade_in, uint
     std::lock_guard<std::mutex> lk(c->mu);
     if (set_dev(c)) return ICW_EDEVICE;
     long long fd[3] = {(long long)n_samples, nfi, nfo};
-    bool ok = hipMemcpy(c->st.fade + (size_t)s * 3, fd, sizeof(fd), hipMemcpyHostToDevice) == hipSuccess;
+    bool ok = quiesce(c) == hipSuccess;
+    ok &= hipMemcpy(c->st.fade + (size_t)s * 3, fd, sizeof(fd), hipMemcpyHostToDevice) == hipSuccess;
     ok &= hipMemset(c->st.pos + s, 0, sizeof(long long)) == hipSuccess;
     if (clr_nframe) ok &= hipMemset(c->st.n_frame + s, 0, sizeof(unsigned long long)) == hipSuccess;
     if (clr_hilb) {
         ok &= hipMemset(c->st.hist + (size_t)s * 4 * ICW_HIST_PITCH, 0, 4 * ICW_HIST_PITCH * sizeof(double)) == hipSuccess;
         ok &= hipMemset(c->st.sncnt + (size_t)s * 4, 0, 4 * sizeof(unsigned long long)) == hipSuccess;
         ok &= hipMemset(c->st.hq_phase + (size_t)s * 2, 0, 2 * sizeof(uint32_t)) == hipSuccess;
+        ok &= hipMemsetD32((hipDeviceptr_t)(c->st.lr_equal + s), 1, 1) == hipSuccess;
     }
     /* sound_render_set_outbits -> sound_render_recalc: prev_rnd, shaper buffers and prev_ns_err
      * reset, the RNG is not (sound_render.c:527-580) */
@@ -599,9 +652,11 @@ int icw_stream_reset_hilbert(icw_ctx *c, int s)
     if (!c || s < 0 || s >= c->n_streams) return ICW_EINVAL;
     std::lock_guard<std::mutex> lk(c->mu);
     if (set_dev(c)) return ICW_EDEVICE;
-    bool ok = hipMemset(c->st.hist + (size_t)s * 4 * ICW_HIST_PITCH, 0, 4 * ICW_HIST_PITCH * sizeof(double)) == hipSuccess;
+    bool ok = quiesce(c) == hipSuccess;
+    ok &= hipMemset(c->st.hist + (size_t)s * 4 * ICW_HIST_PITCH, 0, 4 * ICW_HIST_PITCH * sizeof(double)) == hipSuccess;
     ok &= hipMemset(c->st.sncnt + (size_t)s * 4, 0, 4 * sizeof(unsigned long long)) == hipSuccess;
     ok &= hipMemset(c->st.hq_phase + (size_t)s * 2, 0, 2 * sizeof(uint32_t)) == hipSuccess;
+    ok &= hipMemsetD32((hipDeviceptr_t)(c->st.lr_equal + s), 1, 1) == hipSuccess;
     return ok ? ICW_OK : ICW_EDEVICE;
 }
 
@@ -610,6 +665,7 @@ int icw_stream_reset_framecnt(icw_ctx *c, int s)
     if (!c || s < 0 || s >= c->n_streams) return ICW_EINVAL;
     std::lock_guard<std::mutex> lk(c->mu);
     if (set_dev(c)) return ICW_EDEVICE;
+    if (quiesce(c) != hipSuccess) return ICW_EDEVICE;
     return hipMemset(c->st.n_frame + s, 0, sizeof(unsigned long long)) == hipSuccess ? ICW_OK : ICW_EDEVICE;
 }
 
@@ -619,7 +675,7 @@ int icw_stream_seek(icw_ctx *c, int s, int64_t frame_pos)
     std::lock_guard<std::mutex> lk(c->mu);
     if (set_dev(c)) return ICW_EDEVICE;
     long long v = (long long)frame_pos;
-    bool ok = hipStreamSynchronize(c->stream) == hipSuccess;
+    bool ok = quiesce(c) == hipSuccess;
     ok &= hipMemcpy(c->st.pos + s, &v, sizeof(v), hipMemcpyHostToDevice) == hipSuccess;
     return ok ? ICW_OK : ICW_EDEVICE;
 }
@@ -628,7 +684,7 @@ int icw_set_input(icw_ctx *c, uint32_t sample_rate, uint32_t fmt, uint32_t chann
 {
     if (!c || sample_rate == 0 || sample_rate > ICW_MAX_FS_SRC || fmt > ICW_FMT_CW_F32 || channels == 0) return ICW_EINVAL;
     std::lock_guard<std::mutex> lk(c->mu);
-    if (set_dev(c) || hipStreamSynchronize(c->stream) != hipSuccess) return ICW_EDEVICE;
+    if (set_dev(c) || quiesce(c) != hipSuccess) return ICW_EDEVICE;
     c->cfg.sample_rate = sample_rate;
     c->cfg.in_format = fmt;
     c->cfg.in_channels = channels;
@@ -699,15 +755,34 @@ int icw_process_streams(icw_ctx *c, int first, int count, const void *in, size_t
     const bool cw = cfg.in_format >= ICW_FMT_CW_F64;
     const bool bus = c->prog.is_bus;
     if (bus && grow((void **)&c->iq, &c->iq_bytes, S * (size_t)Tb * 4 * sizeof(double))) return ICW_ENOMEM;
-    hipStream_t st2 = c->stream2, st3 = c->stream3;
     const bool dither = c->serial_render && cfg.render.render_type != ICW_RENDER_ROUND;
     if (dither)
         for (int p = 0; p < n_sets; ++p)
             if (grow((void **)&c->dith[p], &c->dith_bytes[p], S * 2 * (size_t)Tb * sizeof(double))) return ICW_ENOMEM;
-    /* the other streams start after everything already queued on st (inputs, previous calls) */
-    if (hipEventRecord(c->join, st) != hipSuccess || hipStreamWaitEvent(st2, c->join, 0) != hipSuccess ||
-        hipStreamWaitEvent(st3, c->join, 0) != hipSuccess)
+
+    /* Streams.  sK runs the IIR state kernel K1 (the serial, issue-bound one); sA runs the input
+     * prep K0, the output kernel K2 and the serial graph / render; sD the dither generator.  When
+     * K1 needs few CUs (4 waves per CU, one per SIMD) sK is confined to those CUs and sA / sD to
+     * the rest, so the frame-parallel kernels never share a SIMD with a recurrence. */
+    hipStream_t sK = st, sA = c->stream2, sD = c->stream3;
+    if (c->serialize) {
+        sA = sD = st;
+    } else if (!cw) {
+        const int k1_waves = (count * 4 + 63) / 64;
+        const int k1_cus = (k1_waves + c->k1_wpc - 1) / c->k1_wpc;
+        if (c->cu_split && k1_cus * 2 <= c->n_cu) {
+            const CuSplit *cs = cu_split(c, k1_cus);
+            if (!cs) return ICW_EDEVICE;
+            sK = cs->k1;
+            sA = cs->rest;
+            sD = cs->dith;
+        }
+    }
+    /* every stream starts after everything already queued on st (inputs, previous calls) */
+    if (hipEventRecord(c->join, st) != hipSuccess)
         return ICW_EDEVICE;
+    for (hipStream_t x : {sK, sA, sD})
+        if (x != st && hipStreamWaitEvent(x, c->join, 0) != hipSuccess) return ICW_EDEVICE;
 
     DevState &ds = c->st;
     const size_t f0 = (size_t)first;
@@ -718,10 +793,12 @@ int icw_process_streams(icw_ctx *c, int first, int count, const void *in, size_t
             c->ev.push_back(e);
         }
     }
-    for (int b = 0; b < n_blocks; ++b) {
-        const int t0 = b * Tb;
-        const int T = std::min(Tb, n_frames - t0);
-        const int p = b & (n_sets - 1);
+    const unsigned long long ssr = (unsigned long long)cfg.sample_rate * ICW_HZ_SCALE;
+
+    /* K0 of block b on sA: xd[p] was last read by K1 of block b-2 (and, complex input, by K2 of
+     * block b-2, which precedes it on sA) */
+    auto launch_k0 = [&](int b) -> int {
+        const int t0 = b * Tb, T = std::min(Tb, n_frames - t0), p = b & (n_sets - 1);
         IcwK0Args a0;
         memset(&a0, 0, sizeof(a0));
         a0.in = d_in + (size_t)t0 * fsz;
@@ -732,63 +809,57 @@ int icw_process_streams(icw_ctx *c, int first, int count, const void *in, size_t
         a0.nch = nch;
         a0.n_streams = count;
         a0.T = T;
+        a0.t0 = t0;
         a0.pos = ds.pos + f0;
         a0.fade = ds.fade + f0 * 3;
         a0.hq_phase = ds.hq_phase + f0 * 2;
         a0.xd = c->xd[p];
         a0.x_pitch = x_pitch;
-        a0.hist = ds.hist + f0 * 4 * ICW_HIST_PITCH;
-        a0.nord = N;
-        a0.mono_dup = c->mono_dup[p];
-        /* xd[p], w[p], info[p] were last read by the output kernel of block b-2 */
-        if (b >= 2 && hipStreamWaitEvent(st, c->k2done[p], 0) != hipSuccess) return ICW_EDEVICE;
-        if (icw_launch_unpack(&a0, st) != hipSuccess) return ICW_EDEVICE;
+        if (b >= 2 && !cw && sK != sA && hipStreamWaitEvent(sA, c->k1done[p], 0) != hipSuccess) return ICW_EDEVICE;
+        if (icw_launch_unpack(&a0, sA) != hipSuccess) return ICW_EDEVICE;
+        if (hipEventRecord(c->k0done[p], sA) != hipSuccess) return ICW_EDEVICE;
+        return ICW_OK;
+    };
 
-        IcwK1Args a1;
-        memset(&a1, 0, sizeof(a1));
-        a1.xd = c->xd[p];
-        a1.x_pitch = x_pitch;
-        a1.nch = nch;
-        a1.n_streams = count;
-        a1.n_chains = count * 4;
-        a1.T = T;
-        a1.hist = ds.hist + f0 * 4 * ICW_HIST_PITCH;
-        a1.sncnt = ds.sncnt + f0 * 4;
-        a1.hq_phase = ds.hq_phase + f0 * 2;
-        a1.pos = ds.pos + f0;
-        a1.n_frame = ds.n_frame + f0;
-        a1.err = ds.err;
-        a1.ssr = (unsigned long long)cfg.sample_rate * ICW_HZ_SCALE;
-        a1.scaled = cfg.frmod_scaled;
-        a1.w = c->w[p];
-        a1.w_pitch = w_pitch;
-        a1.info_phase = c->info_phase[p];
-        a1.info_nframe = c->info_nframe[p];
-        memcpy(a1.pc, c->pc, sizeof(a1.pc));
-        if (timing) hipEventRecord(c->ev[4 * b], st);
-        hipError_t e1;
-        if (cw) {
-            /* complex input: no Hilbert, only the block bookkeeping */
-            IcwAdvArgs av;
-            memset(&av, 0, sizeof(av));
-            av.n_streams = count;
-            av.T = T;
-            av.hq_phase = a1.hq_phase;
-            av.pos = a1.pos;
-            av.n_frame = a1.n_frame;
-            av.ssr = a1.ssr;
-            av.scaled = a1.scaled;
-            av.info_phase = a1.info_phase;
-            av.info_nframe = a1.info_nframe;
-            e1 = icw_launch_advance(&av, st);
-        } else {
-            e1 = c->pair_mode ? icw_launch_iir_pair(&a1, N, cfg.iir_kahan, cfg.iir_subnorm_reject, st)
-                              : icw_launch_iir_state(&a1, N, cfg.iir_kahan, cfg.iir_subnorm_reject, st);
+    int rc0 = launch_k0(0);
+    if (rc0) return rc0;
+    for (int b = 0; b < n_blocks; ++b) {
+        const int t0 = b * Tb;
+        const int T = std::min(Tb, n_frames - t0);
+        const int p = b & (n_sets - 1);
+        /* the next block's input prep overlaps this block's recurrence */
+        if (b + 1 < n_blocks && (rc0 = launch_k0(b + 1)) != ICW_OK) return rc0;
+
+        if (!cw) {
+            IcwK1Args a1;
+            memset(&a1, 0, sizeof(a1));
+            a1.xd = c->xd[p];
+            a1.x_pitch = x_pitch;
+            a1.nch = nch;
+            a1.n_streams = count;
+            a1.n_chains = count * 4;
+            a1.T = T;
+            a1.hist = ds.hist + f0 * 4 * ICW_HIST_PITCH;
+            a1.sncnt = ds.sncnt + f0 * 4;
+            a1.err = ds.err;
+            a1.w = c->w[p];
+            a1.w_pitch = w_pitch;
+            a1.lr_equal = ds.lr_equal + f0;
+            a1.info_dup = c->info_dup[p];
+            memcpy(a1.pc, c->pc, sizeof(a1.pc));
+            /* K0(b) done; it came after K2(b-2) on sA, the last reader of w[p] / info_dup[p] */
+            if (sK != sA && hipStreamWaitEvent(sK, c->k0done[p], 0) != hipSuccess) return ICW_EDEVICE;
+            if (timing) hipEventRecord(c->ev[4 * b], sK);
+            const hipError_t e1 = c->pair_mode ? icw_launch_iir_pair(&a1, N, cfg.iir_kahan, cfg.iir_subnorm_reject, sK)
+                                               : icw_launch_iir_state(&a1, N, cfg.iir_kahan, cfg.iir_subnorm_reject, sK);
+            if (e1 != hipSuccess) return ICW_EDEVICE;
+            if (timing) hipEventRecord(c->ev[4 * b + 1], sK);
+            if (hipEventRecord(c->k1done[p], sK) != hipSuccess) return ICW_EDEVICE;
+            if (sK != sA && hipStreamWaitEvent(sA, c->k1done[p], 0) != hipSuccess) return ICW_EDEVICE;
+        } else if (timing) {
+            hipEventRecord(c->ev[4 * b], sA);
+            hipEventRecord(c->ev[4 * b + 1], sA);
         }
-        if (e1 != hipSuccess) return ICW_EDEVICE;
-        if (timing) hipEventRecord(c->ev[4 * b + 1], st);
-        if (hipEventRecord(c->k1done[p], st) != hipSuccess || hipStreamWaitEvent(st2, c->k1done[p], 0) != hipSuccess)
-            return ICW_EDEVICE;
 
         IcwK2Args a2;
         memset(&a2, 0, sizeof(a2));
@@ -797,9 +868,11 @@ int icw_process_streams(icw_ctx *c, int first, int count, const void *in, size_t
         a2.n_streams = count;
         a2.T = T;
         a2.n_chains = count * 4;
-        a2.info_phase = c->info_phase[p];
-        a2.info_nframe = c->info_nframe[p];
-        a2.ssr = a1.ssr;
+        a2.nch = nch;
+        a2.t0 = t0;
+        a2.hq_phase = ds.hq_phase + f0 * 2;
+        a2.n_frame = ds.n_frame + f0;
+        a2.ssr = ssr;
         a2.scaled = cfg.frmod_scaled;
         a2.sample_rate = cfg.sample_rate;
         a2.prog = c->d_prog;
@@ -822,19 +895,20 @@ int icw_process_streams(icw_ctx *c, int first, int count, const void *in, size_t
         memcpy(a2.pd, c->pd, sizeof(a2.pd));
         a2.d0 = c->d0;
         a2.cw = cw ? 1 : 0;
-        a2.mono_dup = c->mono_dup[p];
+        a2.info_dup = cw ? nullptr : c->info_dup[p];
         a2.xin = c->xd[p];
         a2.x_pitch = x_pitch;
         if (bus) a2.iq_out = c->iq;
-        if (timing) hipEventRecord(c->ev[4 * b + 2], st2);
-        if (icw_launch_output(&a2, N, cfg.iir_kahan, st2) != hipSuccess) return ICW_EDEVICE;
+        if (timing) hipEventRecord(c->ev[4 * b + 2], sA);
+        if (icw_launch_output(&a2, N, cfg.iir_kahan, sA) != hipSuccess) return ICW_EDEVICE;
         if (bus) {
             IcwK4Args a4;
             memset(&a4, 0, sizeof(a4));
             a4.iq = c->iq;
             a4.n_streams = count;
             a4.T = T;
-            a4.info_nframe = a2.info_nframe;
+            a4.t0 = t0;
+            a4.n_frame = a2.n_frame;
             a4.ssr = a2.ssr;
             a4.scaled = a2.scaled;
             a4.sample_rate = a2.sample_rate;
@@ -842,7 +916,7 @@ int icw_process_streams(icw_ctx *c, int first, int count, const void *in, size_t
             a4.bus = a2.bus;
             a4.pre = a2.pre;
             a4.pre_stride = a2.pre_stride;
-            if (icw_launch_graph_serial(&a4, st2) != hipSuccess) return ICW_EDEVICE;
+            if (icw_launch_graph_serial(&a4, sA) != hipSuccess) return ICW_EDEVICE;
         }
         if (c->serial_render) {
             IcwK3Args a3;
@@ -865,20 +939,35 @@ int icw_process_streams(icw_ctx *c, int first, int count, const void *in, size_t
                 /* K3a for this block on its own stream: dith[p] was last read by K3b of block b-2 */
                 a3.dith = c->dith[p];
                 a3.dith_pitch = (size_t)count * 2;    /* time-major [T][count*2] */
-                if (b >= 2 && hipStreamWaitEvent(st3, c->k2done[p], 0) != hipSuccess) return ICW_EDEVICE;
-                const hipError_t ed = c->dither_lane ? icw_launch_dither_lane(&a3, st3) : icw_launch_dither(&a3, st3);
-                if (ed != hipSuccess || hipEventRecord(c->ditdone[p], st3) != hipSuccess ||
-                    hipStreamWaitEvent(st2, c->ditdone[p], 0) != hipSuccess)
+                if (b >= 2 && sD != sA && hipStreamWaitEvent(sD, c->k2done[p], 0) != hipSuccess) return ICW_EDEVICE;
+                const hipError_t ed = c->dither_lane ? icw_launch_dither_lane(&a3, sD) : icw_launch_dither(&a3, sD);
+                if (ed != hipSuccess || hipEventRecord(c->ditdone[p], sD) != hipSuccess ||
+                    (sD != sA && hipStreamWaitEvent(sA, c->ditdone[p], 0) != hipSuccess))
                     return ICW_EDEVICE;
             }
-            if (icw_launch_render(&a3, st2) != hipSuccess) return ICW_EDEVICE;
+            if (icw_launch_render(&a3, sA) != hipSuccess) return ICW_EDEVICE;
         }
-        if (timing) hipEventRecord(c->ev[4 * b + 3], st2);
-        if (hipEventRecord(c->k2done[p], st2) != hipSuccess) return ICW_EDEVICE;
+        if (timing) hipEventRecord(c->ev[4 * b + 3], sA);
+        if (hipEventRecord(c->k2done[p], sA) != hipSuccess) return ICW_EDEVICE;
     }
-    /* join: the caller's stream completes only after the last output kernel */
-    if (hipEventRecord(c->join, st2) != hipSuccess || hipStreamWaitEvent(st, c->join, 0) != hipSuccess)
-        return ICW_EDEVICE;
+    /* join: the caller's stream continues after every kernel of the call, then the call-start
+     * position / phases / frame counters advance (icw_advance) */
+    for (hipStream_t x : {sK, sA, sD})
+        if (x != st && (hipEventRecord(c->join, x) != hipSuccess || hipStreamWaitEvent(st, c->join, 0) != hipSuccess))
+            return ICW_EDEVICE;
+    {
+        IcwAdvArgs av;
+        memset(&av, 0, sizeof(av));
+        av.n_streams = count;
+        av.cw = cw ? 1 : 0;
+        av.n = n_frames;
+        av.hq_phase = ds.hq_phase + f0 * 2;
+        av.pos = ds.pos + f0;
+        av.n_frame = ds.n_frame + f0;
+        av.ssr = ssr;
+        av.scaled = cfg.frmod_scaled;
+        if (icw_launch_advance(&av, st) != hipSuccess) return ICW_EDEVICE;
+    }
     if (!dev) {
         if (hipMemcpy2DAsync(out, out_stride, d_out, dos, dos, S, hipMemcpyDeviceToHost, st) != hipSuccess)
             return ICW_EDEVICE;
@@ -916,7 +1005,7 @@ int icw_synchronize(icw_ctx *c)
 {
     if (!c) return ICW_EINVAL;
     if (set_dev(c)) return ICW_EDEVICE;
-    if (hipStreamSynchronize(c->stream) != hipSuccess) return ICW_EDEVICE;
+    if (quiesce(c) != hipSuccess) return ICW_EDEVICE;
     int e = 0;
     if (hipMemcpy(&e, c->st.err, sizeof(int), hipMemcpyDeviceToHost) != hipSuccess || e) return ICW_EDEVICE;
     return ICW_OK;
@@ -995,7 +1084,7 @@ int icw_get_state(icw_ctx *c, int s, void *blob, size_t size)
     b.nord = (uint32_t)c->nord;
     b.has_render = c->serial_render ? 1u : 0u;
     long long fd[3];
-    bool ok = hipStreamSynchronize(c->stream) == hipSuccess;
+    bool ok = quiesce(c) == hipSuccess;
     ok &= hipMemcpy(&b.n_frame, c->st.n_frame + s, 8, hipMemcpyDeviceToHost) == hipSuccess;
     ok &= hipMemcpy(&b.pos, c->st.pos + s, 8, hipMemcpyDeviceToHost) == hipSuccess;
     ok &= hipMemcpy(fd, c->st.fade + (size_t)s * 3, sizeof(fd), hipMemcpyDeviceToHost) == hipSuccess;
@@ -1026,7 +1115,7 @@ int icw_set_state(icw_ctx *c, int s, const void *blob, size_t size)
     std::lock_guard<std::mutex> lk(c->mu);
     if (set_dev(c)) return ICW_EDEVICE;
     long long fd[3] = {b.n_samples, b.n_fade_in, b.n_fade_out};
-    bool ok = hipStreamSynchronize(c->stream) == hipSuccess;
+    bool ok = quiesce(c) == hipSuccess;
     ok &= hipMemcpy(c->st.n_frame + s, &b.n_frame, 8, hipMemcpyHostToDevice) == hipSuccess;
     ok &= hipMemcpy(c->st.pos + s, &b.pos, 8, hipMemcpyHostToDevice) == hipSuccess;
     ok &= hipMemcpy(c->st.fade + (size_t)s * 3, fd, sizeof(fd), hipMemcpyHostToDevice) == hipSuccess;
@@ -1034,6 +1123,8 @@ int icw_set_state(icw_ctx *c, int s, const void *blob, size_t size)
     ok &= hipMemcpy(c->st.hist + (size_t)s * 4 * ICW_HIST_PITCH, b.hist, sizeof(b.hist), hipMemcpyHostToDevice) == hipSuccess;
     ok &= hipMemcpy(c->st.sncnt + (size_t)s * 4, b.sncnt, sizeof(b.sncnt), hipMemcpyHostToDevice) == hipSuccess;
     ok &= hipMemcpy(c->st.bus + (size_t)s * ICW_N_INPUTS * 4, b.bus, sizeof(b.bus), hipMemcpyHostToDevice) == hipSuccess;
+    const uint32_t eq = (b.hq_phase[0] == b.hq_phase[1] && !memcmp(b.hist[0], b.hist[2], sizeof(b.hist[0]) * 2)) ? 1u : 0u;
+    ok &= hipMemcpy(c->st.lr_equal + s, &eq, 4, hipMemcpyHostToDevice) == hipSuccess;
     if (c->serial_render) {
         const size_t G = (size_t)c->n_streams * 2;
         for (int ch = 0; ch < 2; ++ch)

@@ -211,19 +211,9 @@ __global__ __launch_bounds__(256) void icw_unpack_frames(IcwK0Args a)
 {
     const int t = blockIdx.x * 256 + threadIdx.x;
     const int s = blockIdx.y;
-    if (t == 0 && a.mono_dup) {
-        /* Mono input feeds both converters the same samples, so if their delay lines and phases
-         * are bit-identical now, the right converters reproduce the left ones through the whole
-         * block and the output kernel may copy instead of recomputing. */
-        uint32_t same = (a.nch == 1 && a.fmt < ICW_FMT_CW_F64 && a.hq_phase[s * 2] == a.hq_phase[s * 2 + 1]) ? 1u : 0u;
-        const double *hl = a.hist + (size_t)s * 4 * ICW_HIST_PITCH;
-        for (int i = 0; same && i < 2 * ICW_HIST_PITCH; ++i)
-            if (__double_as_longlong(hl[i]) != __double_as_longlong(hl[2 * ICW_HIST_PITCH + i])) same = 0u;
-        a.mono_dup[s] = same;
-    }
     if (t >= a.T) return;
     const unsigned char *fp = a.in + (size_t)s * a.in_stride + (size_t)t * a.fsz;
-    const long long ix = a.pos[s] + t;
+    const long long ix = a.pos[s] + a.t0 + t;
     const double fd = icw_fade(ix, a.fade[s * 3 + 0], a.fade[s * 3 + 1], a.fade[s * 3 + 2]);
     if (a.fmt >= ICW_FMT_CW_F64) {
         /* complex (CWAVE) sample: I/Q per channel, mono -> R = L, fade on all four
@@ -253,7 +243,7 @@ __global__ __launch_bounds__(256) void icw_unpack_frames(IcwK0Args a)
     double *xs = a.xd + (size_t)s * 4 * a.x_pitch + t;
 #pragma unroll
     for (int ch = 0; ch < 2; ++ch) {
-        const unsigned k = (a.hq_phase[s * 2 + ch] + (unsigned)t) & 3u;
+        const unsigned k = (a.hq_phase[s * 2 + ch] + (unsigned)(a.t0 + t)) & 3u;
         xs[(size_t)(ch * 2 + 0) * a.x_pitch] = icw_filter_in(v[ch], k);
         xs[(size_t)(ch * 2 + 1) * a.x_pitch] = icw_filter_in(v[ch], (k + 1u) & 3u);
     }
@@ -281,7 +271,7 @@ __global__ __launch_bounds__(64) void icw_iir_state(IcwK1Args a)
 #pragma unroll
     for (int i = 0; i < N; ++i) R[N - 1 - i] = a.hist[(size_t)g * ICW_HIST_PITCH + i];
 
-    const unsigned ph0 = a.hq_phase[s * 2 + c];
+    if (f == 0 && c == 0) a.info_dup[s] = a.lr_equal[s];     /* this block's start (for K2) */
     const double *xp = a.xd + (size_t)g * a.x_pitch;
     double *wrow = a.w + (size_t)g * a.w_pitch;
     /* history rows [0, N): row j = z_{N-1-j} = R[j] */
@@ -318,16 +308,16 @@ __global__ __launch_bounds__(64) void icw_iir_state(IcwK1Args a)
     }
     icw_store_hist<N, 0>(R, a.hist, g, n_chains);
     a.sncnt[g] += cnt;
-    if (f == 0) {
-        a.info_phase[s * 2 + c] = ph0;
-        a.hq_phase[s * 2 + c] = (ph0 + (unsigned)T) & 3u;
-        if (c == 0) {
-            a.pos[s] += T;
-            const unsigned long long n0 = a.n_frame[s];
-            a.info_nframe[s] = n0;
-            a.n_frame[s] = a.scaled ? (n0 + (unsigned long long)T) % a.ssr : n0 + (unsigned long long)T;
-        }
+    /* are the stream's right converters still bit-identical to its left ones?  The 4 chains of a
+     * stream are lanes 4k..4k+3 of this wave; lane ^ 2 is the same filter of the other channel */
+    bool eq = true;
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+        const double o = __shfl_xor(R[i], 2);
+        eq = eq && (__double_as_longlong(o) == __double_as_longlong(R[i]));
     }
+    const bool eq_q = __shfl_xor((int)eq, 1) != 0;
+    if (f == 0 && c == 0) a.lr_equal[s] = (eq && eq_q) ? 1u : 0u;
 }
 
 /* ---------------------------------------- IIR state kernel, chain+helper wave pair (K1p) ---- */
@@ -502,7 +492,6 @@ __global__ __launch_bounds__(128) void icw_iir_pair(IcwK1Args a)
     }
     __syncthreads();
 
-    const unsigned ph0 = a.hq_phase[s * 2 + c];
     if (wave == 1) {
         /* ------------------------------- helper wave ------------------------------- */
         const double *xp = a.xd + (size_t)g * a.x_pitch;
@@ -605,15 +594,9 @@ __global__ __launch_bounds__(128) void icw_iir_pair(IcwK1Args a)
     if (!valid) return;
     icw_store_hist<N, 0>(R, a.hist, g, a.n_chains);
     a.sncnt[g] += cnt;
-    if (f == 0) {
-        a.info_phase[s * 2 + c] = ph0;
-        a.hq_phase[s * 2 + c] = (ph0 + (unsigned)T) & 3u;
-        if (c == 0) {
-            a.pos[s] += T;
-            const unsigned long long n0 = a.n_frame[s];
-            a.info_nframe[s] = n0;
-            a.n_frame[s] = a.scaled ? (n0 + (unsigned long long)T) % a.ssr : n0 + (unsigned long long)T;
-        }
+    if (f == 0 && c == 0) {   /* the pair kernel does not track converter identity: no shortcut */
+        a.info_dup[s] = 0u;
+        a.lr_equal[s] = 0u;
     }
 }
 
@@ -705,11 +688,12 @@ __device__ __forceinline__ int icw_render_round(double input, const IcwRenderK &
 
 /* modulator frame counter -> norm_omega of frame t of the block (adv_modulator.c:611-625);
  * n0 is the block-start counter (< ssr in scaled mode) */
-__device__ __forceinline__ double icw_omega(unsigned long long n0, int t, int scaled, unsigned long long ssr,
+__device__ __forceinline__ double icw_omega(unsigned long long n0, long long t, int scaled, unsigned long long ssr,
                                             uint32_t sample_rate)
 {
+    /* n0: the counter at the call's start (< ssr when scaled); t: frames since then */
     if (scaled) {
-        const unsigned long long n = (t == 0) ? n0 : (n0 + (unsigned long long)t) % ssr;
+        const unsigned long long n = (n0 + (unsigned long long)t) % ssr;
         return (2.0 * ICW_PI) * ((double)n) / ((double)ssr);
     }
     return (2.0 * ICW_PI) * ((double)(n0 + (unsigned long long)t)) / (double)sample_rate;
@@ -822,7 +806,7 @@ __global__ __launch_bounds__(ICW_K2_TILE) void icw_output(IcwK2Args a)
             double y[4];
             y[0] = icw_iir_out<N, KAHAN>(&lw[0][tl], pc, pd, a.d0);
             y[1] = icw_iir_out<N, KAHAN>(&lw[1][tl], pc, pd, a.d0);
-            if (a.mono_dup && a.mono_dup[s]) {
+            if (a.nch == 1 && a.info_dup && a.info_dup[s] && a.hq_phase[s * 2] == a.hq_phase[s * 2 + 1]) {
                 y[2] = y[0];
                 y[3] = y[1];
             } else {
@@ -835,7 +819,7 @@ __global__ __launch_bounds__(ICW_K2_TILE) void icw_output(IcwK2Args a)
 #pragma unroll
             for (int ch = 0; ch < 2; ++ch) {
                 const double yi = y[ch * 2], yq = y[ch * 2 + 1];
-                const unsigned k = (a.info_phase[s * 2 + ch] + (unsigned)t) & 3u;
+                const unsigned k = (a.hq_phase[s * 2 + ch] + (unsigned)(a.t0 + t)) & 3u;
                 switch (k) {
                 case 0: oI[ch] = yi * 2.0; oQ[ch] = yq * 2.0; break;
                 case 1: oI[ch] = -yq * 2.0; oQ[ch] = yi * 2.0; break;
@@ -853,7 +837,7 @@ __global__ __launch_bounds__(ICW_K2_TILE) void icw_output(IcwK2Args a)
             return;   /* do_render == 0 in this mode: no barrier follows */
         }
 
-        const double omega = icw_omega(a.info_nframe[s], t, a.scaled, a.ssr, a.sample_rate);
+        const double omega = icw_omega(a.n_frame[s], a.t0 + t, a.scaled, a.ssr, a.sample_rate);
 
         /* DSP list (adv_modulator.c:637-751) */
         const IcwProg *P = a.prog;
@@ -951,11 +935,11 @@ __global__ __launch_bounds__(64) void icw_graph_serial(IcwK4Args a)
     double *gb = a.bus + (size_t)s * ICW_N_INPUTS * 4;
     for (int k = 0; k < ICW_N_INPUTS * 4; ++k) bus[k][lane] = gb[k];
     const IcwProg *P = a.prog;
-    const unsigned long long n0 = a.info_nframe[s];
+    const unsigned long long n0 = a.n_frame[s];
     const double *iq = a.iq + (size_t)s * a.T * 4;
     double *pre = a.pre + (size_t)s * a.pre_stride;
     for (int t = 0; t < a.T; ++t) {
-        const double omega = icw_omega(n0, t, a.scaled, a.ssr, a.sample_rate);
+        const double omega = icw_omega(n0, a.t0 + t, a.scaled, a.ssr, a.sample_rate);
         bus[0][lane] = iq[(size_t)t * 4 + 0];
         bus[1][lane] = iq[(size_t)t * 4 + 1];
         bus[2][lane] = iq[(size_t)t * 4 + 2];
@@ -987,19 +971,19 @@ __global__ __launch_bounds__(64) void icw_graph_serial(IcwK4Args a)
     for (int k = 0; k < ICW_N_INPUTS * 4; ++k) gb[k] = bus[k][lane];
 }
 
-/* Block bookkeeping for complex input, where no IIR state kernel runs: the Hilbert phases stay
- * (the converters are not called for CWAVE samples), the reader position and the modulator
- * frame counter advance by T, and the block-start snapshot for the output kernel is taken. */
+/* Call-end bookkeeping: the reader position, the Hilbert phases (not for complex input -- the
+ * converters were not called) and the modulator frame counter advance by the call's frames. */
 __global__ __launch_bounds__(64) void icw_advance(IcwAdvArgs a)
 {
     const int s = blockIdx.x * 64 + threadIdx.x;
     if (s >= a.n_streams) return;
-    a.info_phase[s * 2 + 0] = a.hq_phase[s * 2 + 0];
-    a.info_phase[s * 2 + 1] = a.hq_phase[s * 2 + 1];
-    a.pos[s] += a.T;
+    a.pos[s] += a.n;
+    if (!a.cw) {
+        a.hq_phase[s * 2 + 0] = (a.hq_phase[s * 2 + 0] + (unsigned)a.n) & 3u;
+        a.hq_phase[s * 2 + 1] = (a.hq_phase[s * 2 + 1] + (unsigned)a.n) & 3u;
+    }
     const unsigned long long n0 = a.n_frame[s];
-    a.info_nframe[s] = n0;
-    a.n_frame[s] = a.scaled ? (n0 + (unsigned long long)a.T) % a.ssr : n0 + (unsigned long long)a.T;
+    a.n_frame[s] = a.scaled ? (n0 + (unsigned long long)a.n) % a.ssr : n0 + (unsigned long long)a.n;
 }
 
 /* ------------------------------------------------------ serial render kernel (K3) ------ */

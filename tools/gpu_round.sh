@@ -39,6 +39,11 @@ for s in "$@"; do
       ( cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/gpurun_out/prof_$WL" -o run \
           -- python3 "$R/bench.py" --workload "$WL" --steps 2 --warmup 1 --no-cpu-baseline ) > gpurun_out/prof_$WL.txt 2>&1
       rc=$?; echo "[prof_$WL] rc=$rc" | tee -a gpurun_out/steps.txt; [ $rc -eq 0 ] || exit 2 ;;
+    profser)   # standalone kernel times: every kernel on one stream
+      R=$(pwd); export TMPDIR=/tmp; export ICW_SERIALIZE=1
+      ( cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/gpurun_out/profser_$WL" -o run \
+          -- python3 "$R/bench.py" --workload "$WL" --steps 2 --warmup 1 --no-cpu-baseline ) > gpurun_out/profser_$WL.txt 2>&1
+      rc=$?; unset ICW_SERIALIZE; echo "[profser_$WL] rc=$rc" | tee -a gpurun_out/steps.txt; [ $rc -eq 0 ] || exit 2 ;;
     pmc)
       R=$(pwd); export TMPDIR=/tmp
       ( cd /tmp && timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$R/gpurun_out/pmc_fetch" -o run \
