@@ -74,6 +74,7 @@ struct IcwK1Args {
     uint32_t *lr_equal;            /* [n_streams] left and right converters bit-identical (state) */
     uint32_t *info_dup;            /* [n_streams] lr_equal at this block's start (for K2) */
     int *err;                      /* set by a bounded spin that gave up (never in a healthy run) */
+    int32_t wg_waves;              /* waves per workgroup of the plain / MFMA kernels (1..4) */
     double pc[20];                 /* loop-back coefficients -a[i+1]/a0 */
 };
 
@@ -103,6 +104,7 @@ struct IcwProg {
     int32_t is_bus;
     int32_t n_regs;
     int32_t bypass;                /* am.is_bypass_list: only the Master, on raw `in` */
+    int32_t needs_omega;           /* some Shift / PM node is active: the frame's norm_omega is used */
     int32_t n_persist;             /* slots read before any write in the frame and never written */
     int32_t persist_reg[ICW_MAX_REGS], persist_slot[ICW_MAX_REGS];
     int32_t n_wb;                  /* slots written in the frame: final value -> persistent bus */

@@ -25,6 +25,7 @@
 extern "C" hipError_t icw_launch_unpack(const IcwK0Args *a, hipStream_t st);
 extern "C" hipError_t icw_launch_iir_pair(const IcwK1Args *a, int nord, int kahan, int subn, hipStream_t st);
 extern "C" hipError_t icw_launch_iir_state(const IcwK1Args *a, int nord, int kahan, int subn, hipStream_t st);
+extern "C" hipError_t icw_launch_iir_mfma(const IcwK1Args *a, int nord, int kahan, int subn, hipStream_t st);
 extern "C" hipError_t icw_launch_render(const IcwK3Args *a, hipStream_t st);
 extern "C" hipError_t icw_launch_dither(const IcwK3Args *a, hipStream_t st);
 extern "C" hipError_t icw_launch_dither_lane(const IcwK3Args *a, hipStream_t st);
@@ -45,6 +46,7 @@ double u2d(unsigned long long u)
 
 /* frames per kernel launch: bounds the w scratch buffer (n_chains * (T+N) doubles) */
 constexpr int kMaxBlockFrames = 1 << 16;
+constexpr int kDefBlockFrames = 1 << 14;   /* launch block: shorter pipeline fill / drain */
 
 struct DevState {
     double *hist = nullptr;               /* [chains][20] */
@@ -100,6 +102,8 @@ struct icw_ctx {
     std::vector<CuSplit> splits;          /* cached CU-partitioned stream sets, by K1 CU count */
     bool cu_split = true;                 /* ICW_CU_SPLIT=0 disables the partition */
     int k1_wpc = 4;                       /* ICW_K1_WPC: K1 waves per CU (one per SIMD) */
+    int k1_wg = 1;                        /* ICW_K1_WG: K1 waves per workgroup */
+    int max_block = kDefBlockFrames;      /* ICW_BLOCK: frames per launch block */
     /* dither generation (K3a) runs on its own stream, double-buffered like the block scratch */
     hipStream_t stream3 = nullptr;
     hipEvent_t ditdone[2] = {nullptr, nullptr};
@@ -118,7 +122,7 @@ struct icw_ctx {
     hipStream_t stream = nullptr;
     std::vector<hipEvent_t> ev;
     int n_cu = 256;
-    bool pair_mode = false;   /* chain+helper wave pairs (few chains per SIMD) vs plain lanes */
+    int k1_mode = 0;          /* K1 variant: 0 plain lanes, 1 chain+helper wave pairs, 2 MFMA product feed */
     bool dither_lane = false; /* ICW_DITHER=lane: lane-per-channel dither generator (A/B only) */
     bool serialize = false;   /* ICW_SERIALIZE=1: every kernel on the caller's stream (profiling) */
     double last_ms[2]{};
@@ -234,6 +238,17 @@ void op_params(const icw_node &n, IcwOp &op)
     }
 }
 
+/* norm_omega is only read by active Shift / PM nodes (adv_modulator.c:519-583): frame-parallel
+ * kernels skip the counter arithmetic and its division otherwise */
+void set_needs_omega(IcwProg &P)
+{
+    P.needs_omega = 0;
+    for (int i = 0; i < P.n_ops; ++i) {
+        const IcwOp &op = P.ops[i];
+        if ((op.mode == ICW_MODE_SHIFT || op.mode == ICW_MODE_PM) && (op.act[0] || op.act[1])) P.needs_omega = 1;
+    }
+}
+
 /* Bus form: the list as the reference runs it (tail -> head, or the head alone when bypassed) */
 int compile_bus(const std::vector<icw_node> &nodes, int bypass, IcwProg &P)
 {
@@ -251,6 +266,7 @@ int compile_bus(const std::vector<icw_node> &nodes, int bypass, IcwProg &P)
     }
     P.n_ops = (int)order.size();
     P.n_regs = 1;
+    set_needs_omega(P);
     return ICW_OK;
 }
 
@@ -306,6 +322,7 @@ int compile_graph(const std::vector<icw_node> &nodes, int bypass, IcwProg &P)
     }
     P.n_ops = (int)order.size();
     P.n_regs = n_regs;
+    set_needs_omega(P);
     for (int k = 0; k < ICW_N_INPUTS; ++k)
         if (written_any[k] && cur[k] >= 0) {
             P.wb_reg[P.n_wb] = cur[k];
@@ -541,10 +558,12 @@ int icw_create(const icw_config *cfg, const icw_node *nodes, int n_nodes, int n_
         const long wgs = ((long)S * 4 + 63) / 64;
         /* measured (profiles/r01_*): the pair kernel's hand-off protocol still costs more than the
          * instructions it removes from the chain wave, so the plain kernel is the default */
-        c->pair_mode = false && wgs <= c->n_cu;
+        (void)wgs;
+        c->k1_mode = 0;
         const char *m = getenv("ICW_K1_MODE");
-        if (m && !strcmp(m, "plain")) c->pair_mode = false;
-        if (m && !strcmp(m, "pair")) c->pair_mode = true;
+        if (m && !strcmp(m, "plain")) c->k1_mode = 0;
+        if (m && !strcmp(m, "pair")) c->k1_mode = 1;
+        if (m && !strcmp(m, "mfma")) c->k1_mode = 2;
         const char *d = getenv("ICW_DITHER");
         c->dither_lane = d && !strcmp(d, "lane");
         const char *z = getenv("ICW_SERIALIZE");
@@ -553,6 +572,10 @@ int icw_create(const icw_config *cfg, const icw_node *nodes, int n_nodes, int n_
         if (cs && !strcmp(cs, "0")) c->cu_split = false;
         const char *wpc = getenv("ICW_K1_WPC");
         if (wpc && atoi(wpc) >= 1 && atoi(wpc) <= 8) c->k1_wpc = atoi(wpc);
+        const char *bl = getenv("ICW_BLOCK");
+        if (bl && atoi(bl) >= 256 && atoi(bl) <= kMaxBlockFrames) c->max_block = atoi(bl);
+        const char *wg = getenv("ICW_K1_WG");
+        if (wg && atoi(wg) >= 1 && atoi(wg) <= 4) c->k1_wg = atoi(wg);
     }
     rc = icw_stream_init(c, 0, n_streams);
     if (rc) { free_all(c); delete c; return rc; }
@@ -741,7 +764,7 @@ int icw_process_streams(icw_ctx *c, int first, int count, const void *in, size_t
     }
 
     const int N = c->nord;
-    const int Tb = std::min(n_frames, kMaxBlockFrames);
+    const int Tb = std::min(n_frames, c->max_block);
     const size_t w_pitch = (size_t)Tb + N + 1;
     const size_t x_pitch = ((size_t)Tb + ICW_MAX_IIR_ORDER + 2) & ~(size_t)1;   /* look-ahead pad */
     const int n_blocks = (n_frames + Tb - 1) / Tb;
@@ -847,10 +870,12 @@ int icw_process_streams(icw_ctx *c, int first, int count, const void *in, size_t
             a1.lr_equal = ds.lr_equal + f0;
             a1.info_dup = c->info_dup[p];
             memcpy(a1.pc, c->pc, sizeof(a1.pc));
+            a1.wg_waves = c->k1_wg;
             /* K0(b) done; it came after K2(b-2) on sA, the last reader of w[p] / info_dup[p] */
             if (sK != sA && hipStreamWaitEvent(sK, c->k0done[p], 0) != hipSuccess) return ICW_EDEVICE;
             if (timing) hipEventRecord(c->ev[4 * b], sK);
-            const hipError_t e1 = c->pair_mode ? icw_launch_iir_pair(&a1, N, cfg.iir_kahan, cfg.iir_subnorm_reject, sK)
+            const hipError_t e1 = c->k1_mode == 2 ? icw_launch_iir_mfma(&a1, N, cfg.iir_kahan, cfg.iir_subnorm_reject, sK)
+                                : c->k1_mode == 1 ? icw_launch_iir_pair(&a1, N, cfg.iir_kahan, cfg.iir_subnorm_reject, sK)
                                                : icw_launch_iir_state(&a1, N, cfg.iir_kahan, cfg.iir_subnorm_reject, sK);
             if (e1 != hipSuccess) return ICW_EDEVICE;
             if (timing) hipEventRecord(c->ev[4 * b + 1], sK);

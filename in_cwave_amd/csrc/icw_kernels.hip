@@ -5,17 +5,14 @@
  * the operand order of the reference so that results are bit-identical to the x86 SSE2 build
  * of in_cwave (IEEE binary64, round-to-nearest, no FMA contraction, denormals preserved).
  *
- * Kernel roles (DESIGN.md "Kernels"):
- *   icw_iir_state   one lane per DF-II chain (stream x channel x {I,Q} filter).  Runs the
- *                   serial part of iir_rp_process_kahan (hblpf.c:1017-1054) -- the loop-back
- *                   Kahan sum that produces the delay-line value w[n] -- with the delay line held
- *                   in VGPRs as a compile-time-rotated ring (unrolled by the filter order N).
- *                   Writes w[] per chain to HBM.  This is the latency-bound critical path.
+ * Kernel roles (DESIGN.md "Kernels"; the serial IIR recurrence K1 lives in icw_iir.hip):
+ *   icw_unpack_frames  K0: unpack + fade + the quadrature mix into per-chain filter inputs.
  *   icw_output      one thread per frame.  Everything that is NOT on the recurrence: the output
  *                   Kahan sum y[n] = sum d_i z_i + d0*c_i z_i (hblpf.c:1029-1043) from the w
  *                   window (frame-parallel), the fs/4 un-mix (lpf_hilbert_quad.c:129-156), the
  *                   DSP graph (adv_modulator.c:637-751) and the elementwise render
  *                   (sound_render.c:691-809, ROUND/flat).  Coalesced tile loads via LDS.
+ *   icw_graph_serial / icw_dither_coop / icw_render_serial   K4 / K3a / K3b (serial forms).
  */
 #include <hip/hip_runtime.h>
 #include <math.h>
@@ -25,14 +22,6 @@
 #include "icw_device.h"
 
 #pragma clang fp contract(off)
-
-/* diagnostic build only (tools/k1_probe.hip): s_memtime stamps of workgroup 0, lane 0 */
-#ifdef ICW_STAMPS
-__device__ unsigned long long icw_stamps[8][1024];
-#define ICW_STAMP(k, n) do { if (blockIdx.x == 0 && lane == 0 && (n) < 1024) icw_stamps[k][n] = __builtin_amdgcn_s_memtime(); } while (0)
-#else
-#define ICW_STAMP(k, n) do { } while (0)
-#endif
 
 #define ICW_PI (3.1415926535897932384626433832795029)
 #define ICW_SQRT2 (1.4142135623730950488016887242097)
@@ -112,96 +101,6 @@ __device__ __forceinline__ double icw_filter_in(double x, unsigned kq)
     return kq == 0 ? x : (kq == 2 ? -x : 0.0);
 }
 
-/* ------------------------------------------------------------ IIR state kernel (K1) ----- */
-/* One unrolled step of the loop-back sum for sample J of an N-block.  The delay line lives in
- * R[]: at step J the logical z_i (i = 0 most recent) is R[(J-1-i) mod N]; the new w is written
- * to R[J], overwriting the oldest value.  All indices are compile-time constants. */
-template <int N, bool KAHAN, bool SUBN, int J>
-__device__ __forceinline__ void icw_iir_step(double (&R)[N], double xin, const double (&pc)[20],
-                                             unsigned &cnt)
-{
-    double S;
-    if (KAHAN) {
-        /* kahan_init(sample); i = 0 term first (hblpf.c:1017-1027) then i = 1..N-1 */
-        double t0 = R[(J - 1 + N) % N] * pc[0];
-        double C = 0.0, Y, T;
-        S = xin;
-        Y = t0 - C; T = S + Y; C = (T - S) - Y; S = T;
-#pragma unroll
-        for (int i = 1; i < N; ++i) {
-            double ti = R[(J - 1 - i + 2 * N) % N] * pc[i];
-            Y = ti - C; T = S + Y; C = (T - S) - Y; S = T;
-        }
-    } else {
-        /* baseline: sum_i = sample; sum_i += z_k * c_i (hblpf.c:898-913) */
-        S = xin;
-#pragma unroll
-        for (int i = 0; i < N; ++i) S += R[(J - 1 - i + 2 * N) % N] * pc[i];
-    }
-    if (SUBN) {
-        /* fabs(sum) < is_subnorm_reject, a BOOL == 1 -> threshold 1.0 (hblpf.c:915, 1046) */
-        const bool z = fabs(S) < 1.0;
-        cnt += z ? 1u : 0u;
-        S = z ? 0.0 : S;
-    }
-    R[J] = S;
-}
-
-
-template <int N, int J>
-__device__ __forceinline__ void icw_store_hist(const double (&R)[N], double *hist, int g, int n_chains)
-{
-    /* after J steps of a block, logical z_i = R[(J-1-i) mod N] */
-#pragma unroll
-    for (int i = 0; i < N; ++i) hist[(size_t)g * ICW_HIST_PITCH + i] = R[(J - 1 - i + 2 * N) % N];
-}
-
-/* R[k] <- R[k+1 mod N]: one static rotation of the ring (moves only) */
-template <int N>
-__device__ __forceinline__ void icw_rotate1(double (&R)[N])
-{
-    const double r0 = R[0];
-#pragma unroll
-    for (int k = 0; k < N - 1; ++k) R[k] = R[k + 1];
-    R[N - 1] = r0;
-}
-
-/* After `rem` (< N) steps the logical order is R[(rem-1-i) mod N].  Rotating left by rem
- * restores the block-start mapping R[(N-1-i)] without any runtime-indexed register access
- * (which the compiler would otherwise demote to scratch). */
-template <int N>
-__device__ __forceinline__ void icw_normalise_ring(double (&R)[N], int rem)
-{
-#pragma unroll
-    for (int k = 1; k < N; ++k)
-        if (k <= rem) icw_rotate1<N>(R);
-}
-
-template <int N, int J0, bool KAHAN, bool SUBN>
-__device__ __forceinline__ void icw_block_steps(double (&R)[N], const double (&xv)[N],
-                                                const double (&pc)[20], unsigned &cnt, int lim)
-{
-    if constexpr (J0 < N) {
-        if (J0 < lim) {
-            icw_iir_step<N, KAHAN, SUBN, J0>(R, xv[J0], pc, cnt);
-            icw_block_steps<N, J0 + 1, KAHAN, SUBN>(R, xv, pc, cnt, lim);
-        }
-    }
-}
-
-/* full block of N steps; after step J consumes xv[J], refill it with the input N samples ahead
- * (rows are padded by >= N doubles, so the last block's look-ahead loads stay in bounds) */
-template <int N, int J0, bool KAHAN, bool SUBN>
-__device__ __forceinline__ void icw_block_steps_pf(double (&R)[N], double (&xv)[N], const double *xnext,
-                                                   const double (&pc)[20], unsigned &cnt)
-{
-    if constexpr (J0 < N) {
-        icw_iir_step<N, KAHAN, SUBN, J0>(R, xv[J0], pc, cnt);
-        xv[J0] = xnext[J0];
-        icw_block_steps_pf<N, J0 + 1, KAHAN, SUBN>(R, xv, xnext, pc, cnt);
-    }
-}
-
 /* Input prep (K0): unpack + fade each frame once (xwave_unpack_csample, xwave_reader.c:908-1001)
  * and lay out every DF-II chain's own input sequence: the quadrature mix of hq_rp_process
  * (lpf_hilbert_quad.c:129-156) feeds the I filter {x, +0, -x, +0} and the Q filter {+0, -x, +0, x}
@@ -249,356 +148,6 @@ __global__ __launch_bounds__(256) void icw_unpack_frames(IcwK0Args a)
     }
 }
 
-template <int N>
-__device__ __forceinline__ void icw_load_x(double (&xv)[N], const double *xp)
-{
-#pragma unroll
-    for (int j = 0; j < N; ++j) xv[j] = xp[j];
-}
-
-template <int N, bool KAHAN, bool SUBN>
-__global__ __launch_bounds__(64) void icw_iir_state(IcwK1Args a)
-{
-    const int g = blockIdx.x * 64 + threadIdx.x;
-    if (g >= a.n_chains) return;
-    const int s = g >> 2, c = (g >> 1) & 1, f = g & 1;
-    const int n_chains = a.n_chains;
-    double pc[20];
-#pragma unroll
-    for (int i = 0; i < 20; ++i) pc[i] = a.pc[i];
-
-    double R[N];
-#pragma unroll
-    for (int i = 0; i < N; ++i) R[N - 1 - i] = a.hist[(size_t)g * ICW_HIST_PITCH + i];
-
-    if (f == 0 && c == 0) a.info_dup[s] = a.lr_equal[s];     /* this block's start (for K2) */
-    const double *xp = a.xd + (size_t)g * a.x_pitch;
-    double *wrow = a.w + (size_t)g * a.w_pitch;
-    /* history rows [0, N): row j = z_{N-1-j} = R[j] */
-#pragma unroll
-    for (int j = 0; j < N; ++j) wrow[j] = R[j];
-
-    const int T = a.T;
-    unsigned cnt = 0;
-    int t = 0;
-    if (T >= N) {
-        /* xv[j] holds the input of step j of the current block; right after a step consumes it the
-         * same register is refilled with the next block's input, so loads run N samples ahead
-         * with no register copies */
-        double xv[N];
-        icw_load_x<N>(xv, xp);
-        for (; t + N <= T; t += N) {
-            icw_block_steps_pf<N, 0, KAHAN, SUBN>(R, xv, xp + t + N, pc, cnt);
-            double *wo = wrow + N + t;
-#pragma unroll
-            for (int j = 0; j < N; ++j) wo[j] = R[j];
-        }
-    }
-    const int rem = T - t;
-    if (rem > 0) {
-        double xv[N];
-#pragma unroll
-        for (int j = 0; j < N; ++j) xv[j] = (j < rem) ? xp[t + j] : 0.0;
-        icw_block_steps<N, 0, KAHAN, SUBN>(R, xv, pc, cnt, rem);
-        double *wo = wrow + N + t;
-#pragma unroll
-        for (int j = 0; j < N; ++j)
-            if (j < rem) wo[j] = R[j];
-        icw_normalise_ring<N>(R, rem);
-    }
-    icw_store_hist<N, 0>(R, a.hist, g, n_chains);
-    a.sncnt[g] += cnt;
-    /* are the stream's right converters still bit-identical to its left ones?  The 4 chains of a
-     * stream are lanes 4k..4k+3 of this wave; lane ^ 2 is the same filter of the other channel */
-    bool eq = true;
-#pragma unroll
-    for (int i = 0; i < N; ++i) {
-        const double o = __shfl_xor(R[i], 2);
-        eq = eq && (__double_as_longlong(o) == __double_as_longlong(R[i]));
-    }
-    const bool eq_q = __shfl_xor((int)eq, 1) != 0;
-    if (f == 0 && c == 0) a.lr_equal[s] = (eq && eq_q) ? 1u : 0u;
-}
-
-/* ---------------------------------------- IIR state kernel, chain+helper wave pair (K1p) ---- */
-/* Latency/issue-bound regime (few chains per SIMD, e.g. BASELINE C2: 1024 chains on 1024 SIMDs).
- * A single wave issues ~1 FP64 instruction per ~4.7 cycles whether or not the instructions depend
- * on each other (tools/lat_probe), so a chain's time per sample is its instruction count.  The
- * workgroup pairs a CHAIN wave with a HELPER wave on another SIMD:
- *   chain : the loop-back Kahan sum (hblpf.c:1017-1046) -- the 4 products that depend on the
- *           newest / oldest states, the 73 dependent adds, the subnorm reject -- and nothing else;
- *   helper: every other product w[m]*c_i (i in [3, N-KT)), the Hilbert input selection, and the
- *           store of w[] to HBM; it publishes them through an LDS ring indexed by target sample.
- * Hand-off: the chain writes w[n] to wring and bumps chain_done; the helper bumps help_done once
- * w[m]'s products are in LDS.  Slot n needs help_done >= n-3; the chain checks the slot of sample
- * n+1 in the middle of sample n and prefetches it in two halves (after the entries are consumed),
- * so LDS latency is off the critical path and the helper has ~2 samples of slack. */
-template <int N>
-struct IcwPair {
-    static constexpr int KT = (N >= 20) ? 2 : 1;   /* oldest products computed by the chain */
-    static constexpr int RING = N - KT;            /* product slots, indexed by target % RING */
-    static constexpr int NH = N - KT - 3;          /* helper products i in [3, N-KT) */
-    static constexpr int NE = NH + 1;              /* + the filter input x_in (entry 0) */
-    static constexpr int WR = 8;                   /* w hand-off ring */
-    static constexpr int HALF = 7;                 /* entries [0,HALF) prefetched mid-sample */
-    static constexpr int IMID = 3 + HALF - 1;      /* steps i < IMID consume entries < HALF */
-};
-
-__device__ __forceinline__ int icw_lds_ld(const int *p)
-{
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-/* blocking LDS poll issued by hand: the compiler's own atomic-load lowering placed a
- * vector-memory drain (s_waitcnt vmcnt(0)) at every poll-loop header, which would wait for the
- * helper's HBM prefetches each sample */
-__device__ __forceinline__ int icw_poll(unsigned off)
-{
-    int v;
-    asm volatile("ds_read_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(off));
-    return __builtin_amdgcn_readfirstlane(v);
-}
-__device__ __forceinline__ void icw_lds_st(int *p, int v)
-{
-    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-
-template <int N, int J, int I>
-__device__ __forceinline__ double icw_pair_prod(const double (&R)[N], const double (&pf)[IcwPair<N>::NE],
-                                                const double (&pc)[20])
-{
-    using P = IcwPair<N>;
-    if constexpr (I < 3 || I >= N - P::KT) return R[(J - 1 - I + 2 * N) % N] * pc[I];
-    else return pf[1 + I - 3];
-}
-
-template <int N, bool KAHAN, int J, int I>
-__device__ __forceinline__ void icw_pair_sum(double &S, double &C, const double (&R)[N],
-                                             const double (&pf)[IcwPair<N>::NE], const double (&pc)[20], int I1)
-{
-    if constexpr (I < N) {
-        if (I < I1) {
-            const double t = icw_pair_prod<N, J, I>(R, pf, pc);
-            if (KAHAN) {
-                const double Y = t - C;
-                const double T = S + Y;
-                C = (T - S) - Y;
-                S = T;
-            } else {
-                S += t;
-            }
-            icw_pair_sum<N, KAHAN, J, I + 1>(S, C, R, pf, pc, I1);
-        }
-    }
-}
-
-/* steps i in [I0, N) starting at template index I0 */
-template <int N, bool KAHAN, int J, int I0>
-__device__ __forceinline__ void icw_pair_range(double &S, double &C, const double (&R)[N],
-                                               const double (&pf)[IcwPair<N>::NE], const double (&pc)[20], int I1)
-{
-    icw_pair_sum<N, KAHAN, J, I0>(S, C, R, pf, pc, I1);
-}
-
-struct IcwPairLds;   /* layout documented in icw_iir_pair */
-
-template <int N, bool KAHAN, bool SUBN, int J>
-__device__ __forceinline__ void icw_pair_sample(double (&R)[N], double (&pf)[IcwPair<N>::NE], const double (&pc)[20],
-                                                unsigned &cnt, const int n, double *prod, double *wring,
-                                                int *chain_done, const int *help_done, const int lane, int *err,
-                                                const unsigned hd_off)
-{
-    using P = IcwPair<N>;
-    /* The poll of help_done is issued by hand at the start of the sample and waited for by hand
-     * in the middle, so its LDS latency hides under the first half of the Kahan chain.  (A plain
-     * load would be sunk by the compiler to its use, with the first half of the sum moved below
-     * the check -- an exposed LDS round trip every sample.)  Extra hand-issued LDS ops only make
-     * the compiler's in-order lgkmcnt waits stronger, never weaker. */
-    int pv;
-    double S = pf[0], C = 0.0;
-    ICW_STAMP(0, n);
-    asm volatile("ds_read_b32 %0, %2" : "=v"(pv), "+v"(S) : "v"(hd_off));
-    icw_pair_range<N, KAHAN, J, 0>(S, C, R, pf, pc, P::IMID);
-    asm volatile("" : "+v"(S), "+v"(C));                       /* first half stays above the check */
-    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(pv) : : "memory");
-    /* mid-sample: slot n+1 must be complete (help_done >= n-2), then prefetch its first half
-     * (x_in and products 3..IMID-1, whose registers were just consumed) */
-    pv = __builtin_amdgcn_readfirstlane(pv);
-    for (int spin = 0; pv < n - 2; ++spin) {          /* bounded: a broken hand-off ends the kernel */
-        if (spin > (1 << 22)) { *err = 1; break; }
-        __builtin_amdgcn_s_sleep(1);
-        pv = icw_poll(hd_off);
-    }
-    ICW_STAMP(1, n);
-    const double *slot = prod + (size_t)((n + 1) % P::RING) * P::NE * 64 + lane;
-#pragma unroll
-    for (int e = 0; e < P::HALF; ++e) pf[e] = slot[e * 64];
-    icw_pair_range<N, KAHAN, J, P::IMID>(S, C, R, pf, pc, N);
-    asm volatile("" : "+v"(S));                                 /* second half above its refill */
-#pragma unroll
-    for (int e = P::HALF; e < P::NE; ++e) pf[e] = slot[e * 64];
-    if (SUBN) {
-        const bool z = fabs(S) < 1.0;
-        cnt += z ? 1u : 0u;
-        S = z ? 0.0 : S;
-    }
-    R[J] = S;
-    /* publish w[n]: LDS operations of one wave are performed in order, so the counter store
-     * cannot overtake the data store; the asm barrier keeps the compiler from reordering them */
-    wring[(n % P::WR) * 64 + lane] = S;
-    __atomic_signal_fence(__ATOMIC_SEQ_CST);
-    if (lane == 0) icw_lds_st(chain_done, n + 1);
-    ICW_STAMP(2, n);
-}
-
-template <int N, bool KAHAN, bool SUBN, int J0>
-__device__ __forceinline__ void icw_pair_block(double (&R)[N], double (&pf)[IcwPair<N>::NE], const double (&pc)[20],
-                                               unsigned &cnt, const int n0, const int lim, double *prod, double *wring,
-                                               int *chain_done, const int *help_done, const int lane, int *err,
-                                               const unsigned hd_off)
-{
-    if constexpr (J0 < N) {
-        if (J0 < lim) {
-            icw_pair_sample<N, KAHAN, SUBN, J0>(R, pf, pc, cnt, n0 + J0, prod, wring, chain_done, help_done, lane, err,
-                                                hd_off);
-            icw_pair_block<N, KAHAN, SUBN, J0 + 1>(R, pf, pc, cnt, n0, lim, prod, wring, chain_done, help_done, lane,
-                                                   err, hd_off);
-        }
-    }
-}
-
-template <int N, bool KAHAN, bool SUBN>
-__global__ __launch_bounds__(128) void icw_iir_pair(IcwK1Args a)
-{
-    using P = IcwPair<N>;
-    __shared__ double prod[P::RING * P::NE * 64];   /* [slot][entry][lane] */
-    __shared__ double wring[P::WR * 64];             /* [n % WR][lane] */
-    __shared__ int counters[2];                       /* chain_done, help_done */
-    int *chain_done = &counters[0];
-    int *help_done = &counters[1];
-
-    const int lane = threadIdx.x & 63;
-    const int wave = threadIdx.x >> 6;
-    const int g0 = blockIdx.x * 64 + lane;
-    const bool valid = g0 < a.n_chains;
-    const int g = valid ? g0 : a.n_chains - 1;
-    const int s = g >> 2, c = (g >> 1) & 1, f = g & 1;
-    const int T = a.T;
-    double pc[20];
-#pragma unroll
-    for (int i = 0; i < 20; ++i) pc[i] = a.pc[i];
-    if (threadIdx.x == 0) {
-        icw_lds_st(chain_done, 0);
-        icw_lds_st(help_done, -0x40000000);
-    }
-    __syncthreads();
-
-    if (wave == 1) {
-        /* ------------------------------- helper wave ------------------------------- */
-        const double *xp = a.xd + (size_t)g * a.x_pitch;
-        double *wrow = a.w + (size_t)g * a.w_pitch;
-        double z[N];   /* z[k] = w[-1-k] (history, most recent first) */
-#pragma unroll
-        for (int k = 0; k < N; ++k) z[k] = a.hist[(size_t)g * ICW_HIST_PITCH + k];
-        if (valid) {
-#pragma unroll
-            for (int j = 0; j < N; ++j) wrow[j] = z[N - 1 - j];
-        }
-        /* prefill: products of history w[m] (m = -1-k) for targets n = m+1+i = i-k >= 0 */
-#pragma unroll
-        for (int k = 0; k < N; ++k)
-#pragma unroll
-            for (int i = 3; i < N - P::KT; ++i) {
-                const int n = i - k;
-                if (n >= 0 && n < T) prod[((size_t)(n % P::RING) * P::NE + 1 + i - 3) * 64 + lane] = z[k] * pc[i];
-            }
-#pragma unroll
-        for (int n = 0; n < 4; ++n)
-            if (n < T) prod[((size_t)(n % P::RING) * P::NE) * 64 + lane] = xp[n];
-        __atomic_signal_fence(__ATOMIC_SEQ_CST);
-        if (lane == 0) icw_lds_st(help_done, 0);
-
-        /* All HBM traffic of the helper happens at 16-sample group boundaries (filter inputs
-         * read a group ahead into registers, the group's w[] written back as one 128-B run per
-         * lane), and the per-sample hand-off is branch-free apart from the poll, so the loop
-         * carries no vector-memory waits.  Products for targets >= T land in ring slots whose
-         * previous targets are already consumed, so they are written unconditionally. */
-        constexpr int U = 16;
-        double xa[U], xb[U], wg[U];
-#pragma unroll
-        for (int u = 0; u < U; ++u) xa[u] = (4 + u < T) ? xp[4 + u] : 0.0;
-#pragma unroll
-        for (int u = 0; u < U; ++u) xb[u] = (U + 4 + u < T) ? xp[U + 4 + u] : 0.0;
-        int cd = 0;
-        const unsigned cd_off = (unsigned)(uintptr_t)chain_done;
-        for (int m0 = 0; m0 < T; m0 += U) {
-            const int ulim = min(U, T - m0);
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                const int m = m0 + u;
-                if (u < ulim) {
-                    for (int spin = 0; cd < m + 1; ++spin) {
-                        if (spin > (1 << 24)) { *a.err = 2; return; }
-                        cd = icw_poll(cd_off);
-                    }
-                    ICW_STAMP(3, m);
-                    const double w = wring[(m % P::WR) * 64 + lane];
-                    wg[u] = w;
-                    const int sb = (m + 4) % P::RING;   /* slot of target m+1+i for i = 3 */
-                    double *pb = prod + lane;
-#pragma unroll
-                    for (int i = 3; i < N - P::KT; ++i) {
-                        int sl = sb + (i - 3);
-                        sl = sl >= P::RING ? sl - P::RING : sl;
-                        pb[((size_t)sl * P::NE + 1 + i - 3) * 64] = w * pc[i];
-                    }
-                    pb[((size_t)sb * P::NE) * 64] = xa[u];
-                    __atomic_signal_fence(__ATOMIC_SEQ_CST);
-                    if (lane == 0) icw_lds_st(help_done, m + 1);
-                    ICW_STAMP(4, m);
-                }
-            }
-            if (valid) {
-#pragma unroll
-                for (int u = 0; u < U; ++u)
-                    if (u < ulim) wrow[N + m0 + u] = wg[u];
-            }
-#pragma unroll
-            for (int u = 0; u < U; ++u) xa[u] = xb[u];
-#pragma unroll
-            for (int u = 0; u < U; ++u) xb[u] = (m0 + 2 * U + 4 + u < T) ? xp[m0 + 2 * U + 4 + u] : 0.0;
-        }
-        return;
-    }
-
-    /* ---------------------------------- chain wave ---------------------------------- */
-    double R[N];
-#pragma unroll
-    for (int i = 0; i < N; ++i) R[N - 1 - i] = a.hist[(size_t)g * ICW_HIST_PITCH + i];
-    for (int spin = 0; __builtin_amdgcn_readfirstlane(icw_lds_ld(help_done)) < 0; ++spin) {
-        if (spin > (1 << 22)) { *a.err = 3; break; }
-        __builtin_amdgcn_s_sleep(1);
-    }
-    double pf[P::NE];
-#pragma unroll
-    for (int e = 0; e < P::NE; ++e) pf[e] = prod[(size_t)e * 64 + lane];
-    const unsigned hd_off = (unsigned)(uintptr_t)help_done;   /* LDS byte offset (flat low bits) */
-    unsigned cnt = 0;
-    int t = 0;
-    for (; t + N <= T; t += N)
-        icw_pair_block<N, KAHAN, SUBN, 0>(R, pf, pc, cnt, t, N, prod, wring, chain_done, help_done, lane, a.err, hd_off);
-    const int rem = T - t;
-    if (rem > 0) {
-        icw_pair_block<N, KAHAN, SUBN, 0>(R, pf, pc, cnt, t, rem, prod, wring, chain_done, help_done, lane, a.err, hd_off);
-        icw_normalise_ring<N>(R, rem);
-    }
-    if (!valid) return;
-    icw_store_hist<N, 0>(R, a.hist, g, a.n_chains);
-    a.sncnt[g] += cnt;
-    if (f == 0 && c == 0) {   /* the pair kernel does not track converter identity: no shortcut */
-        a.info_dup[s] = 0u;
-        a.lr_equal[s] = 0u;
-    }
-}
 
 /* ------------------------------------------------------------- output kernel (K2) ------- */
 struct IcwLR { double lre, lim, rre, rim; };
@@ -693,7 +242,10 @@ __device__ __forceinline__ double icw_omega(unsigned long long n0, long long t, 
 {
     /* n0: the counter at the call's start (< ssr when scaled); t: frames since then */
     if (scaled) {
-        const unsigned long long n = (n0 + (unsigned long long)t) % ssr;
+        /* (n0 + t) mod ssr; n0 < ssr, so one subtraction covers any call shorter than ssr frames
+         * (1000 s of audio) -- the 64-bit remainder is the rare path */
+        unsigned long long n = n0 + (unsigned long long)t;
+        if (n >= ssr) n = (n - ssr < ssr) ? n - ssr : n % ssr;
         return (2.0 * ICW_PI) * ((double)n) / ((double)ssr);
     }
     return (2.0 * ICW_PI) * ((double)(n0 + (unsigned long long)t)) / (double)sample_rate;
@@ -778,11 +330,14 @@ __global__ __launch_bounds__(ICW_K2_TILE) void icw_output(IcwK2Args a)
     const int t = t0 + tl;
     const int T = a.T;
 
+    /* mono input, converters bit-identical at block start (K1's flag) and in phase: the right
+     * filter outputs are copies of the left ones this block */
+    const bool dup = !a.cw && a.nch == 1 && a.info_dup && a.info_dup[s] && a.hq_phase[s * 2] == a.hq_phase[s * 2 + 1];
     if (!a.cw) {
-        /* stage the w windows of the stream's 4 chains: rows [t0, t0+nrow) */
+        /* stage the w windows of the stream's chains (2 when dup): rows [t0, t0+nrow) */
         const int nrow = min(ICW_K2_TILE, T - t0) + N + (KAHAN ? 0 : 1);
-#pragma unroll
-        for (int c = 0; c < 4; ++c) {
+        const int nc = dup ? 2 : 4;
+        for (int c = 0; c < nc; ++c) {
             const double *src = a.w + (size_t)(s * 4 + c) * a.w_pitch + t0;
             for (int r = tl; r < nrow; r += ICW_K2_TILE) lw[c][r] = src[r];
         }
@@ -806,7 +361,7 @@ __global__ __launch_bounds__(ICW_K2_TILE) void icw_output(IcwK2Args a)
             double y[4];
             y[0] = icw_iir_out<N, KAHAN>(&lw[0][tl], pc, pd, a.d0);
             y[1] = icw_iir_out<N, KAHAN>(&lw[1][tl], pc, pd, a.d0);
-            if (a.nch == 1 && a.info_dup && a.info_dup[s] && a.hq_phase[s * 2] == a.hq_phase[s * 2 + 1]) {
+            if (dup) {
                 y[2] = y[0];
                 y[3] = y[1];
             } else {
@@ -837,10 +392,9 @@ __global__ __launch_bounds__(ICW_K2_TILE) void icw_output(IcwK2Args a)
             return;   /* do_render == 0 in this mode: no barrier follows */
         }
 
-        const double omega = icw_omega(a.n_frame[s], a.t0 + t, a.scaled, a.ssr, a.sample_rate);
-
         /* DSP list (adv_modulator.c:637-751) */
         const IcwProg *P = a.prog;
+        const double omega = P->needs_omega ? icw_omega(a.n_frame[s], a.t0 + t, a.scaled, a.ssr, a.sample_rate) : 0.0;
         IcwRegFile R;
         R.base = lregs + tl;
         R.set(0, in);
@@ -939,7 +493,7 @@ __global__ __launch_bounds__(64) void icw_graph_serial(IcwK4Args a)
     const double *iq = a.iq + (size_t)s * a.T * 4;
     double *pre = a.pre + (size_t)s * a.pre_stride;
     for (int t = 0; t < a.T; ++t) {
-        const double omega = icw_omega(n0, a.t0 + t, a.scaled, a.ssr, a.sample_rate);
+        const double omega = P->needs_omega ? icw_omega(n0, a.t0 + t, a.scaled, a.ssr, a.sample_rate) : 0.0;
         bus[0][lane] = iq[(size_t)t * 4 + 0];
         bus[1][lane] = iq[(size_t)t * 4 + 1];
         bus[2][lane] = iq[(size_t)t * 4 + 2];
@@ -1511,63 +1065,11 @@ __global__ __launch_bounds__(64) void icw_render_serial(IcwK3Args a)
 }
 
 /* ---------------------------------------------------------------- launch wrappers ------- */
-template <int N, bool K, bool S>
-static hipError_t launch_k1_t(const IcwK1Args &a, hipStream_t st)
-{
-    const int blocks = (a.n_chains + 63) / 64;
-    hipLaunchKernelGGL((icw_iir_state<N, K, S>), dim3(blocks), dim3(64), 0, st, a);
-    return hipGetLastError();
-}
-
-template <int N, bool K, bool S>
-static hipError_t launch_k1p_t(const IcwK1Args &a, hipStream_t st)
-{
-    const int blocks = (a.n_chains + 63) / 64;
-    hipLaunchKernelGGL((icw_iir_pair<N, K, S>), dim3(blocks), dim3(128), 0, st, a);
-    return hipGetLastError();
-}
-
-template <int N>
-static hipError_t launch_k1p_n(const IcwK1Args &a, bool kahan, bool subn, hipStream_t st)
-{
-    if (kahan) return subn ? launch_k1p_t<N, true, true>(a, st) : launch_k1p_t<N, true, false>(a, st);
-    return subn ? launch_k1p_t<N, false, true>(a, st) : launch_k1p_t<N, false, false>(a, st);
-}
-
-extern "C" hipError_t icw_launch_iir_pair(const IcwK1Args *a, int nord, int kahan, int subn, hipStream_t st)
-{
-    switch (nord) {
-    case 15: return launch_k1p_n<15>(*a, kahan, subn, st);
-    case 18: return launch_k1p_n<18>(*a, kahan, subn, st);
-    case 19: return launch_k1p_n<19>(*a, kahan, subn, st);
-    case 20: return launch_k1p_n<20>(*a, kahan, subn, st);
-    }
-    return hipErrorInvalidValue;
-}
-
-template <int N>
-static hipError_t launch_k1_n(const IcwK1Args &a, bool kahan, bool subn, hipStream_t st)
-{
-    if (kahan) return subn ? launch_k1_t<N, true, true>(a, st) : launch_k1_t<N, true, false>(a, st);
-    return subn ? launch_k1_t<N, false, true>(a, st) : launch_k1_t<N, false, false>(a, st);
-}
-
 extern "C" hipError_t icw_launch_unpack(const IcwK0Args *a, hipStream_t st)
 {
     dim3 grid((a->T + 255) / 256, a->n_streams);
     hipLaunchKernelGGL(icw_unpack_frames, grid, dim3(256), 0, st, *a);
     return hipGetLastError();
-}
-
-extern "C" hipError_t icw_launch_iir_state(const IcwK1Args *a, int nord, int kahan, int subn, hipStream_t st)
-{
-    switch (nord) {
-    case 15: return launch_k1_n<15>(*a, kahan, subn, st);
-    case 18: return launch_k1_n<18>(*a, kahan, subn, st);
-    case 19: return launch_k1_n<19>(*a, kahan, subn, st);
-    case 20: return launch_k1_n<20>(*a, kahan, subn, st);
-    }
-    return hipErrorInvalidValue;
 }
 
 template <int N, bool K>
