@@ -12,7 +12,8 @@
 #define ICW_MAX_OPS   64     /* DSP ops (nodes) per graph on the device path */
 #define ICW_MAX_REG_OPS 16   /* ops of a graph the frame-parallel register program accepts */
 #define ICW_MAX_REGS  8      /* value registers: `in`, node outputs, persistent slots */
-#define ICW_K2_TILE   256    /* frames per output-kernel workgroup */
+#define ICW_K2_TILE   256    /* frames per output-kernel tile (= workgroup size) */
+#define ICW_K2_TPW    4      /* consecutive tiles per output-kernel workgroup */
 #define ICW_HIST_PITCH 20    /* doubles per chain in the delay-line state */
 #define ICW_RSTATE    42     /* doubles of render state per channel: prev_rnd, prev_ns_err, E[20], O[20] */
 
@@ -28,6 +29,7 @@ struct IcwK0Args {
     const long long *pos;          /* [n_streams] reader position at the call's start */
     const long long *fade;         /* [n_streams][3] n_samples, n_fade_in, n_fade_out */
     const uint32_t *hq_phase;      /* [n_streams][2] Hilbert phase at the call's start */
+    int32_t dedup;                 /* mono dedup: the right chains' rows are not needed */
     double *xd;                    /* [n_chains][x_pitch]: each chain's own filter input sequence;
                                       complex input: rows s*4 + ch*2 + {0: I, 1: Q} hold the samples */
     size_t x_pitch;
@@ -75,6 +77,7 @@ struct IcwK1Args {
     uint32_t *info_dup;            /* [n_streams] lr_equal at this block's start (for K2) */
     int *err;                      /* set by a bounded spin that gave up (never in a healthy run) */
     int32_t wg_waves;              /* waves per workgroup of the plain / MFMA kernels (1..4) */
+    int32_t dedup;                 /* mono, every stream's converters identical: left chains only */
     double pc[20];                 /* loop-back coefficients -a[i+1]/a0 */
 };
 
@@ -93,6 +96,8 @@ struct IcwOp {
     double gain[2];
     double f[2];                   /* effective (scaled) frequency */
     double pp[2], lp[2], fa[2];    /* PM: fphase*PI, flevel*PI, fangle */
+    int32_t tslot[2];              /* Shift / PM channel: column of the per-frame rotation table */
+    int32_t pad_;
 };
 
 /* A compiled DSP list.  Register form (frame-parallel output kernel): every slot read resolves at
@@ -105,6 +110,7 @@ struct IcwProg {
     int32_t n_regs;
     int32_t bypass;                /* am.is_bypass_list: only the Master, on raw `in` */
     int32_t needs_omega;           /* some Shift / PM node is active: the frame's norm_omega is used */
+    int32_t n_trig;                /* active Shift / PM channels = columns of the rotation table */
     int32_t n_persist;             /* slots read before any write in the frame and never written */
     int32_t persist_reg[ICW_MAX_REGS], persist_slot[ICW_MAX_REGS];
     int32_t n_wb;                  /* slots written in the frame: final value -> persistent bus */
@@ -167,6 +173,22 @@ struct IcwK2Args {
     size_t x_pitch;
     int32_t cw;
     double *iq_out;                /* bus-form graph: write `in` here [n_streams][T][4], skip the rest */
+    int32_t trig;                  /* prog.needs_omega: instantiate the Shift / PM code */
+    const double *trig_tab;        /* nullable [T][trig_pitch]: (cos, sin) per active Shift / PM channel
+                                      for streams whose call-start counter equals stream 0's */
+    int32_t trig_pitch;
+};
+
+/* Per-frame rotation table (one thread per frame): the Shift / PM factors depend only on the frame
+ * counter, so streams in step share them -- computed once per block, not once per stream. */
+struct IcwTrigArgs {
+    const IcwProg *prog;
+    const unsigned long long *n_frame;   /* the reference stream's call-start counter (stream 0) */
+    long long t0;
+    int32_t T, scaled, trig_pitch;
+    unsigned long long ssr;
+    uint32_t sample_rate;
+    double *tab;                   /* [T][trig_pitch] */
 };
 
 #endif

@@ -30,6 +30,7 @@ extern "C" hipError_t icw_launch_render(const IcwK3Args *a, hipStream_t st);
 extern "C" hipError_t icw_launch_dither(const IcwK3Args *a, hipStream_t st);
 extern "C" hipError_t icw_launch_dither_lane(const IcwK3Args *a, hipStream_t st);
 extern "C" hipError_t icw_launch_output(const IcwK2Args *a, int nord, int kahan, hipStream_t st);
+extern "C" hipError_t icw_launch_trig_table(const IcwTrigArgs *a, hipStream_t st);
 extern "C" hipError_t icw_launch_graph_serial(const IcwK4Args *a, hipStream_t st);
 extern "C" hipError_t icw_launch_advance(const IcwAdvArgs *a, hipStream_t st);
 
@@ -104,6 +105,7 @@ struct icw_ctx {
     int k1_wpc = 4;                       /* ICW_K1_WPC: K1 waves per CU (one per SIMD) */
     int k1_wg = 1;                        /* ICW_K1_WG: K1 waves per workgroup */
     int max_block = kDefBlockFrames;      /* ICW_BLOCK: frames per launch block */
+    bool dedup_ok = true;                 /* ICW_DEDUP=0 disables the mono K1 dedup (A/B) */
     /* dither generation (K3a) runs on its own stream, double-buffered like the block scratch */
     hipStream_t stream3 = nullptr;
     hipEvent_t ditdone[2] = {nullptr, nullptr};
@@ -117,6 +119,12 @@ struct icw_ctx {
     size_t rpre_bytes = 0;
     double *iq = nullptr;                 /* per-block `in` buffer for the bus-form graph */
     size_t iq_bytes = 0;
+    double *trig = nullptr;               /* per-block rotation table [T][2 * n_trig] */
+    size_t trig_bytes = 0;
+    /* per stream: known on the host to have bit-identical left / right converters (fresh or reset
+     * state, or a set_state with equal halves, and no stereo block since) -- mono calls over such
+     * streams run K1 on the left chains only */
+    std::vector<char> lr_known;
     bool serial_render = false;
     uint32_t mt_seed_state[2][624];       /* seeded MT19937 states for L / R (mtrnd_init_seed) */
     hipStream_t stream = nullptr;
@@ -243,9 +251,16 @@ void op_params(const icw_node &n, IcwOp &op)
 void set_needs_omega(IcwProg &P)
 {
     P.needs_omega = 0;
+    P.n_trig = 0;
     for (int i = 0; i < P.n_ops; ++i) {
-        const IcwOp &op = P.ops[i];
-        if ((op.mode == ICW_MODE_SHIFT || op.mode == ICW_MODE_PM) && (op.act[0] || op.act[1])) P.needs_omega = 1;
+        IcwOp &op = P.ops[i];
+        op.tslot[0] = op.tslot[1] = -1;
+        if (op.mode != ICW_MODE_SHIFT && op.mode != ICW_MODE_PM) continue;
+        for (int c = 0; c < 2; ++c)
+            if (op.act[c]) {
+                op.tslot[c] = P.n_trig++;     /* a column of the per-frame rotation table */
+                P.needs_omega = 1;
+            }
     }
 }
 
@@ -412,7 +427,7 @@ void free_all(icw_ctx *c)
 {
     DevState &s = c->st;
     void *ptrs[] = {s.mt, s.mt_idx, s.rs, s.lr_equal, c->rpre, c->iq, s.err, s.hist, s.sncnt, s.hq_phase, s.pos, s.fade,
-                    s.n_frame, s.bus, s.clips, s.peak_bits, c->d_prog, c->info_dup[0], c->info_dup[1], c->w[0], c->w[1],
+                    s.n_frame, s.bus, s.clips, s.peak_bits, c->d_prog, c->info_dup[0], c->info_dup[1], c->w[0], c->w[1], c->trig,
                     c->xd[0], c->xd[1], c->d_in, c->d_out, c->d_pre};
     for (void *p : ptrs)
         if (p) hipFree(p);
@@ -550,6 +565,7 @@ int icw_create(const icw_config *cfg, const icw_node *nodes, int n_nodes, int n_
         return rc < 0 ? (rc == ICW_ENOMEM ? ICW_ENOMEM : ICW_EDEVICE) : ICW_EDEVICE;
     }
     c->peak_db.assign(S * 2, ICW_SR_ZERO_SIGNAL_DB);
+    c->lr_known.assign(S, 1);
     {
         hipDeviceProp_t prop;
         if (hipGetDeviceProperties(&prop, c->device) == hipSuccess) c->n_cu = prop.multiProcessorCount;
@@ -574,6 +590,8 @@ int icw_create(const icw_config *cfg, const icw_node *nodes, int n_nodes, int n_
         if (wpc && atoi(wpc) >= 1 && atoi(wpc) <= 8) c->k1_wpc = atoi(wpc);
         const char *bl = getenv("ICW_BLOCK");
         if (bl && atoi(bl) >= 256 && atoi(bl) <= kMaxBlockFrames) c->max_block = atoi(bl);
+        const char *dd = getenv("ICW_DEDUP");
+        if (dd && !strcmp(dd, "0")) c->dedup_ok = false;
         const char *wg = getenv("ICW_K1_WG");
         if (wg && atoi(wg) >= 1 && atoi(wg) <= 4) c->k1_wg = atoi(wg);
     }
@@ -607,6 +625,7 @@ int icw_stream_init(icw_ctx *c, int first, int count)
     ok &= hipMemsetAsync(s.sncnt + f * 4, 0, n * 4 * sizeof(unsigned long long), st) == hipSuccess;
     ok &= hipMemsetAsync(s.hq_phase + f * 2, 0, n * 2 * sizeof(uint32_t), st) == hipSuccess;
     ok &= hipMemsetD32Async((hipDeviceptr_t)(s.lr_equal + f), 1, n, st) == hipSuccess;
+    for (size_t i = 0; i < n; ++i) c->lr_known[f + i] = 1;
     ok &= hipMemsetAsync(s.pos + f, 0, n * sizeof(long long), st) == hipSuccess;
     ok &= hipMemsetAsync(s.n_frame + f, 0, n * sizeof(unsigned long long), st) == hipSuccess;
     ok &= hipMemsetAsync(s.bus + f * ICW_N_INPUTS * 4, 0, n * ICW_N_INPUTS * 4 * sizeof(double), st) == hipSuccess;
@@ -662,6 +681,7 @@ int icw_stream_open(icw_ctx *c, int s, int64_t n_samples, uint32_t fade_in, uint
         ok &= hipMemset(c->st.sncnt + (size_t)s * 4, 0, 4 * sizeof(unsigned long long)) == hipSuccess;
         ok &= hipMemset(c->st.hq_phase + (size_t)s * 2, 0, 2 * sizeof(uint32_t)) == hipSuccess;
         ok &= hipMemsetD32((hipDeviceptr_t)(c->st.lr_equal + s), 1, 1) == hipSuccess;
+        c->lr_known[s] = 1;
     }
     /* sound_render_set_outbits -> sound_render_recalc: prev_rnd, shaper buffers and prev_ns_err
      * reset, the RNG is not (sound_render.c:527-580) */
@@ -680,6 +700,7 @@ int icw_stream_reset_hilbert(icw_ctx *c, int s)
     ok &= hipMemset(c->st.sncnt + (size_t)s * 4, 0, 4 * sizeof(unsigned long long)) == hipSuccess;
     ok &= hipMemset(c->st.hq_phase + (size_t)s * 2, 0, 2 * sizeof(uint32_t)) == hipSuccess;
     ok &= hipMemsetD32((hipDeviceptr_t)(c->st.lr_equal + s), 1, 1) == hipSuccess;
+    c->lr_known[s] = 1;
     return ok ? ICW_OK : ICW_EDEVICE;
 }
 
@@ -777,6 +798,12 @@ int icw_process_streams(icw_ctx *c, int first, int count, const void *in, size_t
         return ICW_ENOMEM;
     const bool cw = cfg.in_format >= ICW_FMT_CW_F64;
     const bool bus = c->prog.is_bus;
+    /* mono dedup: every stream of the call known to hold identical left / right converters */
+    bool dedup = !cw && nch == 1 && c->dedup_ok && c->k1_mode == 0;   /* plain K1 only */
+    for (int i = 0; dedup && i < count; ++i) dedup = c->lr_known[first + i] != 0;
+    const bool table = c->prog.needs_omega && !bus && c->prog.n_trig > 0;
+    if (table && grow((void **)&c->trig, &c->trig_bytes, (size_t)Tb * 2 * c->prog.n_trig * sizeof(double)))
+        return ICW_ENOMEM;
     if (bus && grow((void **)&c->iq, &c->iq_bytes, S * (size_t)Tb * 4 * sizeof(double))) return ICW_ENOMEM;
     const bool dither = c->serial_render && cfg.render.render_type != ICW_RENDER_ROUND;
     if (dither)
@@ -791,7 +818,7 @@ int icw_process_streams(icw_ctx *c, int first, int count, const void *in, size_t
     if (c->serialize) {
         sA = sD = st;
     } else if (!cw) {
-        const int k1_waves = (count * 4 + 63) / 64;
+        const int k1_waves = (count * (dedup ? 2 : 4) + 63) / 64;
         const int k1_cus = (k1_waves + c->k1_wpc - 1) / c->k1_wpc;
         if (c->cu_split && k1_cus * 2 <= c->n_cu) {
             const CuSplit *cs = cu_split(c, k1_cus);
@@ -838,6 +865,7 @@ int icw_process_streams(icw_ctx *c, int first, int count, const void *in, size_t
         a0.hq_phase = ds.hq_phase + f0 * 2;
         a0.xd = c->xd[p];
         a0.x_pitch = x_pitch;
+        a0.dedup = dedup ? 1 : 0;
         if (b >= 2 && !cw && sK != sA && hipStreamWaitEvent(sA, c->k1done[p], 0) != hipSuccess) return ICW_EDEVICE;
         if (icw_launch_unpack(&a0, sA) != hipSuccess) return ICW_EDEVICE;
         if (hipEventRecord(c->k0done[p], sA) != hipSuccess) return ICW_EDEVICE;
@@ -871,6 +899,7 @@ int icw_process_streams(icw_ctx *c, int first, int count, const void *in, size_t
             a1.info_dup = c->info_dup[p];
             memcpy(a1.pc, c->pc, sizeof(a1.pc));
             a1.wg_waves = c->k1_wg;
+            a1.dedup = dedup ? 1 : 0;
             /* K0(b) done; it came after K2(b-2) on sA, the last reader of w[p] / info_dup[p] */
             if (sK != sA && hipStreamWaitEvent(sK, c->k0done[p], 0) != hipSuccess) return ICW_EDEVICE;
             if (timing) hipEventRecord(c->ev[4 * b], sK);
@@ -924,6 +953,24 @@ int icw_process_streams(icw_ctx *c, int first, int count, const void *in, size_t
         a2.xin = c->xd[p];
         a2.x_pitch = x_pitch;
         if (bus) a2.iq_out = c->iq;
+        a2.trig = c->prog.needs_omega;
+        if (table) {
+            IcwTrigArgs at;
+            memset(&at, 0, sizeof(at));
+            at.prog = c->d_prog;
+            at.n_frame = a2.n_frame;
+            at.t0 = t0;
+            at.T = T;
+            at.scaled = cfg.frmod_scaled;
+            at.trig_pitch = 2 * c->prog.n_trig;
+            at.ssr = ssr;
+            at.sample_rate = cfg.sample_rate;
+            at.tab = c->trig;
+            /* same stream as K2: the previous block's K2 has read the table before it is rewritten */
+            if (icw_launch_trig_table(&at, sA) != hipSuccess) return ICW_EDEVICE;
+            a2.trig_tab = c->trig;
+            a2.trig_pitch = at.trig_pitch;
+        }
         if (timing) hipEventRecord(c->ev[4 * b + 2], sA);
         if (icw_launch_output(&a2, N, cfg.iir_kahan, sA) != hipSuccess) return ICW_EDEVICE;
         if (bus) {
@@ -975,6 +1022,8 @@ int icw_process_streams(icw_ctx *c, int first, int count, const void *in, size_t
         if (timing) hipEventRecord(c->ev[4 * b + 3], sA);
         if (hipEventRecord(c->k2done[p], sA) != hipSuccess) return ICW_EDEVICE;
     }
+    if (!cw && nch > 1)
+        for (int i = 0; i < count; ++i) c->lr_known[first + i] = 0;   /* stereo: the halves diverge */
     /* join: the caller's stream continues after every kernel of the call, then the call-start
      * position / phases / frame counters advance (icw_advance) */
     for (hipStream_t x : {sK, sA, sD})
@@ -1150,6 +1199,7 @@ int icw_set_state(icw_ctx *c, int s, const void *blob, size_t size)
     ok &= hipMemcpy(c->st.bus + (size_t)s * ICW_N_INPUTS * 4, b.bus, sizeof(b.bus), hipMemcpyHostToDevice) == hipSuccess;
     const uint32_t eq = (b.hq_phase[0] == b.hq_phase[1] && !memcmp(b.hist[0], b.hist[2], sizeof(b.hist[0]) * 2)) ? 1u : 0u;
     ok &= hipMemcpy(c->st.lr_equal + s, &eq, 4, hipMemcpyHostToDevice) == hipSuccess;
+    c->lr_known[s] = eq ? 1 : 0;
     if (c->serial_render) {
         const size_t G = (size_t)c->n_streams * 2;
         for (int ch = 0; ch < 2; ++ch)

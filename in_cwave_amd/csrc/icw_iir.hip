@@ -127,8 +127,11 @@ __device__ __forceinline__ void icw_load_x(double (&xv)[N], const double *xp)
 template <int N, bool KAHAN, bool SUBN>
 __global__ __launch_bounds__(256) void icw_iir_state(IcwK1Args a)
 {
-    const int g = blockIdx.x * blockDim.x + threadIdx.x;
-    if (g >= a.n_chains) return;
+    /* mono dedup (host-known: mono input and every stream's converters identical): one lane per
+     * LEFT chain; the right converters' state is written as a copy of the left one */
+    const int gi = blockIdx.x * blockDim.x + threadIdx.x;
+    if (gi >= (a.dedup ? a.n_chains / 2 : a.n_chains)) return;
+    const int g = a.dedup ? (((gi >> 1) << 2) | (gi & 1)) : gi;
     const int s = g >> 2, c = (g >> 1) & 1, f = g & 1;
     const int n_chains = a.n_chains;
     double pc[20];
@@ -176,6 +179,12 @@ __global__ __launch_bounds__(256) void icw_iir_state(IcwK1Args a)
     }
     icw_store_hist<N, 0>(R, a.hist, g, n_chains);
     a.sncnt[g] += cnt;
+    if (a.dedup) {
+        icw_store_hist<N, 0>(R, a.hist, g + 2, n_chains);
+        a.sncnt[g + 2] += cnt;
+        if (f == 0) a.lr_equal[s] = 1u;
+        return;
+    }
     /* are the stream's right converters still bit-identical to its left ones?  The 4 chains of a
      * stream are lanes 4k..4k+3 of this wave; lane ^ 2 is the same filter of the other channel */
     bool eq = true;

@@ -140,8 +140,10 @@ __global__ __launch_bounds__(256) void icw_unpack_frames(IcwK0Args a)
         v[1] = v[0];
     }
     double *xs = a.xd + (size_t)s * 4 * a.x_pitch + t;
+    const int nchw = a.dedup ? 1 : 2;          /* mono dedup: K1 reads the left rows only */
 #pragma unroll
     for (int ch = 0; ch < 2; ++ch) {
+        if (ch >= nchw) break;
         const unsigned k = (a.hq_phase[s * 2 + ch] + (unsigned)(a.t0 + t)) & 3u;
         xs[(size_t)(ch * 2 + 0) * a.x_pitch] = icw_filter_in(v[ch], k);
         xs[(size_t)(ch * 2 + 1) * a.x_pitch] = icw_filter_in(v[ch], (k + 1u) & 3u);
@@ -251,10 +253,27 @@ __device__ __forceinline__ double icw_omega(unsigned long long n0, long long t, 
     return (2.0 * ICW_PI) * ((double)(n0 + (unsigned long long)t)) / (double)sample_rate;
 }
 
+/* The rotation factor e^{j phi} of channel c of an active Shift / PM node at norm_omega
+ * (dsp_shift adv_modulator.c:519-550, dsp_pm adv_modulator.c:554-583).  The one definition used by
+ * the per-frame table kernel and by the inline path, so both produce the same bits. */
+__device__ __forceinline__ void icw_trig(const IcwOp &op, int c, double omega, double &cs, double &sn)
+{
+    const double ph = fmod(omega * op.f[c], 2.0 * ICW_PI);
+    if (op.mode == ICW_MODE_SHIFT) {
+        sincos(ph, &sn, &cs);
+        if (op.neg[c]) sn = -sn;
+    } else {
+        const double psi = op.lp[c] * (sin(ph + op.pp[c]) + op.fa[c]);
+        sincos(psi, &sn, &cs);
+    }
+}
+
 /* One DSP node on its mixed input d (adv_modulator.c:669-751): channel exchange, I/Q swap,
- * gains, then Master (-> lOut/rOut) or Shift / PM / Mix (-> o, returns true). */
+ * gains, then Master (-> lOut/rOut) or Shift / PM / Mix (-> o, returns true).  trow: this frame's
+ * row of the rotation table (nullable: compute the factors inline). */
+template <bool TRIG = true>
 __device__ __forceinline__ bool icw_exec_op(const IcwOp &op, IcwLR d, double omega, IcwLR &o, double &lOut,
-                                            double &rOut)
+                                            double &rOut, const double *trow = nullptr)
 {
     double xt;
     switch (op.xch) {
@@ -279,34 +298,18 @@ __device__ __forceinline__ bool icw_exec_op(const IcwOp &op, IcwLR d, double ome
         lOut = icw_master(op.tout[0], d.lre, d.lim);
         rOut = icw_master(op.tout[1], d.rre, d.rim);
         return false;
-    case ICW_MODE_SHIFT: {
-        double cs, sn;
-        if (op.act[0]) {
-            const double ph = fmod(omega * op.f[0], 2.0 * ICW_PI);
-            sincos(ph, &sn, &cs);
-            if (op.neg[0]) sn = -sn;
-            icw_rot(d.lre, d.lim, cs, sn, o.lre, o.lim);
-        } else { o.lre = d.lre; o.lim = d.lim; }
-        if (op.act[1]) {
-            const double ph = fmod(omega * op.f[1], 2.0 * ICW_PI);
-            sincos(ph, &sn, &cs);
-            if (op.neg[1]) sn = -sn;
-            icw_rot(d.rre, d.rim, cs, sn, o.rre, o.rim);
-        } else { o.rre = d.rre; o.rim = d.rim; }
-        return true;
-    }
+    case ICW_MODE_SHIFT:
     case ICW_MODE_PM: {
+        if constexpr (!TRIG) { o = d; return true; }   /* no active Shift/PM in the program */
         double cs, sn;
         if (op.act[0]) {
-            const double ph = fmod(omega * op.f[0], 2.0 * ICW_PI);
-            const double psi = op.lp[0] * (sin(ph + op.pp[0]) + op.fa[0]);
-            sincos(psi, &sn, &cs);
+            if (trow) { cs = trow[op.tslot[0] * 2]; sn = trow[op.tslot[0] * 2 + 1]; }
+            else icw_trig(op, 0, omega, cs, sn);
             icw_rot(d.lre, d.lim, cs, sn, o.lre, o.lim);
         } else { o.lre = d.lre; o.lim = d.lim; }
         if (op.act[1]) {
-            const double ph = fmod(omega * op.f[1], 2.0 * ICW_PI);
-            const double psi = op.lp[1] * (sin(ph + op.pp[1]) + op.fa[1]);
-            sincos(psi, &sn, &cs);
+            if (trow) { cs = trow[op.tslot[1] * 2]; sn = trow[op.tslot[1] * 2 + 1]; }
+            else icw_trig(op, 1, omega, cs, sn);
             icw_rot(d.rre, d.rim, cs, sn, o.rre, o.rim);
         } else { o.rre = d.rre; o.rim = d.rim; }
         return true;
@@ -317,137 +320,175 @@ __device__ __forceinline__ bool icw_exec_op(const IcwOp &op, IcwLR d, double ome
     }
 }
 
-template <int N, bool KAHAN>
+/* Output kernel (K2).  A workgroup owns ICW_K2_TPW consecutive 256-frame tiles of one stream.
+ * The w window of tile k+1 is loaded into registers while tile k is computed, then written to the
+ * other half of a double-buffered LDS window: the global-load latency hides behind FP64 work and
+ * the meters reduce once per workgroup.  TRIG = the program has an active Shift / PM node. */
+template <int N, bool KAHAN, bool TRIG>
 __global__ __launch_bounds__(ICW_K2_TILE) void icw_output(IcwK2Args a)
 {
-    __shared__ double lw[4][ICW_K2_TILE + 24];
-    extern __shared__ __attribute__((aligned(16))) double lregs[];   /* [n_regs][4][ICW_K2_TILE] */
-    __shared__ unsigned red_clip[2][ICW_K2_TILE / 64];
-    __shared__ double red_pk[2][ICW_K2_TILE / 64];
+    constexpr int TILE = ICW_K2_TILE;
+    constexpr int NR = N + (KAHAN ? 0 : 1);          /* window rows past the tile */
+    __shared__ double lw[2][4][TILE + 24];
+    extern __shared__ __attribute__((aligned(16))) double lregs[];   /* [n_regs][4][TILE] */
+    __shared__ unsigned red_clip[2][TILE / 64];
+    __shared__ double red_pk[2][TILE / 64];
     const int s = blockIdx.y;
-    const int t0 = blockIdx.x * ICW_K2_TILE;
     const int tl = threadIdx.x;
-    const int t = t0 + tl;
     const int T = a.T;
+    const int tw0 = blockIdx.x * TILE * ICW_K2_TPW;
+    const int ntile = min(ICW_K2_TPW, (T - tw0 + TILE - 1) / TILE);
 
     /* mono input, converters bit-identical at block start (K1's flag) and in phase: the right
      * filter outputs are copies of the left ones this block */
     const bool dup = !a.cw && a.nch == 1 && a.info_dup && a.info_dup[s] && a.hq_phase[s * 2] == a.hq_phase[s * 2 + 1];
-    if (!a.cw) {
-        /* stage the w windows of the stream's chains (2 when dup): rows [t0, t0+nrow) */
-        const int nrow = min(ICW_K2_TILE, T - t0) + N + (KAHAN ? 0 : 1);
-        const int nc = dup ? 2 : 4;
-        for (int c = 0; c < nc; ++c) {
-            const double *src = a.w + (size_t)(s * 4 + c) * a.w_pitch + t0;
-            for (int r = tl; r < nrow; r += ICW_K2_TILE) lw[c][r] = src[r];
+    const int nc = dup ? 2 : 4;
+    /* the per-frame rotation table holds this stream's factors when its counter is in step */
+    const bool use_tab = TRIG && a.trig_tab && a.n_frame[s] == a.n_frame[0];
+    double pf[4][2];
+    auto load_tile = [&](int k) {
+        const int tt = tw0 + k * TILE;
+        const int nrow = min(TILE, T - tt) + NR;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            if (c < nc) {
+                const double *src = a.w + (size_t)(s * 4 + c) * a.w_pitch + tt;
+                pf[c][0] = tl < nrow ? src[tl] : 0.0;
+                pf[c][1] = (tl < NR && tl + TILE < nrow) ? src[tl + TILE] : 0.0;
+            }
         }
+    };
+    auto store_tile = [&](int buf) {
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            if (c < nc) {
+                lw[buf][c][tl] = pf[c][0];
+                if (tl < NR) lw[buf][c][tl + TILE] = pf[c][1];
+            }
+        }
+    };
+    if (!a.cw) {
+        load_tile(0);
+        store_tile(0);
         __syncthreads();
     }
 
+    const IcwProg *P = a.prog;
+    IcwRegFile R;
+    R.base = lregs + tl;
+    /* slots read but never written in the frame hold their block-start values */
+    for (int r = 0; r < P->n_persist; ++r) {
+        const double *b = a.bus + ((size_t)s * ICW_N_INPUTS + P->persist_slot[r]) * 4;
+        IcwLR v; v.lre = b[0]; v.lim = b[1]; v.rre = b[2]; v.rim = b[3];
+        R.set(P->persist_reg[r], v);
+    }
+    double pc[20], pd[20];
+#pragma unroll
+    for (int i = 0; i < 20; ++i) { pc[i] = a.pc[i]; pd[i] = a.pd[i]; }
+
     unsigned clip_l = 0, clip_r = 0;
     double pk_l = 0.0, pk_r = 0.0;
-    if (t < T) {
-        IcwLR in;
-        if (a.cw) {
-            /* complex (CWAVE) input: the analytic signal as read (xwave_reader.c:939-966) */
-            const double *xs = a.xin + (size_t)s * 4 * a.x_pitch + t;
-            in.lre = xs[0]; in.lim = xs[a.x_pitch]; in.rre = xs[2 * a.x_pitch]; in.rim = xs[3 * a.x_pitch];
-        } else {
-            double pc[20], pd[20];
-#pragma unroll
-            for (int i = 0; i < 20; ++i) { pc[i] = a.pc[i]; pd[i] = a.pd[i]; }
-            /* filter outputs of the 4 chains (L-I, L-Q, R-I, R-Q); the right pair is a copy when the
-             * converters are provably identical this block (mono, equal state: K0's flag) */
-            double y[4];
-            y[0] = icw_iir_out<N, KAHAN>(&lw[0][tl], pc, pd, a.d0);
-            y[1] = icw_iir_out<N, KAHAN>(&lw[1][tl], pc, pd, a.d0);
-            if (dup) {
-                y[2] = y[0];
-                y[3] = y[1];
+    for (int k = 0; k < ntile; ++k) {
+        const bool more = !a.cw && k + 1 < ntile;
+        if (more) load_tile(k + 1);
+        const int t = tw0 + k * TILE + tl;
+        const double (&W)[4][TILE + 24] = lw[k & 1];
+        if (t < T) {
+            IcwLR in;
+            if (a.cw) {
+                /* complex (CWAVE) input: the analytic signal as read (xwave_reader.c:939-966) */
+                const double *xs = a.xin + (size_t)s * 4 * a.x_pitch + t;
+                in.lre = xs[0]; in.lim = xs[a.x_pitch]; in.rre = xs[2 * a.x_pitch]; in.rim = xs[3 * a.x_pitch];
             } else {
-                y[2] = icw_iir_out<N, KAHAN>(&lw[2][tl], pc, pd, a.d0);
-                y[3] = icw_iir_out<N, KAHAN>(&lw[3][tl], pc, pd, a.d0);
+                /* filter outputs of the 4 chains (L-I, L-Q, R-I, R-Q) */
+                double y[4];
+                y[0] = icw_iir_out<N, KAHAN>(&W[0][tl], pc, pd, a.d0);
+                y[1] = icw_iir_out<N, KAHAN>(&W[1][tl], pc, pd, a.d0);
+                if (dup) {
+                    y[2] = y[0];
+                    y[3] = y[1];
+                } else {
+                    y[2] = icw_iir_out<N, KAHAN>(&W[2][tl], pc, pd, a.d0);
+                    y[3] = icw_iir_out<N, KAHAN>(&W[3][tl], pc, pd, a.d0);
+                }
+                /* fs/4 un-mix (lpf_hilbert_quad.c:129-156) */
+                double oI[2], oQ[2];
+#pragma unroll
+                for (int ch = 0; ch < 2; ++ch) {
+                    const double yi = y[ch * 2], yq = y[ch * 2 + 1];
+                    const unsigned kq = (a.hq_phase[s * 2 + ch] + (unsigned)(a.t0 + t)) & 3u;
+                    switch (kq) {
+                    case 0: oI[ch] = yi * 2.0; oQ[ch] = yq * 2.0; break;
+                    case 1: oI[ch] = -yq * 2.0; oQ[ch] = yi * 2.0; break;
+                    case 2: oI[ch] = -yi * 2.0; oQ[ch] = -yq * 2.0; break;
+                    default: oI[ch] = yq * 2.0; oQ[ch] = -yi * 2.0; break;
+                    }
+                }
+                in.lre = oI[0]; in.lim = oQ[0]; in.rre = oI[1]; in.rim = oQ[1];
             }
 
-            /* fs/4 un-mix (lpf_hilbert_quad.c:129-156) */
-            double oI[2], oQ[2];
-#pragma unroll
-            for (int ch = 0; ch < 2; ++ch) {
-                const double yi = y[ch * 2], yq = y[ch * 2 + 1];
-                const unsigned k = (a.hq_phase[s * 2 + ch] + (unsigned)(a.t0 + t)) & 3u;
-                switch (k) {
-                case 0: oI[ch] = yi * 2.0; oQ[ch] = yq * 2.0; break;
-                case 1: oI[ch] = -yq * 2.0; oQ[ch] = yi * 2.0; break;
-                case 2: oI[ch] = -yi * 2.0; oQ[ch] = -yq * 2.0; break;
-                default: oI[ch] = yq * 2.0; oQ[ch] = -yi * 2.0; break;
+            if (a.iq_out) {
+                /* bus-form graph: the serial graph kernel takes it from here (do_render == 0) */
+                double *q = a.iq_out + ((size_t)s * T + t) * 4;
+                q[0] = in.lre; q[1] = in.lim; q[2] = in.rre; q[3] = in.rim;
+            } else {
+                const double *trow = use_tab ? a.trig_tab + (size_t)t * a.trig_pitch : nullptr;
+                const double omega = (TRIG && !use_tab) ? icw_omega(a.n_frame[s], a.t0 + t, a.scaled, a.ssr, a.sample_rate)
+                                                        : 0.0;
+                /* DSP list (adv_modulator.c:637-751) */
+                R.set(0, in);
+                double lOut = 0.0, rOut = 0.0;
+                for (int oi = 0; oi < P->n_ops; ++oi) {
+                    const IcwOp &op = P->ops[oi];
+                    IcwLR d;
+                    if (P->bypass) {
+                        d = in;
+                    } else {
+                        d.lre = d.lim = d.rre = d.rim = 0.0;
+                        for (int q = 0; q < op.n_in; ++q) {
+                            IcwLR v;
+                            R.get(op.in_reg[q], v);
+                            d.lre += v.lre; d.lim += v.lim; d.rre += v.rre; d.rim += v.rim;
+                        }
+                    }
+                    IcwLR o;
+                    if (icw_exec_op<TRIG>(op, d, omega, o, lOut, rOut, trow)) R.set(op.out_reg, o);
+                }
+
+                if (a.pre) {
+                    double *p = a.pre + (size_t)s * a.pre_stride + (size_t)t * 2;
+                    p[0] = lOut; p[1] = rOut;
+                }
+                if (a.do_render) {
+                    const int vl = icw_render_round(lOut, a.rk, clip_l, pk_l);
+                    const int vr = icw_render_round(rOut, a.rk, clip_r, pk_r);
+                    unsigned char *o = a.out + (size_t)s * a.out_stride;
+                    if (a.rk.is24) {
+                        unsigned char *q = o + (size_t)t * 6;
+                        q[0] = (unsigned char)vl; q[1] = (unsigned char)(vl >> 8); q[2] = (unsigned char)(vl >> 16);
+                        q[3] = (unsigned char)vr; q[4] = (unsigned char)(vr >> 8); q[5] = (unsigned char)(vr >> 16);
+                    } else {
+                        const unsigned pk = ((unsigned)vl & 0xffffu) | ((unsigned)vr << 16);
+                        *(unsigned *)(o + (size_t)t * 4) = pk;
+                    }
+                }
+                /* persistent bus write-back from the block's last frame */
+                if (t == T - 1) {
+                    double *b0 = a.bus + (size_t)s * ICW_N_INPUTS * 4;
+                    b0[0] = in.lre; b0[1] = in.lim; b0[2] = in.rre; b0[3] = in.rim;
+                    for (int q = 0; q < P->n_wb; ++q) {
+                        IcwLR v;
+                        R.get(P->wb_reg[q], v);
+                        double *b = b0 + P->wb_slot[q] * 4;
+                        b[0] = v.lre; b[1] = v.lim; b[2] = v.rre; b[3] = v.rim;
+                    }
                 }
             }
-            in.lre = oI[0]; in.lim = oQ[0]; in.rre = oI[1]; in.rim = oQ[1];
         }
-
-        if (a.iq_out) {
-            /* bus-form graph: the serial graph kernel takes it from here */
-            double *q = a.iq_out + ((size_t)s * T + t) * 4;
-            q[0] = in.lre; q[1] = in.lim; q[2] = in.rre; q[3] = in.rim;
-            return;   /* do_render == 0 in this mode: no barrier follows */
-        }
-
-        /* DSP list (adv_modulator.c:637-751) */
-        const IcwProg *P = a.prog;
-        const double omega = P->needs_omega ? icw_omega(a.n_frame[s], a.t0 + t, a.scaled, a.ssr, a.sample_rate) : 0.0;
-        IcwRegFile R;
-        R.base = lregs + tl;
-        R.set(0, in);
-        for (int r = 0; r < P->n_persist; ++r) {
-            const double *b = a.bus + ((size_t)s * ICW_N_INPUTS + P->persist_slot[r]) * 4;
-            IcwLR v; v.lre = b[0]; v.lim = b[1]; v.rre = b[2]; v.rim = b[3];
-            R.set(P->persist_reg[r], v);
-        }
-        double lOut = 0.0, rOut = 0.0;
-        for (int oi = 0; oi < P->n_ops; ++oi) {
-            const IcwOp &op = P->ops[oi];
-            IcwLR d;
-            if (P->bypass) {
-                d = in;
-            } else {
-                d.lre = d.lim = d.rre = d.rim = 0.0;
-                for (int k = 0; k < op.n_in; ++k) {
-                    IcwLR v;
-                    R.get(op.in_reg[k], v);
-                    d.lre += v.lre; d.lim += v.lim; d.rre += v.rre; d.rim += v.rim;
-                }
-            }
-            IcwLR o;
-            if (icw_exec_op(op, d, omega, o, lOut, rOut)) R.set(op.out_reg, o);
-        }
-
-        if (a.pre) {
-            double *p = a.pre + (size_t)s * a.pre_stride + (size_t)t * 2;
-            p[0] = lOut; p[1] = rOut;
-        }
-        if (a.do_render) {
-            const int vl = icw_render_round(lOut, a.rk, clip_l, pk_l);
-            const int vr = icw_render_round(rOut, a.rk, clip_r, pk_r);
-            unsigned char *o = a.out + (size_t)s * a.out_stride;
-            if (a.rk.is24) {
-                unsigned char *q = o + (size_t)t * 6;
-                q[0] = (unsigned char)vl; q[1] = (unsigned char)(vl >> 8); q[2] = (unsigned char)(vl >> 16);
-                q[3] = (unsigned char)vr; q[4] = (unsigned char)(vr >> 8); q[5] = (unsigned char)(vr >> 16);
-            } else {
-                const unsigned pk = ((unsigned)vl & 0xffffu) | ((unsigned)vr << 16);
-                *(unsigned *)(o + (size_t)t * 4) = pk;
-            }
-        }
-        /* persistent bus write-back from the block's last frame */
-        if (t == T - 1) {
-            double *b0 = a.bus + (size_t)s * ICW_N_INPUTS * 4;
-            b0[0] = in.lre; b0[1] = in.lim; b0[2] = in.rre; b0[3] = in.rim;
-            for (int k = 0; k < P->n_wb; ++k) {
-                IcwLR v;
-                R.get(P->wb_reg[k], v);
-                double *b = b0 + P->wb_slot[k] * 4;
-                b[0] = v.lre; b[1] = v.lim; b[2] = v.rre; b[3] = v.rim;
-            }
+        if (more) {
+            /* the other half was last read in tile k-1, before the previous barrier */
+            store_tile((k + 1) & 1);
+            __syncthreads();
         }
     }
 
@@ -467,9 +508,33 @@ __global__ __launch_bounds__(ICW_K2_TILE) void icw_output(IcwK2Args a)
         __syncthreads();
         if (tl < 2) {
             unsigned cs = 0; double pm = 0.0;
-            for (int i = 0; i < ICW_K2_TILE / 64; ++i) { cs += red_clip[tl][i]; pm = fmax(pm, red_pk[tl][i]); }
+            for (int i = 0; i < TILE / 64; ++i) { cs += red_clip[tl][i]; pm = fmax(pm, red_pk[tl][i]); }
             if (cs) atomicAdd(&a.clips[s * 2 + tl], cs);
             if (pm > 0.0) atomicMax(&a.peak_bits[s * 2 + tl], (unsigned long long)__double_as_longlong(pm));
+        }
+    }
+}
+
+/* Per-frame rotation table: the Shift / PM factors of frame t depend only on the modulator frame
+ * counter, which all streams of a batch share while they are in step (same call-start counter).
+ * One thread per frame evaluates each active channel's factor once (icw_trig, the same code as
+ * the inline path); K2 reads the row instead of running fmod / sin / sincos per stream. */
+__global__ __launch_bounds__(256) void icw_trig_table(IcwTrigArgs a)
+{
+    const int t = blockIdx.x * 256 + threadIdx.x;
+    if (t >= a.T) return;
+    const IcwProg *P = a.prog;
+    const double omega = icw_omega(a.n_frame[0], a.t0 + t, a.scaled, a.ssr, a.sample_rate);
+    double *row = a.tab + (size_t)t * a.trig_pitch;
+    for (int oi = 0; oi < P->n_ops; ++oi) {
+        const IcwOp &op = P->ops[oi];
+        if (op.mode != ICW_MODE_SHIFT && op.mode != ICW_MODE_PM) continue;
+        for (int c = 0; c < 2; ++c) {
+            if (!op.act[c]) continue;
+            double cs, sn;
+            icw_trig(op, c, omega, cs, sn);
+            row[op.tslot[c] * 2] = cs;
+            row[op.tslot[c] * 2 + 1] = sn;
         }
     }
 }
@@ -1075,9 +1140,11 @@ extern "C" hipError_t icw_launch_unpack(const IcwK0Args *a, hipStream_t st)
 template <int N, bool K>
 static hipError_t launch_k2_t(const IcwK2Args &a, hipStream_t st)
 {
-    dim3 grid((a.T + ICW_K2_TILE - 1) / ICW_K2_TILE, a.n_streams);
+    constexpr int span = ICW_K2_TILE * ICW_K2_TPW;
+    dim3 grid((a.T + span - 1) / span, a.n_streams);
     const size_t lds = (size_t)a.n_regs * 4 * ICW_K2_TILE * sizeof(double);
-    hipLaunchKernelGGL((icw_output<N, K>), grid, dim3(ICW_K2_TILE), lds, st, a);
+    if (a.trig) hipLaunchKernelGGL((icw_output<N, K, true>), grid, dim3(ICW_K2_TILE), lds, st, a);
+    else hipLaunchKernelGGL((icw_output<N, K, false>), grid, dim3(ICW_K2_TILE), lds, st, a);
     return hipGetLastError();
 }
 
@@ -1140,6 +1207,12 @@ extern "C" hipError_t icw_launch_output(const IcwK2Args *a, int nord, int kahan,
     case 20: return kahan ? launch_k2_t<20, true>(*a, st) : launch_k2_t<20, false>(*a, st);
     }
     return hipErrorInvalidValue;
+}
+
+extern "C" hipError_t icw_launch_trig_table(const IcwTrigArgs *a, hipStream_t st)
+{
+    hipLaunchKernelGGL(icw_trig_table, dim3((a->T + 255) / 256), dim3(256), 0, st, *a);
+    return hipGetLastError();
 }
 
 extern "C" hipError_t icw_launch_graph_serial(const IcwK4Args *a, hipStream_t st)

@@ -12,10 +12,10 @@ pytestmark = pytest.mark.gpu
 REL_TOL = 1e-6   # north_star: "within 1e-6 relative for the float Hilbert/modulator stages"
 
 
-@pytest.fixture(autouse=True, params=["pair", "plain"])
+@pytest.fixture(autouse=True, params=["pair", "plain", "mfma"])
 def k1_mode(request, monkeypatch):
-    """run every case through both IIR-state kernels: the chain+helper wave pair (few chains per
-    SIMD) and the plain lane-per-chain kernel (throughput regime)"""
+    """run every case through every IIR-state kernel: the plain lane-per-chain kernel (default),
+    the chain+helper wave pair and the MFMA product feed (both experimental, kept bit-exact)"""
     monkeypatch.setenv("ICW_K1_MODE", request.param)
     return request.param
 
@@ -175,3 +175,63 @@ def test_meters_match_oracle(oracle, icw):
         m, r = ctx.meters(s), st.meters()
         assert m["clips"] == r["clips"] and m["desubnorm"] == r["desubnorm"]
         assert m["peak_db"] == r["peak_db"]
+
+
+def test_mono_dedup_state_and_meters(oracle, icw):
+    """mono input on fresh streams: K1 runs the left chains only and writes the right converters'
+    state as a copy -- outputs, meters (de-subnorm counts of all four filters) and the state blob
+    must equal the full computation's, and a later stereo track must still match the oracle"""
+    fs = 48000
+    cfg = graph.default_config(fs, channels=1)
+    nodes = graph.graph_master_only()
+    raw = synth.batch_pcm(5, 3000, fs, channels=1)
+    raw[2, :] = 0                                    # digital silence: every w rejected (sncnt)
+    ctx = icw.Context(cfg, nodes, 5)
+    out, pre = ctx.process(raw, 3000, want_pre=True)
+    sts = [oracle.Stream(cfg, nodes) for _ in range(5)]
+    for s in range(5):
+        ro, rp = sts[s].process(raw[s], 3000, want_pre=True)
+        assert np.array_equal(pre[s].view(np.uint64), rp.view(np.uint64)), s
+        assert np.array_equal(out[s], ro), s
+        m, r = ctx.meters(s), sts[s].meters()
+        assert m["desubnorm"] == r["desubnorm"] and m["clips"] == r["clips"], s
+    # the blob holds identical halves (the copy), so a stereo continuation stays exact
+    for s in range(5):
+        blob = abi.StateBlob.from_buffer_copy(ctx.get_state(s))
+        h = np.ctypeslib.as_array(blob.hist)
+        assert np.array_equal(h[0].view(np.uint64), h[2].view(np.uint64))
+        assert np.array_equal(h[1].view(np.uint64), h[3].view(np.uint64))
+        assert blob.sncnt[0] == blob.sncnt[2] and blob.sncnt[1] == blob.sncnt[3]
+    raw2 = synth.batch_pcm(5, 2000, fs, channels=2, first=9)
+    ctx.set_input(fs, abi.FMT_I16, 2)
+    out2, pre2 = ctx.process(raw2, 2000, want_pre=True)
+    for s in range(5):
+        sts[s].set_input(fs, abi.FMT_I16, 2)
+        ro, rp = sts[s].process(raw2[s], 2000, want_pre=True)
+        assert np.array_equal(pre2[s].view(np.uint64), rp.view(np.uint64)), s
+        assert np.array_equal(out2[s], ro), s
+
+
+def test_trig_table_streams_out_of_step(oracle, icw):
+    """the per-frame rotation table serves streams whose frame counter equals stream 0's; a stream
+    reset to another counter takes the inline path -- both must match the oracle"""
+    fs = 44100
+    cfg = graph.default_config(fs)
+    nodes = graph.graph_pm_shift_mix()
+    ctx = icw.Context(cfg, nodes, 4)
+    sts = [oracle.Stream(cfg, nodes) for _ in range(4)]
+    raw = synth.batch_pcm(4, 1700, fs)
+    ctx.process(raw, 1700)
+    for s in range(4):
+        sts[s].process(raw[s], 1700)
+    # stream 2 restarts its modulator counter (a track change with is_clr_nframe_trk)
+    ctx.stream_open(2, 1 << 40, clr_nframe=1)
+    sts[2].open(1 << 40, clr_nframe=1)
+    raw2 = synth.batch_pcm(4, 2500, fs, first=4)
+    out, pre = ctx.process(raw2, 2500, want_pre=True)
+    for s in range(4):
+        ro, rp = sts[s].process(raw2[s], 2500, want_pre=True)
+        rel = np.abs(pre[s] - rp) / np.maximum(np.abs(rp), 1.0)
+        assert rel.max() <= REL_TOL, s
+        same = pre[s].view(np.uint64) == rp.view(np.uint64)
+        assert np.array_equal(out[s].reshape(2500, 2, 2)[same], ro.reshape(2500, 2, 2)[same]), s
