@@ -872,14 +872,18 @@ int icw_process_streams(icw_ctx *c, int first, int count, const void *in, size_t
         return ICW_OK;
     };
 
+    /* Real input: K0(b+2) is queued on sA right after K1(b) (it reuses K1(b)'s xd buffer) and
+     * before K2(b), so it runs beside K1(b+1) and is done long before K1(b+2) needs it; queued
+     * behind K2(b+1) instead, it would sit between two recurrences whenever K2 is as long as K1.
+     * Complex input: K2(b) reads K0(b)'s rows, so K0(b+1) goes before K2(b) as usual. */
     int rc0 = launch_k0(0);
     if (rc0) return rc0;
+    if (!cw && n_blocks > 1 && (rc0 = launch_k0(1)) != ICW_OK) return rc0;
     for (int b = 0; b < n_blocks; ++b) {
         const int t0 = b * Tb;
         const int T = std::min(Tb, n_frames - t0);
         const int p = b & (n_sets - 1);
-        /* the next block's input prep overlaps this block's recurrence */
-        if (b + 1 < n_blocks && (rc0 = launch_k0(b + 1)) != ICW_OK) return rc0;
+        if (cw && b + 1 < n_blocks && (rc0 = launch_k0(b + 1)) != ICW_OK) return rc0;
 
         if (!cw) {
             IcwK1Args a1;
@@ -900,8 +904,9 @@ int icw_process_streams(icw_ctx *c, int first, int count, const void *in, size_t
             memcpy(a1.pc, c->pc, sizeof(a1.pc));
             a1.wg_waves = c->k1_wg;
             a1.dedup = dedup ? 1 : 0;
-            /* K0(b) done; it came after K2(b-2) on sA, the last reader of w[p] / info_dup[p] */
+            /* K0(b) done, and K2(b-2), the last reader of w[p] / info_dup[p] */
             if (sK != sA && hipStreamWaitEvent(sK, c->k0done[p], 0) != hipSuccess) return ICW_EDEVICE;
+            if (b >= 2 && sK != sA && hipStreamWaitEvent(sK, c->k2done[p], 0) != hipSuccess) return ICW_EDEVICE;
             if (timing) hipEventRecord(c->ev[4 * b], sK);
             const hipError_t e1 = c->k1_mode == 2 ? icw_launch_iir_mfma(&a1, N, cfg.iir_kahan, cfg.iir_subnorm_reject, sK)
                                 : c->k1_mode == 1 ? icw_launch_iir_pair(&a1, N, cfg.iir_kahan, cfg.iir_subnorm_reject, sK)
@@ -910,6 +915,7 @@ int icw_process_streams(icw_ctx *c, int first, int count, const void *in, size_t
             if (timing) hipEventRecord(c->ev[4 * b + 1], sK);
             if (hipEventRecord(c->k1done[p], sK) != hipSuccess) return ICW_EDEVICE;
             if (sK != sA && hipStreamWaitEvent(sA, c->k1done[p], 0) != hipSuccess) return ICW_EDEVICE;
+            if (b + 2 < n_blocks && (rc0 = launch_k0(b + 2)) != ICW_OK) return rc0;
         } else if (timing) {
             hipEventRecord(c->ev[4 * b], sA);
             hipEventRecord(c->ev[4 * b + 1], sA);

@@ -156,6 +156,53 @@ struct IcwLR { double lre, lim, rre, rim; };
 
 /* output Kahan sum of iir_rp_process_kahan (hblpf.c:1029-1043) for the sample whose delay line
  * is z_i = win[N-1-i] (win = w[t-N .. t-1]); baseline form (hblpf.c:898-925) needs w[t]=win[N] */
+/* the same sums for NC chains at once, interleaved by term: each coefficient is live for one
+ * term of all NC chains instead of across NC whole sums (with the chains back to back, all 2N
+ * coefficients stay live in SGPRs and spill to VGPR lanes -- a v_readlane per use) */
+template <int N, bool KAHAN, int NC>
+__device__ __forceinline__ void icw_iir_out_n(const double *const (&win)[NC], const double (&pc)[20],
+                                              const double (&pd)[20], double d0, double (&y)[NC])
+{
+    if (KAHAN) {
+        double S[NC], C[NC];
+#pragma unroll
+        for (int c = 0; c < NC; ++c) {
+            const double z = win[c][N - 1];
+            const double t0 = z * pc[0];
+            double Y, T;
+            S[c] = z * pd[0];
+            C[c] = 0.0;
+            const double x = t0 * d0;
+            Y = x - C[c]; T = S[c] + Y; C[c] = (T - S[c]) - Y; S[c] = T;
+        }
+#pragma unroll
+        for (int i = 1; i < N; ++i) {
+#pragma unroll
+            for (int c = 0; c < NC; ++c) {
+                const double z = win[c][N - 1 - i];
+                const double ti = z * pc[i];
+                double x = z * pd[i], Y, T;
+                Y = x - C[c]; T = S[c] + Y; C[c] = (T - S[c]) - Y; S[c] = T;
+                x = ti * d0;
+                Y = x - C[c]; T = S[c] + Y; C[c] = (T - S[c]) - Y; S[c] = T;
+            }
+        }
+#pragma unroll
+        for (int c = 0; c < NC; ++c) y[c] = S[c];
+    } else {
+        double so[NC];
+#pragma unroll
+        for (int c = 0; c < NC; ++c) so[c] = 0.0;
+#pragma unroll
+        for (int i = 0; i < N; ++i) {
+#pragma unroll
+            for (int c = 0; c < NC; ++c) so[c] += win[c][N - 1 - i] * pd[i];
+        }
+#pragma unroll
+        for (int c = 0; c < NC; ++c) y[c] = win[c][N] * d0 + so[c];
+    }
+}
+
 template <int N, bool KAHAN>
 __device__ __forceinline__ double icw_iir_out(const double *win, const double (&pc)[20],
                                               const double (&pd)[20], double d0)
@@ -402,14 +449,15 @@ __global__ __launch_bounds__(ICW_K2_TILE) void icw_output(IcwK2Args a)
             } else {
                 /* filter outputs of the 4 chains (L-I, L-Q, R-I, R-Q) */
                 double y[4];
-                y[0] = icw_iir_out<N, KAHAN>(&W[0][tl], pc, pd, a.d0);
-                y[1] = icw_iir_out<N, KAHAN>(&W[1][tl], pc, pd, a.d0);
                 if (dup) {
-                    y[2] = y[0];
-                    y[3] = y[1];
+                    const double *const wins[2] = {&W[0][tl], &W[1][tl]};
+                    double y2[2];
+                    icw_iir_out_n<N, KAHAN, 2>(wins, pc, pd, a.d0, y2);
+                    y[0] = y[2] = y2[0];
+                    y[1] = y[3] = y2[1];
                 } else {
-                    y[2] = icw_iir_out<N, KAHAN>(&W[2][tl], pc, pd, a.d0);
-                    y[3] = icw_iir_out<N, KAHAN>(&W[3][tl], pc, pd, a.d0);
+                    const double *const wins[4] = {&W[0][tl], &W[1][tl], &W[2][tl], &W[3][tl]};
+                    icw_iir_out_n<N, KAHAN, 4>(wins, pc, pd, a.d0, y);
                 }
                 /* fs/4 un-mix (lpf_hilbert_quad.c:129-156) */
                 double oI[2], oQ[2];
