@@ -31,12 +31,12 @@ sys.path.insert(0, str(ROOT))
 
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 CLOCK_GHZ = 2.4                # MI355X max engine clock (MI355X_MICROARCH.md chip table)
-# Issue floor of icw_iir_state (DESIGN.md "Roofline"): one wave issues ~one FP64 VALU instruction
-# per 4.7 cycles whether or not they depend on each other (profiles/r01_fp64_latency_probe.txt),
-# and the order-19 Kahan chain costs 19 mul + 73 add + 3 reject + 5 bookkeeping = 100 VALU per
-# sample in the compiled loop (ISA listing) -> ~470 cycles per sample per chain.
-K1_VALU_PER_SAMPLE = 100
-CYC_PER_FP64_VALU = 4.7
+# Issue floor of icw_iir_state (DESIGN.md "Roofline"): a lone wave issues one FP64 VALU instruction
+# every 5.0 cycles, dependent or not and whatever the operand banks (profiles/r01_fp64_bank_probe.txt),
+# and the order-19 Kahan loop-back sum compiles to 19 mul + 73 add + 1 cmp + 3 cndmask = 96 VALU per
+# sample (ISA listing of icw_iir_state<19,1,1>) -> ~480 cycles per sample per chain.
+K1_VALU_PER_SAMPLE = 96
+CYC_PER_FP64_VALU = 5.0
 PMC_FILE = ROOT / "profiles" / "r01_c2_pmc.json"
 FP64_PEAK_TFLOPS = 78.6        # MI355X FP64 vector (256 CU x 2.4 GHz x 128 flop/clk), vendor figure
 
@@ -212,7 +212,8 @@ def main():
         "output_kernel_avg_launch_ms": k2_avg_s * 1e3,
         "fp64_tflops_chain": (1124.0 * frames_per_launch / (k1_avg_s + k2_avg_s) / 1e12) if k1_avg_s else None,
         "fp64_peak_tflops": FP64_PEAK_TFLOPS,
-        "note": f"issue-bound serial IIR recurrence: {4 * S} chains x ~100 FP64 VALU/sample (DESIGN.md)",
+        "note": f"issue-bound serial IIR recurrence: one lane per DF-II chain ({4 * S} chains, 2 per stream "
+                f"with the mono dedup), {K1_VALU_PER_SAMPLE} FP64 VALU per sample (DESIGN.md)",
     }
     del flops_per_frame
 
