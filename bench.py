@@ -120,12 +120,16 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
+    # one process per GPU; ICW_BENCH_BACKEND=gloo + fewer GPUs than ranks is the rehearsal mode of
+    # tests/test_gpu_bench.py (ranks share a device; RCCL needs one GPU per rank)
+    ndev = torch.cuda.device_count()
+    local_dev = local % max(1, ndev)
     if world > 1:
         import torch.distributed as dist
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", rank=rank, world_size=world)
-    dev = torch.device("cuda", local)
+        torch.cuda.set_device(local_dev)
+        dist.init_process_group(os.environ.get("ICW_BENCH_BACKEND", "nccl"), rank=rank, world_size=world)
+    dev = torch.device("cuda", local_dev)
     torch.cuda.set_device(dev)
 
     from in_cwave_amd import graph, synth
@@ -136,7 +140,7 @@ def main():
     T = a.frames or W["frames"]
     fs = W["fs"]
     cfg, nodes, fmt = workload_config(W)
-    ctx = L.Context(cfg, nodes, S, device=local)
+    ctx = L.Context(cfg, nodes, S, device=local_dev)
     # synthetic input of the workload's shape for this rank's shard of streams (SURVEY 8(d)
     # generator); 16 distinct generated streams are tiled over the shard to bound setup time
     n_gen = min(S, 16)
@@ -177,7 +181,8 @@ def main():
     elapsed = time.perf_counter() - t0
     ctx.synchronize()     # raises if a kernel reported a failed hand-off
     if dist:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed], dtype=torch.float64,
+                         device=dev if dist.get_backend() == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 

@@ -174,6 +174,8 @@ struct IcwK2Args {
     int32_t cw;
     double *iq_out;                /* bus-form graph: write `in` here [n_streams][T][4], skip the rest */
     int32_t trig;                  /* prog.needs_omega: instantiate the Shift / PM code */
+    unsigned long long *sncnt;     /* [n_chains] de-subnorm rejections (hblpf.c:1046-1050), counted
+                                      here from the block's w rows; null: not counted */
     const double *trig_tab;        /* nullable [T][trig_pitch]: (cos, sin) per active Shift / PM channel
                                       for streams whose call-start counter equals stream 0's */
     int32_t trig_pitch;

@@ -960,6 +960,7 @@ int icw_process_streams(icw_ctx *c, int first, int count, const void *in, size_t
         a2.x_pitch = x_pitch;
         if (bus) a2.iq_out = c->iq;
         a2.trig = c->prog.needs_omega;
+        a2.sncnt = (!cw && cfg.iir_subnorm_reject) ? ds.sncnt + f0 * 4 : nullptr;
         if (table) {
             IcwTrigArgs at;
             memset(&at, 0, sizeof(at));

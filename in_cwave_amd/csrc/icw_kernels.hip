@@ -375,7 +375,7 @@ template <int N, bool KAHAN, bool TRIG>
 __global__ __launch_bounds__(ICW_K2_TILE) void icw_output(IcwK2Args a)
 {
     constexpr int TILE = ICW_K2_TILE;
-    constexpr int NR = N + (KAHAN ? 0 : 1);          /* window rows past the tile */
+    constexpr int NR = N + 1;                        /* window rows past the tile (row N+t: w[t]) */
     __shared__ double lw[2][4][TILE + 24];
     extern __shared__ __attribute__((aligned(16))) double lregs[];   /* [n_regs][4][TILE] */
     __shared__ unsigned red_clip[2][TILE / 64];
@@ -435,6 +435,10 @@ __global__ __launch_bounds__(ICW_K2_TILE) void icw_output(IcwK2Args a)
 
     unsigned clip_l = 0, clip_r = 0;
     double pk_l = 0.0, pk_r = 0.0;
+    /* de-subnorm rejections of this workgroup's frames, per chain: the reject stores exactly +0.0
+     * (hblpf.c:1046-1050) and every |sum| < 1 is rejected, so a w row equal to 0.0 is one count */
+    const bool count_sn = !a.cw && a.sncnt;
+    unsigned sn[4] = {0u, 0u, 0u, 0u};
     for (int k = 0; k < ntile; ++k) {
         const bool more = !a.cw && k + 1 < ntile;
         if (more) load_tile(k + 1);
@@ -447,6 +451,11 @@ __global__ __launch_bounds__(ICW_K2_TILE) void icw_output(IcwK2Args a)
                 const double *xs = a.xin + (size_t)s * 4 * a.x_pitch + t;
                 in.lre = xs[0]; in.lim = xs[a.x_pitch]; in.rre = xs[2 * a.x_pitch]; in.rim = xs[3 * a.x_pitch];
             } else {
+                if (count_sn) {
+#pragma unroll
+                    for (int c = 0; c < 4; ++c)
+                        if (c < nc) sn[c] += (W[c][tl + N] == 0.0) ? 1u : 0u;
+                }
                 /* filter outputs of the 4 chains (L-I, L-Q, R-I, R-Q) */
                 double y[4];
                 if (dup) {
@@ -540,6 +549,23 @@ __global__ __launch_bounds__(ICW_K2_TILE) void icw_output(IcwK2Args a)
         }
     }
 
+    if (count_sn) {
+        __shared__ unsigned red_sn[4][TILE / 64];
+        const int wv = tl >> 6;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            unsigned v = sn[c];
+            for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+            if ((tl & 63) == 0) red_sn[c][wv] = v;
+        }
+        __syncthreads();
+        if (tl < 4) {
+            unsigned long long tot = 0;
+            for (int i = 0; i < TILE / 64; ++i) tot += red_sn[tl < nc ? tl : tl - 2][i];
+            /* dup: the right converters ran identically, so they rejected the same samples */
+            if (tot) atomicAdd(&a.sncnt[(size_t)s * 4 + tl], tot);
+        }
+    }
     if (a.do_render) {
         /* per-workgroup meters: wave reduce, LDS, one atomic per stream/channel */
         for (int off = 32; off > 0; off >>= 1) {

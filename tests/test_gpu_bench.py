@@ -1,0 +1,48 @@
+"""bench.py end to end on the GPU: the single-process line, and the multi-rank path (torchrun,
+barrier, max-over-ranks timing, whole-job value) rehearsed with two ranks on the box's one GPU
+over gloo -- the driver's 8-GPU run takes the same code with RCCL, one GPU per rank."""
+import json
+import os
+import socket
+import subprocess
+import sys
+from pathlib import Path
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+ROOT = Path(__file__).resolve().parents[1]
+
+
+def _line(out):
+    lines = [l for l in out.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, out[-2000:]
+    return json.loads(lines[0])
+
+
+def test_bench_single_rank_line():
+    r = subprocess.run([sys.executable, "bench.py", "--steps", "1", "--warmup", "1", "--frames", "65536",
+                        "--no-cpu-baseline"], cwd=ROOT, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    d = _line(r.stdout)
+    assert d["n_gpus"] == 1 and d["unit"] == "Msamples/s" and d["higher_is_better"] is True
+    assert d["value"] > 0 and d["roofline"]["avg_launch_ms"] > 0
+    # value = 2 x frames x streams / time
+    assert abs(d["value"] - 2.0 * 256 * 65536 / (d["ms_per_step"] / 1e3) / 1e6) < 1e-6 * d["value"]
+
+
+def test_bench_two_ranks_rehearsal():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    env = dict(os.environ, ICW_BENCH_BACKEND="gloo")
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                        "--master-addr", "127.0.0.1", "--master-port", str(port), "bench.py", "--gpus", "2",
+                        "--steps", "1", "--warmup", "1", "--frames", "32768", "--streams", "64"],
+                       cwd=ROOT, capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = _line(r.stdout)
+    assert d["n_gpus"] == 2 and d["cpu_baseline"] is None
+    # whole-job value: both ranks' streams over the max-over-ranks time
+    assert abs(d["value"] - 2.0 * 2 * 64 * 32768 / (d["ms_per_step"] / 1e3) / 1e6) < 1e-6 * d["value"]
