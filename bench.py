@@ -33,9 +33,10 @@ HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 CLOCK_GHZ = 2.4                # MI355X max engine clock (MI355X_MICROARCH.md chip table)
 # Issue floor of icw_iir_state (DESIGN.md "Roofline"): a lone wave issues one FP64 VALU instruction
 # every 5.0 cycles, dependent or not and whatever the operand banks (profiles/r01_fp64_bank_probe.txt),
-# and the order-19 Kahan loop-back sum compiles to 19 mul + 73 add + 1 cmp + 3 cndmask = 96 VALU per
-# sample (ISA listing of icw_iir_state<19,1,1>) -> ~480 cycles per sample per chain.
-K1_VALU_PER_SAMPLE = 96
+# and the order-19 Kahan loop-back sum compiles to 19 v_mul_f64 + 73 v_add_f64 + 1 v_cmp_f64 = 93
+# FP64 VALU per sample (ISA listing of icw_iir_state<19,1,1>; the 2 v_cndmask_b32 of the
+# reject are 32-bit ops and left out) -> 465 cycles per sample per chain.
+K1_VALU_PER_SAMPLE = 93
 CYC_PER_FP64_VALU = 5.0
 PMC_FILE = ROOT / "profiles" / "r01_c2_pmc.json"
 FP64_PEAK_TFLOPS = 78.6        # MI355X FP64 vector (256 CU x 2.4 GHz x 128 flop/clk), vendor figure
