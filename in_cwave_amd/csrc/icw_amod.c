@@ -66,10 +66,12 @@ int icw_mod_context_fopen(icw_mod_context *mc, uint32_t sample_rate, uint32_t fm
 
 int icw_amod_process_samples(char *buf, icw_mod_context *mc, const void *tbuff, unsigned n_frames)
 {
-    static const unsigned fmt_bytes[5] = {1, 2, 3, 4, 4};
+    /* bytes per channel sample: HRW_FMT_* (xwave_reader.c:553-580), then the CWAVE complex samples
+     * (cw_slen, xwave_reader.c:246-252): the reader hands either kind to amod_process_samples */
+    static const unsigned fmt_bytes[9] = {1, 2, 3, 4, 4, 16, 4, 6, 8};
     unsigned fsz;
     int rc;
-    if (!mc || (n_frames && (!buf || !tbuff)) || mc->cfg.in_format > ICW_FMT_F32) return ICW_EINVAL;
+    if (!mc || (n_frames && (!buf || !tbuff)) || mc->cfg.in_format > ICW_FMT_CW_F32) return ICW_EINVAL;
     if (n_frames == 0) return 0;                    /* EOF: nothing read */
     fsz = fmt_bytes[mc->cfg.in_format] * mc->cfg.in_channels;
     rc = icw_process_streams(mc->ctx, 0, 1, tbuff, (size_t)n_frames * fsz, buf,

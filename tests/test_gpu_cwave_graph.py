@@ -174,3 +174,38 @@ def test_mono_after_stereo_track(oracle, icw):
     raw = synth.batch_pcm(2, 3000, fs, channels=1)
     _, pre = ctx2.process(raw, 3000, want_pre=True)
     assert np.array_equal(pre[:, :, 0].view(np.uint64), pre[:, :, 1].view(np.uint64))
+
+
+@pytest.mark.parametrize("fmt", CW)
+def test_dropin_boundary_takes_cwave(oracle, icw, fmt):
+    """icw_amod_process_samples (the amod_process_samples drop-in) fed CWAVE blocks the way the
+    reader hands them over (576-frame blocks of raw complex samples): WAV track first, then a
+    CWAVE track in the same context -- the converters keep their state across it"""
+    import ctypes as C
+    lib = icw.load()
+    fs = 48000
+    cfg = graph.default_config(fs)
+    nodes = graph.graph_shift_master()
+    arr = graph.node_array(nodes)
+    st = C.c_int()
+    mc = lib.icw_mod_context_create(C.byref(cfg), arr, len(nodes), 0, C.byref(st))
+    assert mc and st.value == abi.OK
+    ref = oracle.Stream(cfg, nodes)
+    osz = lib.icw_mod_context_out_size(mc)
+    for track, (f, n) in enumerate([(abi.FMT_I16, 1700), (fmt, 2300)]):
+        raw = synth.batch_pcm(1, n, fs, channels=2, fmt=f, first=11 + track)[0]
+        assert lib.icw_mod_context_fopen(mc, fs, f, 2, n, 0, 0, 0, 0, 0) == abi.OK
+        ref.set_input(fs, f, 2)
+        ref.open(n)
+        fsz = abi.FMT_BYTES[f] * 2
+        got = []
+        for t in range(0, n, 576):
+            k = min(576, n - t)
+            blk = np.ascontiguousarray(raw[t * fsz:(t + k) * fsz])
+            buf = np.zeros(k * osz, np.uint8)
+            assert lib.icw_amod_process_samples(buf.ctypes.data, mc, blk.ctypes.data, k) == k
+            got.append(buf)
+        ro, _ = ref.process(raw, n)
+        d = np.abs(np.concatenate(got).view("<i2").astype(int) - ro.view("<i2").astype(int))
+        assert d.max() <= 1 and (d > 0).mean() < 1e-3, (track, d.max())    # Shift: sin/cos ulps
+    lib.icw_mod_context_destroy(mc)
