@@ -73,8 +73,11 @@ struct IcwK1Args {
     unsigned long long *sncnt;     /* [n_chains] subnorm rejections */
     double *w;                     /* [n_chains][w_pitch]: rows [0,N) history, [N,N+T) block */
     size_t w_pitch;
-    uint32_t *lr_equal;            /* [n_streams] left and right converters bit-identical (state) */
-    uint32_t *info_dup;            /* [n_streams] lr_equal at this block's start (for K2) */
+    uint32_t *lr_equal;            /* [n_streams][2] per filter (I, Q): the right converter's chain is
+                                      bit-identical to the left one (state) */
+    uint32_t *info_dup;            /* [n_streams][2] lr_equal at this block's start (for K2) */
+    const uint32_t *hq_phase;      /* [n_streams][2] call-start Hilbert phases (zero-input parity) */
+    long long t0;                  /* block offset into the call */
     int *err;                      /* set by a bounded spin that gave up (never in a healthy run) */
     int32_t wg_waves;              /* waves per workgroup of the plain / MFMA kernels (1..4) */
     int32_t dedup;                 /* mono, every stream's converters identical: left chains only */
@@ -168,7 +171,7 @@ struct IcwK2Args {
     unsigned long long *peak_bits; /* [n_streams][2] max |q| as ordered bits */
     IcwRenderK rk;
     double pc[20], pd[20], d0;
-    const uint32_t *info_dup;      /* [n_streams] K1's flag: the converters were identical at block start */
+    const uint32_t *info_dup;      /* [n_streams][2] K1's flags: the converters were identical at block start */
     const double *xin;             /* complex input: K0's I/Q rows (then w is unused) */
     size_t x_pitch;
     int32_t cw;

@@ -64,7 +64,7 @@ struct DevState {
     uint32_t *mt = nullptr;               /* [624][2*streams] */
     int32_t *mt_idx = nullptr;            /* [2*streams] */
     double *rs = nullptr;                 /* [2*streams][ICW_RSTATE] */
-    uint32_t *lr_equal = nullptr;         /* [streams] right converters bit-identical to left ones */
+    uint32_t *lr_equal = nullptr;         /* [streams][2] right converters bit-identical to left ones, per filter */
 };
 
 /* streams confined to disjoint CU sets: K1 on k1_cus CUs spread over the device, the rest on
@@ -544,8 +544,8 @@ int icw_create(const icw_config *cfg, const icw_node *nodes, int n_nodes, int n_
         rc |= dalloc(&s.mt_idx, S * 2);
         rc |= dalloc(&s.rs, S * 2 * ICW_RSTATE);
     }
-    rc |= dalloc(&s.lr_equal, S);
-    for (int p = 0; p < 2; ++p) rc |= dalloc(&c->info_dup[p], S);
+    rc |= dalloc(&s.lr_equal, S * 2);
+    for (int p = 0; p < 2; ++p) rc |= dalloc(&c->info_dup[p], S * 2);
     rc |= dalloc(&c->d_prog, 1);
     if (rc == ICW_OK && hipMemcpy(c->d_prog, &c->prog, sizeof(IcwProg), hipMemcpyHostToDevice) != hipSuccess)
         rc = ICW_EDEVICE;
@@ -624,7 +624,7 @@ int icw_stream_init(icw_ctx *c, int first, int count)
     ok &= hipMemsetAsync(s.hist + f * 4 * ICW_HIST_PITCH, 0, n * 4 * ICW_HIST_PITCH * sizeof(double), st) == hipSuccess;
     ok &= hipMemsetAsync(s.sncnt + f * 4, 0, n * 4 * sizeof(unsigned long long), st) == hipSuccess;
     ok &= hipMemsetAsync(s.hq_phase + f * 2, 0, n * 2 * sizeof(uint32_t), st) == hipSuccess;
-    ok &= hipMemsetD32Async((hipDeviceptr_t)(s.lr_equal + f), 1, n, st) == hipSuccess;
+    ok &= hipMemsetD32Async((hipDeviceptr_t)(s.lr_equal + f * 2), 1, n * 2, st) == hipSuccess;
     for (size_t i = 0; i < n; ++i) c->lr_known[f + i] = 1;
     ok &= hipMemsetAsync(s.pos + f, 0, n * sizeof(long long), st) == hipSuccess;
     ok &= hipMemsetAsync(s.n_frame + f, 0, n * sizeof(unsigned long long), st) == hipSuccess;
@@ -680,7 +680,7 @@ int icw_stream_open(icw_ctx *c, int s, int64_t n_samples, uint32_t fade_in, uint
         ok &= hipMemset(c->st.hist + (size_t)s * 4 * ICW_HIST_PITCH, 0, 4 * ICW_HIST_PITCH * sizeof(double)) == hipSuccess;
         ok &= hipMemset(c->st.sncnt + (size_t)s * 4, 0, 4 * sizeof(unsigned long long)) == hipSuccess;
         ok &= hipMemset(c->st.hq_phase + (size_t)s * 2, 0, 2 * sizeof(uint32_t)) == hipSuccess;
-        ok &= hipMemsetD32((hipDeviceptr_t)(c->st.lr_equal + s), 1, 1) == hipSuccess;
+        ok &= hipMemsetD32((hipDeviceptr_t)(c->st.lr_equal + (size_t)s * 2), 1, 2) == hipSuccess;
         c->lr_known[s] = 1;
     }
     /* sound_render_set_outbits -> sound_render_recalc: prev_rnd, shaper buffers and prev_ns_err
@@ -699,7 +699,7 @@ int icw_stream_reset_hilbert(icw_ctx *c, int s)
     ok &= hipMemset(c->st.hist + (size_t)s * 4 * ICW_HIST_PITCH, 0, 4 * ICW_HIST_PITCH * sizeof(double)) == hipSuccess;
     ok &= hipMemset(c->st.sncnt + (size_t)s * 4, 0, 4 * sizeof(unsigned long long)) == hipSuccess;
     ok &= hipMemset(c->st.hq_phase + (size_t)s * 2, 0, 2 * sizeof(uint32_t)) == hipSuccess;
-    ok &= hipMemsetD32((hipDeviceptr_t)(c->st.lr_equal + s), 1, 1) == hipSuccess;
+    ok &= hipMemsetD32((hipDeviceptr_t)(c->st.lr_equal + (size_t)s * 2), 1, 2) == hipSuccess;
     c->lr_known[s] = 1;
     return ok ? ICW_OK : ICW_EDEVICE;
 }
@@ -818,7 +818,9 @@ int icw_process_streams(icw_ctx *c, int first, int count, const void *in, size_t
     if (c->serialize) {
         sA = sD = st;
     } else if (!cw) {
-        const int k1_waves = (count * (dedup ? 2 : 4) + 63) / 64;
+        /* plain K1: 128-lane groups of 32 streams (64 with the dedup); the variants: a lane per chain */
+        const int k1_waves = c->k1_mode == 0 ? ((count + (dedup ? 63 : 31)) / (dedup ? 64 : 32)) * 2
+                                             : (count * 4 + 63) / 64;
         const int k1_cus = (k1_waves + c->k1_wpc - 1) / c->k1_wpc;
         if (c->cu_split && k1_cus * 2 <= c->n_cu) {
             const CuSplit *cs = cu_split(c, k1_cus);
@@ -899,7 +901,9 @@ int icw_process_streams(icw_ctx *c, int first, int count, const void *in, size_t
             a1.err = ds.err;
             a1.w = c->w[p];
             a1.w_pitch = w_pitch;
-            a1.lr_equal = ds.lr_equal + f0;
+            a1.lr_equal = ds.lr_equal + f0 * 2;
+            a1.hq_phase = ds.hq_phase + f0 * 2;
+            a1.t0 = t0;
             a1.info_dup = c->info_dup[p];
             memcpy(a1.pc, c->pc, sizeof(a1.pc));
             a1.wg_waves = c->k1_wg;
@@ -1205,7 +1209,8 @@ int icw_set_state(icw_ctx *c, int s, const void *blob, size_t size)
     ok &= hipMemcpy(c->st.sncnt + (size_t)s * 4, b.sncnt, sizeof(b.sncnt), hipMemcpyHostToDevice) == hipSuccess;
     ok &= hipMemcpy(c->st.bus + (size_t)s * ICW_N_INPUTS * 4, b.bus, sizeof(b.bus), hipMemcpyHostToDevice) == hipSuccess;
     const uint32_t eq = (b.hq_phase[0] == b.hq_phase[1] && !memcmp(b.hist[0], b.hist[2], sizeof(b.hist[0]) * 2)) ? 1u : 0u;
-    ok &= hipMemcpy(c->st.lr_equal + s, &eq, 4, hipMemcpyHostToDevice) == hipSuccess;
+    const uint32_t eq2[2] = {eq, eq};
+    ok &= hipMemcpy(c->st.lr_equal + (size_t)s * 2, eq2, sizeof(eq2), hipMemcpyHostToDevice) == hipSuccess;
     c->lr_known[s] = eq ? 1 : 0;
     if (c->serial_render) {
         const size_t G = (size_t)c->n_streams * 2;

@@ -117,6 +117,50 @@ __device__ __forceinline__ void icw_block_steps_pf(double (&R)[N], double (&xv)[
     }
 }
 
+/* Zero-input step (Kahan, subnorm reject on).  Every other sample of a chain's input is the
+ * literal +0.0 of hq_rp_process (lpf_hilbert_quad.c:136-151).  With sample = +0:
+ *   kahan_init(+0): S = +0, C = 0;  i = 0: Y = t0, T = +0 + t0, C = (T - 0) - t0 = +0, S = T;
+ *   i = 1: Y = t1 - (+0) = t1.
+ * So S = t0 and C = +0 after step 0, and step 1's Y is t1: 4 adds fewer.  S can differ from the
+ * reference only in the sign of a zero (t0 = -0 gives T = +0); a zero's sign is absorbed by the
+ * first nonzero term, and a sum that stays zero is rejected to +0.0 (|S| < 1, hblpf.c:1046), so
+ * w is bit-identical.  (With the reject off the sign would survive: that mode takes icw_iir_step.) */
+template <int N, int J>
+__device__ __forceinline__ void icw_iir_step_z(double (&R)[N], const double (&pc)[20], unsigned &cnt)
+{
+    double S = R[(J - 1 + N) % N] * pc[0];
+    double C, Y, T;
+    Y = R[(J - 2 + 2 * N) % N] * pc[1];
+    T = S + Y; C = (T - S) - Y; S = T;
+#pragma unroll
+    for (int i = 2; i < N; ++i) {
+        const double ti = R[(J - 1 - i + 2 * N) % N] * pc[i];
+        Y = ti - C; T = S + Y; C = (T - S) - Y; S = T;
+    }
+    const bool z = fabs(S) < 1.0;
+    cnt += z ? 1u : 0u;
+    S = z ? 0.0 : S;
+    R[J] = S;
+}
+
+/* A block of N steps whose input is zero at the steps J with (J & 1) == Z.  The next block's
+ * zero steps are the other parity (N is odd), so the look-ahead refill of xv[J] is needed exactly
+ * where this block's step J had a zero input. */
+template <int N, int J0, int Z, bool SUBN>
+__device__ __forceinline__ void icw_block_steps_zpf(double (&R)[N], double (&xv)[N], const double *xnext,
+                                                    const double (&pc)[20], unsigned &cnt)
+{
+    if constexpr (J0 < N) {
+        if constexpr ((J0 & 1) == Z) {
+            icw_iir_step_z<N, J0>(R, pc, cnt);
+            xv[J0] = xnext[J0];
+        } else {
+            icw_iir_step<N, true, SUBN, J0>(R, xv[J0], pc, cnt);
+        }
+        icw_block_steps_zpf<N, J0 + 1, Z, SUBN>(R, xv, xnext, pc, cnt);
+    }
+}
+
 template <int N>
 __device__ __forceinline__ void icw_load_x(double (&xv)[N], const double *xp)
 {
@@ -124,15 +168,26 @@ __device__ __forceinline__ void icw_load_x(double (&xv)[N], const double *xp)
     for (int j = 0; j < N; ++j) xv[j] = xp[j];
 }
 
+/* Lane layout: a group of 128 lanes (two waves) covers 32 streams (64 with the mono dedup); wave
+ * f of the group holds filter f (0: I, 1: Q) of every channel, lane l = stream (l >> 1), channel
+ * (l & 1) -- or stream l, left channel, under the dedup.  A wave's chains then share the phase
+ * parity of their zero inputs whenever the streams' Hilbert phases agree in parity (the usual
+ * case: streams started together), which the zero-input fast path needs. */
+__device__ __forceinline__ bool icw_k1_chain(int gi, int count, bool dedup, int &s, int &ch, int &f)
+{
+    const int grp = gi >> 7, w = (gi >> 6) & 1, l = gi & 63;
+    f = w;
+    if (dedup) { s = grp * 64 + l; ch = 0; }
+    else { s = grp * 32 + (l >> 1); ch = l & 1; }
+    return s < count;
+}
+
 template <int N, bool KAHAN, bool SUBN>
 __global__ __launch_bounds__(256) void icw_iir_state(IcwK1Args a)
 {
-    /* mono dedup (host-known: mono input and every stream's converters identical): one lane per
-     * LEFT chain; the right converters' state is written as a copy of the left one */
-    const int gi = blockIdx.x * blockDim.x + threadIdx.x;
-    if (gi >= (a.dedup ? a.n_chains / 2 : a.n_chains)) return;
-    const int g = a.dedup ? (((gi >> 1) << 2) | (gi & 1)) : gi;
-    const int s = g >> 2, c = (g >> 1) & 1, f = g & 1;
+    int s, ch, f;
+    if (!icw_k1_chain(blockIdx.x * blockDim.x + threadIdx.x, a.n_streams, a.dedup != 0, s, ch, f)) return;
+    const int g = s * 4 + ch * 2 + f;
     const int n_chains = a.n_chains;
     double pc[20];
 #pragma unroll
@@ -142,7 +197,8 @@ __global__ __launch_bounds__(256) void icw_iir_state(IcwK1Args a)
 #pragma unroll
     for (int i = 0; i < N; ++i) R[N - 1 - i] = a.hist[(size_t)g * ICW_HIST_PITCH + i];
 
-    if (f == 0 && c == 0) a.info_dup[s] = a.lr_equal[s];     /* this block's start (for K2) */
+    /* this block's start (for K2); each (stream, filter) flag is read and written by one wave */
+    if (ch == 0) a.info_dup[s * 2 + f] = a.lr_equal[s * 2 + f];
     const double *xp = a.xd + (size_t)g * a.x_pitch;
     double *wrow = a.w + (size_t)g * a.w_pitch;
     /* history rows [0, N): row j = z_{N-1-j} = R[j] */
@@ -158,6 +214,31 @@ __global__ __launch_bounds__(256) void icw_iir_state(IcwK1Args a)
          * with no register copies */
         double xv[N];
         icw_load_x<N>(xv, xp);
+        if constexpr (KAHAN && SUBN && (N & 1)) {
+            /* block-relative sample n has a zero input iff (phi + n) is odd (I: k = hq + t0 + n odd;
+             * Q: k + 1 odd); the fast path needs one parity across the wave */
+            const unsigned phi = (a.hq_phase[s * 2 + ch] + (unsigned)a.t0 + (unsigned)f) & 1u;
+            const unsigned phi0 = __builtin_amdgcn_readfirstlane(phi);
+            if (__all(phi == phi0) && T >= 3 * N) {
+                if (phi0) {   /* align: pairs start on a nonzero sample */
+                    icw_block_steps_pf<N, 0, KAHAN, SUBN>(R, xv, xp + t + N, pc, cnt);
+                    double *wo = wrow + N + t;
+#pragma unroll
+                    for (int j = 0; j < N; ++j) wo[j] = R[j];
+                    t += N;
+                }
+                for (; t + 2 * N <= T; t += 2 * N) {
+                    icw_block_steps_zpf<N, 0, 1, SUBN>(R, xv, xp + t + N, pc, cnt);
+                    double *wo = wrow + N + t;
+#pragma unroll
+                    for (int j = 0; j < N; ++j) wo[j] = R[j];
+                    icw_block_steps_zpf<N, 0, 0, SUBN>(R, xv, xp + t + 2 * N, pc, cnt);
+#pragma unroll
+                    for (int j = 0; j < N; ++j) wo[N + j] = R[j];
+                }
+                icw_load_x<N>(xv, xp + t);   /* the zero steps left half of xv unloaded */
+            }
+        }
         for (; t + N <= T; t += N) {
             icw_block_steps_pf<N, 0, KAHAN, SUBN>(R, xv, xp + t + N, pc, cnt);
             double *wo = wrow + N + t;
@@ -183,19 +264,18 @@ __global__ __launch_bounds__(256) void icw_iir_state(IcwK1Args a)
     icw_store_hist<N, 0>(R, a.hist, g, n_chains);
     if (a.dedup) {
         icw_store_hist<N, 0>(R, a.hist, g + 2, n_chains);
-        if (f == 0) a.lr_equal[s] = 1u;
+        a.lr_equal[s * 2 + f] = 1u;
         return;
     }
-    /* are the stream's right converters still bit-identical to its left ones?  The 4 chains of a
-     * stream are lanes 4k..4k+3 of this wave; lane ^ 2 is the same filter of the other channel */
+    /* is this (stream, filter)'s right converter still bit-identical to its left one?  The two
+     * channels of a stream are lanes l, l ^ 1 of this wave */
     bool eq = true;
 #pragma unroll
     for (int i = 0; i < N; ++i) {
-        const double o = __shfl_xor(R[i], 2);
+        const double o = __shfl_xor(R[i], 1);
         eq = eq && (__double_as_longlong(o) == __double_as_longlong(R[i]));
     }
-    const bool eq_q = __shfl_xor((int)eq, 1) != 0;
-    if (f == 0 && c == 0) a.lr_equal[s] = (eq && eq_q) ? 1u : 0u;
+    if (ch == 0) a.lr_equal[s * 2 + f] = eq ? 1u : 0u;
 }
 
 /* ------------------------------------------- IIR state kernel, MFMA product feed (K1m) ---- */
@@ -326,7 +406,7 @@ __global__ __launch_bounds__(256) void icw_iir_state_mf(IcwK1Args a)
 #pragma unroll
     for (int i = 0; i < N; ++i) R[N - 1 - i] = a.hist[(size_t)g * ICW_HIST_PITCH + i];
 
-    if (own && f == 0 && c == 0) a.info_dup[s] = a.lr_equal[s];
+    if (own && c == 0) a.info_dup[s * 2 + f] = a.lr_equal[s * 2 + f];
     const double *xp = a.xd + (size_t)g * a.x_pitch;
     double *wrow = a.w + (size_t)g * a.w_pitch;
     if (own) {
@@ -375,7 +455,7 @@ __global__ __launch_bounds__(256) void icw_iir_state_mf(IcwK1Args a)
     if (!own) return;
     icw_store_hist<N, 0>(R, a.hist, g, n_chains);
     (void)cnt;   /* counted by K2 */
-    if (f == 0 && c == 0) a.lr_equal[s] = (eq && eq_q) ? 1u : 0u;
+    if (c == 0) a.lr_equal[s * 2 + f] = (eq && eq_q) ? 1u : 0u;
 }
 
 /* ---------------------------------------- IIR state kernel, chain+helper wave pair (K1p) ---- */
@@ -652,18 +732,20 @@ __global__ __launch_bounds__(128) void icw_iir_pair(IcwK1Args a)
     if (!valid) return;
     icw_store_hist<N, 0>(R, a.hist, g, a.n_chains);
     (void)cnt;   /* counted by K2 */
-    if (f == 0 && c == 0) {   /* the pair kernel does not track converter identity: no shortcut */
-        a.info_dup[s] = 0u;
-        a.lr_equal[s] = 0u;
+    if (c == 0) {   /* the pair kernel does not track converter identity: no shortcut */
+        a.info_dup[s * 2 + f] = 0u;
+        a.lr_equal[s * 2 + f] = 0u;
     }
 }
 /* ---------------------------------------------------------------- launch wrappers ------- */
 template <int N, bool K, bool S>
 static hipError_t launch_k1_t(const IcwK1Args &a, hipStream_t st)
 {
-    /* wg_waves waves per workgroup: 4 puts one recurrence wave on each SIMD of a CU */
+    /* 128-lane groups of 32 streams (64 under the mono dedup), see icw_k1_chain */
+    const int spg = a.dedup ? 64 : 32;
+    const long lanes = (long)((a.n_streams + spg - 1) / spg) * 128;
     const int tpb = 64 * a.wg_waves;
-    const int blocks = (a.n_chains + tpb - 1) / tpb;
+    const int blocks = (int)((lanes + tpb - 1) / tpb);
     hipLaunchKernelGGL((icw_iir_state<N, K, S>), dim3(blocks), dim3(tpb), 0, st, a);
     return hipGetLastError();
 }

@@ -388,7 +388,8 @@ __global__ __launch_bounds__(ICW_K2_TILE) void icw_output(IcwK2Args a)
 
     /* mono input, converters bit-identical at block start (K1's flag) and in phase: the right
      * filter outputs are copies of the left ones this block */
-    const bool dup = !a.cw && a.nch == 1 && a.info_dup && a.info_dup[s] && a.hq_phase[s * 2] == a.hq_phase[s * 2 + 1];
+    const bool dup = !a.cw && a.nch == 1 && a.info_dup && a.info_dup[s * 2] && a.info_dup[s * 2 + 1] &&
+                     a.hq_phase[s * 2] == a.hq_phase[s * 2 + 1];
     const int nc = dup ? 2 : 4;
     /* the per-frame rotation table holds this stream's factors when its counter is in step */
     const bool use_tab = TRIG && a.trig_tab && a.n_frame[s] == a.n_frame[0];

@@ -235,3 +235,28 @@ def test_trig_table_streams_out_of_step(oracle, icw):
         assert rel.max() <= REL_TOL, s
         same = pre[s].view(np.uint64) == rp.view(np.uint64)
         assert np.array_equal(out[s].reshape(2500, 2, 2)[same], ro.reshape(2500, 2, 2)[same]), s
+
+
+def test_zero_input_fast_path_mixed_phases(oracle, icw):
+    """K1's zero-input fast path needs one phase parity per wave: after an odd-length block and a
+    Hilbert reset of one stream, a wave mixes parities (generic path) while other waves do not --
+    every stream must still match the oracle bit for bit (Master only: exact pre-render)"""
+    fs = 48000
+    cfg = graph.default_config(fs)
+    nodes = graph.graph_master_only()
+    S = 40                                              # two 32-stream lane groups, one partial
+    ctx = icw.Context(cfg, nodes, S)
+    sts = [oracle.Stream(cfg, nodes) for _ in range(S)]
+    raw = synth.batch_pcm(S, 1001, fs)
+    ctx.process(raw, 1001)
+    for s in range(S):
+        sts[s].process(raw[s], 1001)
+    for s in (1, 35):                                   # phase 0 among streams at phase 1001 & 3
+        ctx.stream_open(s, 1 << 40, clr_hilb=1)
+        sts[s].open(1 << 40, clr_hilb=1)
+    raw2 = synth.batch_pcm(S, 3000, fs, first=S)
+    out, pre = ctx.process(raw2, 3000, want_pre=True)
+    for s in range(S):
+        ro, rp = sts[s].process(raw2[s], 3000, want_pre=True)
+        assert np.array_equal(pre[s].view(np.uint64), rp.view(np.uint64)), s
+        assert np.array_equal(out[s], ro), s
