@@ -32,11 +32,12 @@ sys.path.insert(0, str(ROOT))
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 CLOCK_GHZ = 2.4                # MI355X max engine clock (MI355X_MICROARCH.md chip table)
 # Issue floor of icw_iir_state (DESIGN.md "Roofline"): a lone wave issues one FP64 VALU instruction
-# every 5.0 cycles, dependent or not and whatever the operand banks (profiles/r01_fp64_bank_probe.txt),
-# and the order-19 Kahan loop-back sum compiles to 19 v_mul_f64 + 73 v_add_f64 + 1 v_cmp_f64 = 93
-# FP64 VALU per sample (ISA listing of icw_iir_state<19,1,1>; the 2 v_cndmask_b32 of the
-# reject are 32-bit ops and left out) -> 465 cycles per sample per chain.
-K1_VALU_PER_SAMPLE = 93
+# per ~5.0 cycles, dependent or not, add or mul, whatever the operand banks
+# (profiles/r01_fp64_bank_probe.txt: 5.00 and 5.25 s_memtime ticks per op on two boxes). The
+# recurrence compiles to 91 FP64 VALU per sample on average (71 v_add_f64 + 19 v_mul_f64 + 1
+# v_cmp_f64: the order-19 Kahan loop-back sum with the zero-input steps 4 adds shorter, ISA of
+# icw_iir_state<19,1,1>) plus 2 v_cndmask_b32 -> a floor of ~455 cycles per sample per chain.
+K1_VALU_PER_SAMPLE = 91
 CYC_PER_FP64_VALU = 5.0
 PMC_FILE = ROOT / "profiles" / "r01_c2_pmc.json"
 FP64_PEAK_TFLOPS = 78.6        # MI355X FP64 vector (256 CU x 2.4 GHz x 128 flop/clk), vendor figure
@@ -219,7 +220,8 @@ def main():
         "fp64_tflops_chain": (1124.0 * frames_per_launch / (k1_avg_s + k2_avg_s) / 1e12) if k1_avg_s else None,
         "fp64_peak_tflops": FP64_PEAK_TFLOPS,
         "note": f"issue-bound serial IIR recurrence: one lane per DF-II chain ({4 * S} chains, 2 per stream "
-                f"with the mono dedup), {K1_VALU_PER_SAMPLE} FP64 VALU per sample (DESIGN.md)",
+                f"with the mono dedup), {K1_VALU_PER_SAMPLE} FP64 VALU per sample; frac ~1 = at the issue floor "
+                f"within the probe's few-% spread (DESIGN.md)",
     }
     del flops_per_frame
 

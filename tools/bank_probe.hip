@@ -47,6 +47,13 @@ PROBE(kahan_cc, INIT,
       "v_add_f64 v[4:5], v[12:13], -v[4:5]\n v_add_f64 v[0:1], v[8:9], v[4:5]\n v_add_f64 v[8:9], v[0:1], -v[8:9]\n v_add_f64 v[4:5], v[8:9], -v[4:5]\n"
       "v_add_f64 v[4:5], v[12:13], -v[4:5]\n v_add_f64 v[8:9], v[0:1], v[4:5]\n v_add_f64 v[0:1], v[8:9], -v[0:1]\n v_add_f64 v[4:5], v[0:1], -v[4:5]", 8)
 
+/* the K1 mix: per 5 instructions, 4 dependent adds (the Kahan chain) + 1 independent mul (a product) */
+PROBE(kahan_mix, INIT,
+      "v_mul_f64 v[10:11], v[12:13], v[14:15]\n v_add_f64 v[2:3], v[10:11], -v[8:9]\n v_add_f64 v[6:7], v[0:1], v[2:3]\n v_add_f64 v[4:5], v[6:7], -v[0:1]\n v_add_f64 v[8:9], v[4:5], -v[2:3]\n"
+      "v_mul_f64 v[10:11], v[14:15], v[12:13]\n v_add_f64 v[2:3], v[10:11], -v[8:9]\n v_add_f64 v[0:1], v[6:7], v[2:3]\n v_add_f64 v[4:5], v[0:1], -v[6:7]\n v_add_f64 v[8:9], v[4:5], -v[2:3]", 10)
+/* independent muls only */
+PROBE(ind_mul, INIT, "v_mul_f64 v[4:5], v[6:7], v[8:9]\n v_mul_f64 v[10:11], v[12:13], v[14:15]\n v_mul_f64 v[0:1], v[6:7], v[14:15]\n v_mul_f64 v[2:3], v[8:9], v[12:13]", 4)
+
 typedef void (*K)(long long *, double *);
 
 static void run(const char *name, K k, int waves, int ops_per_rep, long long *dcyc, double *dout)
@@ -72,6 +79,8 @@ int main()
         run("mul_b02", mul_b02, w, 4, dcyc, dout);
         run("kahan_nc", kahan_nc, w, 8, dcyc, dout);
         run("kahan_cc", kahan_cc, w, 8, dcyc, dout);
+        run("kahan_mix", kahan_mix, w, 10, dcyc, dout);
+        run("ind_mul", ind_mul, w, 4, dcyc, dout);
     }
     return 0;
 }
