@@ -267,20 +267,43 @@ __device__ __forceinline__ void icw_rot(double re, double im, double cs, double 
     oim = re * sn + im * cs;
 }
 
+/* The rounding step of sound_render_value (sound_render.c:757-767) in fewer instructions, same bits:
+ * q - ro is q + (-ro) in IEEE arithmetic, and ro / -ro differ only in the sign bit of the high
+ * word, so one 32-bit select replaces the two 64-bit ones.  Then the peak: `aq > pk ? aq : pk`
+ * equals fmax(pk, aq) here, because pk never holds a NaN and fmax returns the number when aq is
+ * NaN (the reference's `cv > pv` is false for a NaN as well, sound_render.c:770-779). */
+__device__ __forceinline__ double icw_round_q(double q, double round_offset, int sign_delta, int &delta)
+{
+    const bool neg = q < 0.0;
+    const unsigned long long rb = (unsigned long long)__double_as_longlong(round_offset);
+    const unsigned hi = (unsigned)(rb >> 32) ^ (neg ? 0x80000000u : 0u);
+    delta = neg ? sign_delta : 0;
+    return q + __longlong_as_double((long long)(((unsigned long long)hi << 32) | (rb & 0xffffffffull)));
+}
+
+/* The clip stage of sound_render_value (sound_render.c:782-797) as it reaches the integer:
+ * q >= hi -> hi - 1, q <= lo -> lo + 1, then (int) truncation.  hi and lo are integers (hi >= 1,
+ * lo <= -2), so for q in [hi-1, hi) the reference keeps q and truncates it to hi - 1, and for q in
+ * (lo, lo+1] to lo + 1: min(q, hi - 1) / max(., lo + 1) give the same integer for every q, with
+ * two instructions on the render's serial chain instead of two compares and four selects.  The
+ * clip counts come from the same comparisons, off the chain.  A NaN q is the caller's case. */
+__device__ __forceinline__ int icw_clamp_int(double q, const IcwRenderK &k, unsigned &clips)
+{
+    clips += (q >= k.hi ? 1u : 0u) + (q <= k.lo ? 1u : 0u);
+    return (int)fmax(fmin(q, k.hi - 1.0), k.lo + 1.0);
+}
+
 /* sound_render_value for ROUND render + flat shaper (sound_render.c:691-809): elementwise */
 __device__ __forceinline__ int icw_render_round(double input, const IcwRenderK &k, unsigned &clips, double &pk)
 {
     input = (input * k.norm_mul) - 0.0;           /* prev_ns_err == 0.0 for the flat shaper */
     double q = input + (0.0 * k.dth_mul);         /* rnd_dth == 0.0 for ROUND */
     int delta;
-    if (q < 0.0) { q -= k.round_offset; delta = k.sign_delta; }
-    else { q += k.round_offset; delta = 0; }
-    const double aq = fabs(q);
-    pk = aq > pk ? aq : pk;
-    if (q >= k.hi) { q = k.hi - 1.0; ++clips; }
-    if (q <= k.lo) { q = k.lo + 1.0; ++clips; }
+    q = icw_round_q(q, k.round_offset, k.sign_delta, delta);
+    pk = fmax(pk, fabs(q));
     /* x86 cvttsd2si semantics: NaN -> INT_MIN ("integer indefinite") */
-    int v = isnan(q) ? (int)0x80000000 : (int)q;
+    const int vc = icw_clamp_int(q, k, clips);    /* unconditional: a NaN counts no clip */
+    int v = isnan(q) ? (int)0x80000000 : vc;
     return (v + delta) << k.norm_shift;
 }
 
@@ -1051,13 +1074,10 @@ __device__ __forceinline__ int icw_render_step(double input, double d, double &p
     input = (input * k.norm_mul) - prev_err;
     double q = input + d;
     int delta;
-    if (q < 0.0) { q -= k.round_offset; delta = k.sign_delta; }
-    else { q += k.round_offset; delta = 0; }
-    const double aq = fabs(q);
-    pk = aq > pk ? aq : pk;
-    if (q >= k.hi) { q = k.hi - 1.0; ++clips; }
-    if (q <= k.lo) { q = k.lo + 1.0; ++clips; }
-    int val = (isnan(q) ? (int)0x80000000 : (int)q) + delta;
+    q = icw_round_q(q, k.round_offset, k.sign_delta, delta);
+    pk = fmax(pk, fabs(q));
+    const int vc = icw_clamp_int(q, k, clips);    /* unconditional: a NaN counts no clip */
+    int val = (isnan(q) ? (int)0x80000000 : vc) + delta;
     /* noise shaping for the next sample (ns_empty / ns_fir / ns_iir) */
     const double ev = (double)val - input;
     double res = 0.0;
