@@ -182,6 +182,7 @@ struct IcwK2Args {
     const double *trig_tab;        /* nullable [T][trig_pitch]: (cos, sin) per active Shift / PM channel
                                       for streams whose call-start counter equals stream 0's */
     int32_t trig_pitch;
+    int32_t zero;                  /* always 0: an offset the compiler cannot fold (keeps loads in a loop) */
 };
 
 /* Per-frame rotation table (one thread per frame): the Shift / PM factors depend only on the frame

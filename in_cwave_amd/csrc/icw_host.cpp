@@ -48,6 +48,7 @@ double u2d(unsigned long long u)
 /* frames per kernel launch: bounds the w scratch buffer (n_chains * (T+N) doubles) */
 constexpr int kMaxBlockFrames = 1 << 16;
 constexpr int kDefBlockFrames = 1 << 14;   /* launch block: shorter pipeline fill / drain */
+constexpr int kSets = 3;                    /* most block scratch sets (ICW_SETS); default 2 */
 
 struct DevState {
     double *hist = nullptr;               /* [chains][20] */
@@ -92,25 +93,26 @@ struct icw_ctx {
     /* scratch */
     /* double-buffered block scratch: block b uses set b & 1, so the output kernel of block b
      * (second stream) overlaps the IIR state kernel of block b+1 */
-    double *w[2] = {nullptr, nullptr};
-    size_t w_bytes[2] = {0, 0};
-    double *xd[2] = {nullptr, nullptr};
-    size_t xd_bytes[2] = {0, 0};
-    uint32_t *info_dup[2] = {nullptr, nullptr};
+    double *w[kSets] = {};
+    size_t w_bytes[kSets] = {};
+    double *xd[kSets] = {};
+    size_t xd_bytes[kSets] = {};
+    uint32_t *info_dup[kSets] = {};
     hipStream_t stream2 = nullptr;
-    hipEvent_t k1done[2] = {nullptr, nullptr}, k2done[2] = {nullptr, nullptr}, join = nullptr;
-    hipEvent_t k0done[2] = {nullptr, nullptr};
+    hipEvent_t k1done[kSets] = {}, k2done[kSets] = {}, join = nullptr;
+    hipEvent_t k0done[kSets] = {};
     std::vector<CuSplit> splits;          /* cached CU-partitioned stream sets, by K1 CU count */
     bool cu_split = true;                 /* ICW_CU_SPLIT=0 disables the partition */
     int k1_wpc = 4;                       /* ICW_K1_WPC: K1 waves per CU (one per SIMD) */
     int k1_wg = 1;                        /* ICW_K1_WG: K1 waves per workgroup */
     int max_block = kDefBlockFrames;      /* ICW_BLOCK: frames per launch block */
     bool dedup_ok = true;                 /* ICW_DEDUP=0 disables the mono K1 dedup (A/B) */
+    int max_sets = 2;                     /* ICW_SETS: block scratch sets (2..kSets) */
     /* dither generation (K3a) runs on its own stream, double-buffered like the block scratch */
     hipStream_t stream3 = nullptr;
-    hipEvent_t ditdone[2] = {nullptr, nullptr};
-    double *dith[2] = {nullptr, nullptr};
-    size_t dith_bytes[2] = {0, 0};
+    hipEvent_t ditdone[kSets] = {};
+    double *dith[kSets] = {};
+    size_t dith_bytes[kSets] = {};
     unsigned char *d_in = nullptr, *d_out = nullptr;
     size_t d_in_bytes = 0, d_out_bytes = 0;
     double *d_pre = nullptr;
@@ -427,17 +429,17 @@ void free_all(icw_ctx *c)
 {
     DevState &s = c->st;
     void *ptrs[] = {s.mt, s.mt_idx, s.rs, s.lr_equal, c->rpre, c->iq, s.err, s.hist, s.sncnt, s.hq_phase, s.pos, s.fade,
-                    s.n_frame, s.bus, s.clips, s.peak_bits, c->d_prog, c->info_dup[0], c->info_dup[1], c->w[0], c->w[1], c->trig,
-                    c->xd[0], c->xd[1], c->d_in, c->d_out, c->d_pre};
+                    s.n_frame, s.bus, s.clips, s.peak_bits, c->d_prog, c->trig, c->d_in, c->d_out, c->d_pre};
     for (void *p : ptrs)
         if (p) hipFree(p);
-    for (double *d : {c->dith[0], c->dith[1]})
-        if (d) hipFree(d);
-    for (hipEvent_t e : {c->ditdone[0], c->ditdone[1]})
-        if (e) hipEventDestroy(e);
+    for (int p = 0; p < kSets; ++p) {
+        for (void *q : {(void *)c->info_dup[p], (void *)c->w[p], (void *)c->xd[p], (void *)c->dith[p]})
+            if (q) hipFree(q);
+        for (hipEvent_t e : {c->ditdone[p], c->k1done[p], c->k2done[p], c->k0done[p]})
+            if (e) hipEventDestroy(e);
+    }
     if (c->stream3) hipStreamDestroy(c->stream3);
-    for (hipEvent_t e : {c->k1done[0], c->k1done[1], c->k2done[0], c->k2done[1], c->k0done[0], c->k0done[1], c->join})
-        if (e) hipEventDestroy(e);
+    if (c->join) hipEventDestroy(c->join);
     for (auto &x : c->splits)
         for (hipStream_t q : {x.k1, x.rest, x.dith})
             if (q) hipStreamDestroy(q);
@@ -545,14 +547,14 @@ int icw_create(const icw_config *cfg, const icw_node *nodes, int n_nodes, int n_
         rc |= dalloc(&s.rs, S * 2 * ICW_RSTATE);
     }
     rc |= dalloc(&s.lr_equal, S * 2);
-    for (int p = 0; p < 2; ++p) rc |= dalloc(&c->info_dup[p], S * 2);
+    for (int p = 0; p < kSets; ++p) rc |= dalloc(&c->info_dup[p], S * 2);
     rc |= dalloc(&c->d_prog, 1);
     if (rc == ICW_OK && hipMemcpy(c->d_prog, &c->prog, sizeof(IcwProg), hipMemcpyHostToDevice) != hipSuccess)
         rc = ICW_EDEVICE;
     if (rc == ICW_OK && hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) rc = ICW_EDEVICE;
     if (rc == ICW_OK && hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking) != hipSuccess) rc = ICW_EDEVICE;
     if (rc == ICW_OK && hipStreamCreateWithFlags(&c->stream3, hipStreamNonBlocking) != hipSuccess) rc = ICW_EDEVICE;
-    for (int p = 0; p < 2 && rc == ICW_OK; ++p)
+    for (int p = 0; p < kSets && rc == ICW_OK; ++p)
         if (hipEventCreateWithFlags(&c->k1done[p], hipEventDisableTiming) != hipSuccess ||
             hipEventCreateWithFlags(&c->k2done[p], hipEventDisableTiming) != hipSuccess ||
             hipEventCreateWithFlags(&c->ditdone[p], hipEventDisableTiming) != hipSuccess ||
@@ -590,6 +592,8 @@ int icw_create(const icw_config *cfg, const icw_node *nodes, int n_nodes, int n_
         if (wpc && atoi(wpc) >= 1 && atoi(wpc) <= 8) c->k1_wpc = atoi(wpc);
         const char *bl = getenv("ICW_BLOCK");
         if (bl && atoi(bl) >= 256 && atoi(bl) <= kMaxBlockFrames) c->max_block = atoi(bl);
+        const char *ns = getenv("ICW_SETS");
+        if (ns && atoi(ns) >= 2 && atoi(ns) <= kSets) c->max_sets = atoi(ns);
         const char *dd = getenv("ICW_DEDUP");
         if (dd && !strcmp(dd, "0")) c->dedup_ok = false;
         const char *wg = getenv("ICW_K1_WG");
@@ -789,7 +793,7 @@ int icw_process_streams(icw_ctx *c, int first, int count, const void *in, size_t
     const size_t w_pitch = (size_t)Tb + N + 1;
     const size_t x_pitch = ((size_t)Tb + ICW_MAX_IIR_ORDER + 2) & ~(size_t)1;   /* look-ahead pad */
     const int n_blocks = (n_frames + Tb - 1) / Tb;
-    const int n_sets = n_blocks > 1 ? 2 : 1;
+    const int n_sets = std::min(n_blocks, c->max_sets);
     for (int p = 0; p < n_sets; ++p) {
         if (grow((void **)&c->w[p], &c->w_bytes[p], S * 4 * w_pitch * sizeof(double))) return ICW_ENOMEM;
         if (grow((void **)&c->xd[p], &c->xd_bytes[p], S * 4 * x_pitch * sizeof(double))) return ICW_ENOMEM;
@@ -850,7 +854,7 @@ int icw_process_streams(icw_ctx *c, int first, int count, const void *in, size_t
     /* K0 of block b on sA: xd[p] was last read by K1 of block b-2 (and, complex input, by K2 of
      * block b-2, which precedes it on sA) */
     auto launch_k0 = [&](int b) -> int {
-        const int t0 = b * Tb, T = std::min(Tb, n_frames - t0), p = b & (n_sets - 1);
+        const int t0 = b * Tb, T = std::min(Tb, n_frames - t0), p = b % n_sets;
         IcwK0Args a0;
         memset(&a0, 0, sizeof(a0));
         a0.in = d_in + (size_t)t0 * fsz;
@@ -868,24 +872,23 @@ int icw_process_streams(icw_ctx *c, int first, int count, const void *in, size_t
         a0.xd = c->xd[p];
         a0.x_pitch = x_pitch;
         a0.dedup = dedup ? 1 : 0;
-        if (b >= 2 && !cw && sK != sA && hipStreamWaitEvent(sA, c->k1done[p], 0) != hipSuccess) return ICW_EDEVICE;
+        if (b >= n_sets && !cw && sK != sA && hipStreamWaitEvent(sA, c->k1done[p], 0) != hipSuccess) return ICW_EDEVICE;
         if (icw_launch_unpack(&a0, sA) != hipSuccess) return ICW_EDEVICE;
         if (hipEventRecord(c->k0done[p], sA) != hipSuccess) return ICW_EDEVICE;
         return ICW_OK;
     };
 
-    /* Real input: K0(b+2) is queued on sA right after K1(b) (it reuses K1(b)'s xd buffer) and
-     * before K2(b), so it runs beside K1(b+1) and is done long before K1(b+2) needs it; queued
-     * behind K2(b+1) instead, it would sit between two recurrences whenever K2 is as long as K1.
-     * Complex input: K2(b) reads K0(b)'s rows, so K0(b+1) goes before K2(b) as usual. */
-    int rc0 = launch_k0(0);
-    if (rc0) return rc0;
-    if (!cw && n_blocks > 1 && (rc0 = launch_k0(1)) != ICW_OK) return rc0;
+    /* n_sets scratch sets (2 by default, ICW_SETS=3): K0 of the first n_sets blocks is queued up
+     * front, K0(b + n_sets) as soon as its xd set is free (below); K1(b + n_sets) reuses the w /
+     * info_dup set that K2(b) read and waits for it.  Three sets measured slower for large
+     * batches (C3: K1 3.96 vs 3.16 ms per launch), so two is the default. */
+    int rc0 = ICW_OK;
+    for (int b = 0; b < n_sets; ++b)
+        if ((rc0 = launch_k0(b)) != ICW_OK) return rc0;
     for (int b = 0; b < n_blocks; ++b) {
         const int t0 = b * Tb;
         const int T = std::min(Tb, n_frames - t0);
-        const int p = b & (n_sets - 1);
-        if (cw && b + 1 < n_blocks && (rc0 = launch_k0(b + 1)) != ICW_OK) return rc0;
+        const int p = b % n_sets;
 
         if (!cw) {
             IcwK1Args a1;
@@ -910,7 +913,7 @@ int icw_process_streams(icw_ctx *c, int first, int count, const void *in, size_t
             a1.dedup = dedup ? 1 : 0;
             /* K0(b) done, and K2(b-2), the last reader of w[p] / info_dup[p] */
             if (sK != sA && hipStreamWaitEvent(sK, c->k0done[p], 0) != hipSuccess) return ICW_EDEVICE;
-            if (b >= 2 && sK != sA && hipStreamWaitEvent(sK, c->k2done[p], 0) != hipSuccess) return ICW_EDEVICE;
+            if (b >= n_sets && sK != sA && hipStreamWaitEvent(sK, c->k2done[p], 0) != hipSuccess) return ICW_EDEVICE;
             if (timing) hipEventRecord(c->ev[4 * b], sK);
             const hipError_t e1 = c->k1_mode == 2 ? icw_launch_iir_mfma(&a1, N, cfg.iir_kahan, cfg.iir_subnorm_reject, sK)
                                 : c->k1_mode == 1 ? icw_launch_iir_pair(&a1, N, cfg.iir_kahan, cfg.iir_subnorm_reject, sK)
@@ -919,7 +922,9 @@ int icw_process_streams(icw_ctx *c, int first, int count, const void *in, size_t
             if (timing) hipEventRecord(c->ev[4 * b + 1], sK);
             if (hipEventRecord(c->k1done[p], sK) != hipSuccess) return ICW_EDEVICE;
             if (sK != sA && hipStreamWaitEvent(sA, c->k1done[p], 0) != hipSuccess) return ICW_EDEVICE;
-            if (b + 2 < n_blocks && (rc0 = launch_k0(b + 2)) != ICW_OK) return rc0;
+            /* real input: K0(b + n_sets) reuses xd[p], which K1(b) read; queued before K2(b) it
+             * runs beside K1(b+1) instead of between two recurrences */
+            if (b + n_sets < n_blocks && (rc0 = launch_k0(b + n_sets)) != ICW_OK) return rc0;
         } else if (timing) {
             hipEventRecord(c->ev[4 * b], sA);
             hipEventRecord(c->ev[4 * b + 1], sA);
@@ -1022,7 +1027,7 @@ int icw_process_streams(icw_ctx *c, int first, int count, const void *in, size_t
                 /* K3a for this block on its own stream: dith[p] was last read by K3b of block b-2 */
                 a3.dith = c->dith[p];
                 a3.dith_pitch = (size_t)count * 2;    /* time-major [T][count*2] */
-                if (b >= 2 && sD != sA && hipStreamWaitEvent(sD, c->k2done[p], 0) != hipSuccess) return ICW_EDEVICE;
+                if (b >= n_sets && sD != sA && hipStreamWaitEvent(sD, c->k2done[p], 0) != hipSuccess) return ICW_EDEVICE;
                 const hipError_t ed = c->dither_lane ? icw_launch_dither_lane(&a3, sD) : icw_launch_dither(&a3, sD);
                 if (ed != hipSuccess || hipEventRecord(c->ditdone[p], sD) != hipSuccess ||
                     (sD != sA && hipStreamWaitEvent(sA, c->ditdone[p], 0) != hipSuccess))
@@ -1032,6 +1037,8 @@ int icw_process_streams(icw_ctx *c, int first, int count, const void *in, size_t
         }
         if (timing) hipEventRecord(c->ev[4 * b + 3], sA);
         if (hipEventRecord(c->k2done[p], sA) != hipSuccess) return ICW_EDEVICE;
+        /* complex input: K0(b + n_sets) reuses xd[p], which K2(b) read */
+        if (cw && b + n_sets < n_blocks && (rc0 = launch_k0(b + n_sets)) != ICW_OK) return rc0;
     }
     if (!cw && nch > 1)
         for (int i = 0; i < count; ++i) c->lr_known[first + i] = 0;   /* stereo: the halves diverge */

@@ -160,8 +160,8 @@ struct IcwLR { double lre, lim, rre, rim; };
  * term of all NC chains instead of across NC whole sums (with the chains back to back, all 2N
  * coefficients stay live in SGPRs and spill to VGPR lanes -- a v_readlane per use) */
 template <int N, bool KAHAN, int NC>
-__device__ __forceinline__ void icw_iir_out_n(const double *const (&win)[NC], const double (&pc)[20],
-                                              const double (&pd)[20], double d0, double (&y)[NC])
+__device__ __forceinline__ void icw_iir_out_n(const double *const (&win)[NC], const double *pc, const double *pd,
+                                              double d0, double (&y)[NC])
 {
     if (KAHAN) {
         double S[NC], C[NC];
@@ -453,9 +453,12 @@ __global__ __launch_bounds__(ICW_K2_TILE) void icw_output(IcwK2Args a)
         IcwLR v; v.lre = b[0]; v.lim = b[1]; v.rre = b[2]; v.rim = b[3];
         R.set(P->persist_reg[r], v);
     }
-    double pc[20], pd[20];
-#pragma unroll
-    for (int i = 0; i < 20; ++i) { pc[i] = a.pc[i]; pd[i] = a.pd[i]; }
+    /* the 2N output-sum coefficients are read from LDS (broadcast) at their one use per frame:
+     * held in SGPRs they crowd out the program's operands and spill to VGPR lanes, a v_readlane
+     * per use.  `zk` (a runtime zero) keeps the loads inside the tile loop. */
+    __shared__ double lcoef[40];
+    if (tl < 40) lcoef[tl] = tl < 20 ? a.pc[tl] : a.pd[tl - 20];
+    __syncthreads();
 
     unsigned clip_l = 0, clip_r = 0;
     double pk_l = 0.0, pk_r = 0.0;
@@ -468,6 +471,7 @@ __global__ __launch_bounds__(ICW_K2_TILE) void icw_output(IcwK2Args a)
         if (more) load_tile(k + 1);
         const int t = tw0 + k * TILE + tl;
         const double (&W)[4][TILE + 24] = lw[k & 1];
+        const int zk = a.zero * k;
         if (t < T) {
             IcwLR in;
             if (a.cw) {
@@ -485,12 +489,12 @@ __global__ __launch_bounds__(ICW_K2_TILE) void icw_output(IcwK2Args a)
                 if (dup) {
                     const double *const wins[2] = {&W[0][tl], &W[1][tl]};
                     double y2[2];
-                    icw_iir_out_n<N, KAHAN, 2>(wins, pc, pd, a.d0, y2);
+                    icw_iir_out_n<N, KAHAN, 2>(wins, lcoef + zk, lcoef + 20 + zk, a.d0, y2);
                     y[0] = y[2] = y2[0];
                     y[1] = y[3] = y2[1];
                 } else {
                     const double *const wins[4] = {&W[0][tl], &W[1][tl], &W[2][tl], &W[3][tl]};
-                    icw_iir_out_n<N, KAHAN, 4>(wins, pc, pd, a.d0, y);
+                    icw_iir_out_n<N, KAHAN, 4>(wins, lcoef + zk, lcoef + 20 + zk, a.d0, y);
                 }
                 /* fs/4 un-mix (lpf_hilbert_quad.c:129-156) */
                 double oI[2], oQ[2];
