@@ -260,3 +260,31 @@ def test_zero_input_fast_path_mixed_phases(oracle, icw):
         ro, rp = sts[s].process(raw2[s], 3000, want_pre=True)
         assert np.array_equal(pre[s].view(np.uint64), rp.view(np.uint64)), s
         assert np.array_equal(out[s], ro), s
+
+
+@pytest.mark.parametrize("streams,ch", [(4096, 1), (2048, 2)])
+def test_large_batch_sampled_against_oracle(oracle, icw, streams, ch):
+    """BASELINE C3 / C4 shard sizes (4096 mono, 2048 stereo streams per GPU) on a short run: many
+    lane groups, the mono dedup, several CU-partitioned K1 workgroups.  A sample of streams from
+    the start, the middle, the last lane group and the very end is checked bit for bit."""
+    fs = 96000 if ch == 1 else 48000
+    cfg = graph.default_config(fs, channels=ch)
+    nodes = graph.graph_master_only() if ch == 1 else graph.graph_shift_master()
+    n = 1200
+    gen = synth.batch_pcm(8, n, fs, channels=ch)          # 8 generated streams tiled over the batch
+    raw = np.ascontiguousarray(np.tile(gen, (streams // 8, 1)))
+    ctx = icw.Context(cfg, nodes, streams)
+    out, pre = ctx.process(raw, n, want_pre=True)
+    for s in (0, 1, 7, streams // 2 + 3, streams - 33, streams - 1):
+        st = oracle.Stream(cfg, nodes)
+        ro, rp = st.process(raw[s], n, want_pre=True)
+        if ch == 1:
+            assert np.array_equal(pre[s].view(np.uint64), rp.view(np.uint64)), s
+            assert np.array_equal(out[s], ro), s
+        else:
+            rel = np.abs(pre[s] - rp) / np.maximum(np.abs(rp), 1.0)
+            assert rel.max() <= REL_TOL, s
+            same = pre[s].view(np.uint64) == rp.view(np.uint64)
+            assert np.array_equal(out[s].reshape(n, 2, 2)[same], ro.reshape(n, 2, 2)[same]), s
+    # streams built from the same generated row produce the same bytes
+    assert np.array_equal(out[3], out[3 + 8 * (streams // 16)])
