@@ -37,7 +37,11 @@ CLOCK_GHZ = 2.4                # MI355X max engine clock (MI355X_MICROARCH.md ch
 # recurrence compiles to 91 FP64 VALU per sample on average (71 v_add_f64 + 19 v_mul_f64 + 1
 # v_cmp_f64: the order-19 Kahan loop-back sum with the zero-input steps 4 adds shorter, ISA of
 # icw_iir_state<19,1,1>) plus 2 v_cndmask_b32 -> a floor of ~455 cycles per sample per chain.
-K1_VALU_PER_SAMPLE = 91
+# The row-broadcast kernel icw_iir_row<19> (small batches: C2) issues 75.5 FP64 VALU per sample:
+# nonzero-input samples 1 + 3 + (18 v_fmac_f64_dpp + 52 v_add_f64) + 1 v_cmp + 2 product muls = 77,
+# zero-input samples 2 + 3 + (17 + 49) + 1 + 2 = 74 (plus 2 v_cndmask_b32, as above).
+K1_VALU_PER_SAMPLE = {0: 91, 3: 75.5}          # by ICW_K1_* (icw_last_k1_kernel)
+K1_KERNEL_NAME = {0: "icw_iir_state", 1: "icw_iir_pair", 2: "icw_iir_state_mf", 3: "icw_iir_row"}
 CYC_PER_FP64_VALU = 5.0
 PMC_FILE = ROOT / "profiles" / "r01_c2_pmc.json"
 FP64_PEAK_TFLOPS = 78.6        # MI355X FP64 vector (256 CU x 2.4 GHz x 128 flop/clk), vendor figure
@@ -199,29 +203,33 @@ def main():
     alg_bytes = W["bytes"]
     achieved = alg_bytes * frames_per_launch / k1_avg_s / 1e9 if k1_avg_s > 0 else None
     flops_per_frame = 4 * 2 * (15 * 19 - 4) / 2    # the recurrence half of 1124 flops/frame
+    k1_kind = ctx.last_k1_kernel()
+    k1_name = K1_KERNEL_NAME.get(k1_kind, "?")
+    valu = K1_VALU_PER_SAMPLE.get(k1_kind)
     traffic = None
     try:   # HBM bytes per launch of the same kernel/config from the committed PMC passes
         pmc = json.loads(PMC_FILE.read_text())
         if int(pmc["frames_per_launch"]) == int(frames_per_launch) and a.workload == "c2":
-            traffic = next(v["hbm_bytes_corrected"] for k, v in pmc["kernels"].items() if "icw_iir_state" in k)
+            traffic = next(v["hbm_bytes_corrected"] for k, v in pmc["kernels"].items()
+                           if k.split("<")[0].split("(")[0].endswith(k1_name))
     except Exception:
         traffic = None
     samples_per_chain = frames_per_launch / S
-    issue_floor_ms = samples_per_chain * K1_VALU_PER_SAMPLE * CYC_PER_FP64_VALU / (CLOCK_GHZ * 1e6)
+    issue_floor_ms = (samples_per_chain * valu * CYC_PER_FP64_VALU / (CLOCK_GHZ * 1e6)) if valu else None
     roof = {
         "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
         "frac": (achieved / HBM_PEAK_GBS) if achieved else None, "traffic": traffic,
-        "issue_bound": {"valu_per_sample": K1_VALU_PER_SAMPLE, "cycles_per_valu": CYC_PER_FP64_VALU,
+        "issue_bound": {"valu_per_sample": valu, "cycles_per_valu": CYC_PER_FP64_VALU,
                         "clock_ghz": CLOCK_GHZ, "floor_ms_per_launch": issue_floor_ms,
-                        "frac": (issue_floor_ms / (k1_avg_s * 1e3)) if k1_avg_s else None},
-        "kernel": "icw_iir_state", "alg_bytes_per_frame": alg_bytes,
+                        "frac": (issue_floor_ms / (k1_avg_s * 1e3)) if (k1_avg_s and issue_floor_ms) else None},
+        "kernel": k1_name, "alg_bytes_per_frame": alg_bytes,
         "frames_per_launch": frames_per_launch, "avg_launch_ms": k1_avg_s * 1e3,
         "output_kernel_avg_launch_ms": k2_avg_s * 1e3,
         "fp64_tflops_chain": (1124.0 * frames_per_launch / (k1_avg_s + k2_avg_s) / 1e12) if k1_avg_s else None,
         "fp64_peak_tflops": FP64_PEAK_TFLOPS,
-        "note": f"issue-bound serial IIR recurrence: one lane per DF-II chain ({4 * S} chains, 2 per stream "
-                f"with the mono dedup), {K1_VALU_PER_SAMPLE} FP64 VALU per sample; frac ~1 = at the issue floor "
-                f"within the probe's few-% spread (DESIGN.md)",
+        "note": f"issue-bound serial IIR recurrence ({4 * S} DF-II chains, 2 per stream with the mono dedup; "
+                f"{'one 16-lane DPP row' if k1_kind == 3 else 'one lane'} per chain), {valu} FP64 VALU per "
+                f"sample; frac ~1 = at the issue floor within the probe's few-% spread (DESIGN.md)",
     }
     del flops_per_frame
 

@@ -26,6 +26,7 @@ extern "C" hipError_t icw_launch_unpack(const IcwK0Args *a, hipStream_t st);
 extern "C" hipError_t icw_launch_iir_pair(const IcwK1Args *a, int nord, int kahan, int subn, hipStream_t st);
 extern "C" hipError_t icw_launch_iir_state(const IcwK1Args *a, int nord, int kahan, int subn, hipStream_t st);
 extern "C" hipError_t icw_launch_iir_mfma(const IcwK1Args *a, int nord, int kahan, int subn, hipStream_t st);
+extern "C" hipError_t icw_launch_iir_row(const IcwK1Args *a, int nord, int kahan, int subn, hipStream_t st);
 extern "C" hipError_t icw_launch_render(const IcwK3Args *a, hipStream_t st);
 extern "C" hipError_t icw_launch_dither(const IcwK3Args *a, hipStream_t st);
 extern "C" hipError_t icw_launch_dither_lane(const IcwK3Args *a, hipStream_t st);
@@ -132,11 +133,13 @@ struct icw_ctx {
     hipStream_t stream = nullptr;
     std::vector<hipEvent_t> ev;
     int n_cu = 256;
-    int k1_mode = 0;          /* K1 variant: 0 plain lanes, 1 chain+helper wave pairs, 2 MFMA product feed */
+    int k1_mode = -1;         /* K1 variant: -1 auto (row / plain), 0 plain lanes, 1 chain+helper wave
+                                 pairs, 2 MFMA product feed, 3 row broadcast (ICW_K1_MODE) */
     bool dither_lane = false; /* ICW_DITHER=lane: lane-per-channel dither generator (A/B only) */
     bool serialize = false;   /* ICW_SERIALIZE=1: every kernel on the caller's stream (profiling) */
     double last_ms[2]{};
     int last_launches[2]{};
+    int last_k1 = -1;                     /* ICW_K1_* of the last real-input call */
     std::mutex mu;
 };
 
@@ -577,11 +580,12 @@ int icw_create(const icw_config *cfg, const icw_node *nodes, int n_nodes, int n_
         /* measured (profiles/r01_*): the pair kernel's hand-off protocol still costs more than the
          * instructions it removes from the chain wave, so the plain kernel is the default */
         (void)wgs;
-        c->k1_mode = 0;
+        c->k1_mode = -1;
         const char *m = getenv("ICW_K1_MODE");
         if (m && !strcmp(m, "plain")) c->k1_mode = 0;
         if (m && !strcmp(m, "pair")) c->k1_mode = 1;
         if (m && !strcmp(m, "mfma")) c->k1_mode = 2;
+        if (m && !strcmp(m, "row")) c->k1_mode = 3;
         const char *d = getenv("ICW_DITHER");
         c->dither_lane = d && !strcmp(d, "lane");
         const char *z = getenv("ICW_SERIALIZE");
@@ -803,8 +807,17 @@ int icw_process_streams(icw_ctx *c, int first, int count, const void *in, size_t
     const bool cw = cfg.in_format >= ICW_FMT_CW_F64;
     const bool bus = c->prog.is_bus;
     /* mono dedup: every stream of the call known to hold identical left / right converters */
-    bool dedup = !cw && nch == 1 && c->dedup_ok && c->k1_mode == 0;   /* plain K1 only */
+    bool dedup = !cw && nch == 1 && c->dedup_ok && (c->k1_mode <= 0 || c->k1_mode == 3);   /* plain / row K1 */
     for (int i = 0; dedup && i < count; ++i) dedup = c->lr_known[first + i] != 0;
+    /* K1 variant of this call.  Auto: the row-broadcast kernel (4 chains per wave, ~17 % fewer
+     * instructions per sample) when its waves fit one per SIMD on at most half the chip, else the
+     * lane-per-chain kernel (64 chains per wave).  The row kernel needs Kahan + the reject. */
+    const int row_waves = (int)(((dedup ? count : 2L * count) + 3) / 4) * 2;
+    const bool row_ok = cfg.iir_kahan && cfg.iir_subnorm_reject;
+    int k1_mode = c->k1_mode;
+    if (k1_mode < 0) k1_mode = (row_ok && !c->serial_render && row_waves * 2 <= c->n_cu * 4) ? 3 : 0;
+    if (k1_mode == 3 && !row_ok) k1_mode = 0;
+    if (!cw) c->last_k1 = k1_mode;
     const bool table = c->prog.needs_omega && !bus && c->prog.n_trig > 0;
     if (table && grow((void **)&c->trig, &c->trig_bytes, (size_t)Tb * 2 * c->prog.n_trig * sizeof(double)))
         return ICW_ENOMEM;
@@ -823,8 +836,8 @@ int icw_process_streams(icw_ctx *c, int first, int count, const void *in, size_t
         sA = sD = st;
     } else if (!cw) {
         /* plain K1: 128-lane groups of 32 streams (64 with the dedup); the variants: a lane per chain */
-        const int k1_waves = c->k1_mode == 0 ? ((count + (dedup ? 63 : 31)) / (dedup ? 64 : 32)) * 2
-                                             : (count * 4 + 63) / 64;
+        const int k1_waves = k1_mode == 0 ? ((count + (dedup ? 63 : 31)) / (dedup ? 64 : 32)) * 2
+                           : k1_mode == 3 ? row_waves : (count * 4 + 63) / 64;
         const int k1_cus = (k1_waves + c->k1_wpc - 1) / c->k1_wpc;
         if (c->cu_split && k1_cus * 2 <= c->n_cu) {
             const CuSplit *cs = cu_split(c, k1_cus);
@@ -915,8 +928,9 @@ int icw_process_streams(icw_ctx *c, int first, int count, const void *in, size_t
             if (sK != sA && hipStreamWaitEvent(sK, c->k0done[p], 0) != hipSuccess) return ICW_EDEVICE;
             if (b >= n_sets && sK != sA && hipStreamWaitEvent(sK, c->k2done[p], 0) != hipSuccess) return ICW_EDEVICE;
             if (timing) hipEventRecord(c->ev[4 * b], sK);
-            const hipError_t e1 = c->k1_mode == 2 ? icw_launch_iir_mfma(&a1, N, cfg.iir_kahan, cfg.iir_subnorm_reject, sK)
-                                : c->k1_mode == 1 ? icw_launch_iir_pair(&a1, N, cfg.iir_kahan, cfg.iir_subnorm_reject, sK)
+            const hipError_t e1 = k1_mode == 3 ? icw_launch_iir_row(&a1, N, cfg.iir_kahan, cfg.iir_subnorm_reject, sK)
+                                : k1_mode == 2 ? icw_launch_iir_mfma(&a1, N, cfg.iir_kahan, cfg.iir_subnorm_reject, sK)
+                                : k1_mode == 1 ? icw_launch_iir_pair(&a1, N, cfg.iir_kahan, cfg.iir_subnorm_reject, sK)
                                                : icw_launch_iir_state(&a1, N, cfg.iir_kahan, cfg.iir_subnorm_reject, sK);
             if (e1 != hipSuccess) return ICW_EDEVICE;
             if (timing) hipEventRecord(c->ev[4 * b + 1], sK);
@@ -1227,6 +1241,12 @@ int icw_set_state(icw_ctx *c, int s, const void *blob, size_t size)
         ok &= hipMemcpy(c->st.rs + (size_t)s * 2 * ICW_RSTATE, b.rs, sizeof(b.rs), hipMemcpyHostToDevice) == hipSuccess;
     }
     return ok ? ICW_OK : ICW_EDEVICE;
+}
+
+int icw_last_k1_kernel(const icw_ctx *c)
+{
+    if (!c) return ICW_EINVAL;
+    return c->last_k1;
 }
 
 int icw_last_timing(icw_ctx *c, double ms[2], int launches[2])

@@ -278,6 +278,225 @@ __global__ __launch_bounds__(256) void icw_iir_state(IcwK1Args a)
     if (ch == 0) a.lr_equal[s * 2 + f] = eq ? 1u : 0u;
 }
 
+/* ------------------------------------------ IIR state kernel, row broadcast (K1r) -------- */
+/* The same Kahan loop-back sum (iir_rp_process_kahan, hblpf.c:1017-1046, subnorm reject on) with
+ * one DF-II chain per 16-lane DPP row instead of one per lane.  What it buys: a wave issues ~one
+ * FP64 VALU op per 5 cycles no matter how many lanes do useful work (tools/dpp_probe.hip), so the
+ * 18 products c_i * w[n-1-i] of the plain kernel (18 of its 93 instructions per sample) are
+ * replaced by ONE lane-parallel multiply per sample:
+ *
+ *   - every lane of a row runs the chain's Kahan sequence redundantly, so w[n] is row-uniform;
+ *   - right after w[n] is known, lane l computes P[n mod N] = c[l+1] * w[n]: term i = l+1 of the
+ *     sample n+1+i.  Terms 17..19 (orders 18..20) use a second register P2 (lanes 0..3);
+ *   - term i's step Y = t_i - C takes t_i straight from lane i-1 of the row through
+ *     `v_fmac_f64_dpp ... row_newbcast:(i-1)` as Y = t_i * 1.0 + NC with NC = -C: one rounding
+ *     of t_i - C, the same value (a DPP fmac issues like a v_add_f64: 20.0 cycles per Kahan step
+ *     either way, profiles/r01_dpp_probe.txt);
+ *   - NC = Y - (T - S) is -((T - S) - Y) exactly, except that an exact-zero difference comes out
+ *     +0 on both sides: intermediate values then differ at most in the sign of a zero, which the
+ *     first nonzero term absorbs, and a sum that stays zero is rejected to +0.0 (|S| < 1,
+ *     hblpf.c:1046).  So w is bit-identical when the reject is on, the only mode this kernel runs.
+ *   - the newest term t0 = c0 * w[n-1] is on the critical path and stays a row-uniform multiply
+ *     (zero-input steps, below, also need t1 row-uniform).
+ *
+ * Per sample: 1 + P-muls (1 or 2) + 73 add/fmac + cmp + 2 cndmask, against 19 mul + 73 add + cmp +
+ * 2 cndmask; the zero-input steps (every other input of a filter is the literal +0.0,
+ * lpf_hilbert_quad.c:136-151) save 4 adds as in icw_iir_state, now for every filter order.  The
+ * price is 16 lanes per chain: 4 chains per wave.  The host takes this kernel only when the
+ * resulting waves fit one per SIMD on at most half the chip (C2, C5); bigger batches keep the
+ * lane-per-chain kernel, whose 64 chains per wave fill the chip at the issue floor. */
+
+/* Products of a new w: r = a * b.  Volatile, like the term chains (icw_row_asm.inc): program order
+ * keeps every DPP read of a product register many instructions after its write (the VALU-write
+ * -> DPP-read hazard needs two). */
+__device__ __forceinline__ double icw_vmul(double a, double b)
+{
+    double r;
+    asm volatile("v_mul_f64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+
+#include "icw_row_asm.inc"
+
+struct IcwRowC {
+    double c0, c1;      /* row-uniform: newest two loop-back coefficients */
+    double pl, pl2;     /* per lane: c[l+1], c[l+17] (0 past the order) */
+    double one;         /* 1.0 in a VGPR (VOP2 src1) */
+};
+
+/* one sample at unroll step J; zero-input step when Z != 2 and (J & 1) == Z.  Logical z_i =
+ * W[(J-1-i) mod N] (row-uniform); the new w goes to W[J] and its products to P[J] / P2[J]. */
+template <int N, int J, int Z>
+__device__ __forceinline__ void icw_row_step(double (&W)[N], double (&P)[N], double (&P2)[N], double xin,
+                                             const IcwRowC &c)
+{
+    constexpr bool ZS = Z != 2 && (J & 1) == Z;
+    double S, Y;
+    if constexpr (ZS) {
+        /* kahan_init(+0) and term 0 collapse to S = t0, C = +0; term 1's Y is t1 */
+        S = W[(J - 1 + N) % N] * c.c0;
+        Y = W[(J - 2 + 2 * N) % N] * c.c1;
+    } else {
+        S = xin;                               /* kahan_init(sample) */
+        Y = W[(J - 1 + N) % N] * c.c0;         /* term 0: t0 - 0 */
+    }
+    const double T = S + Y;
+    double NC = Y - (T - S);
+    /* terms I0..N-1: Y = t_i - C with t_i = lane i-1 of P (i-17 of P2), one asm block */
+    S = icw_row_chain<N, ZS ? 2 : 1, J>(T, NC, c.one, P, P2);
+    S = fabs(S) < 1.0 ? 0.0 : S;               /* hblpf.c:1046 */
+    W[J] = S;
+    P[J] = icw_vmul(c.pl, S);
+    if constexpr (N > 17) P2[J] = icw_vmul(c.pl2, S);
+}
+
+/* a block of N samples; xv[J] is refilled with the input N samples ahead right after step J when
+ * the next block's step J (zero parity ZN) consumes an input */
+template <int N, int J, int Z, int ZN>
+__device__ __forceinline__ void icw_row_block(double (&W)[N], double (&P)[N], double (&P2)[N], double (&xv)[N],
+                                              const double *xnext, const IcwRowC &c)
+{
+    if constexpr (J < N) {
+        icw_row_step<N, J, Z>(W, P, P2, xv[J], c);
+        if constexpr (!(ZN != 2 && (J & 1) == ZN)) xv[J] = xnext[J];
+        icw_row_block<N, J + 1, Z, ZN>(W, P, P2, xv, xnext, c);
+    }
+}
+
+template <int N, int J>
+__device__ __forceinline__ void icw_row_block_lim(double (&W)[N], double (&P)[N], double (&P2)[N],
+                                                  const double (&xv)[N], const IcwRowC &c, int lim)
+{
+    if constexpr (J < N) {
+        if (J < lim) {
+            icw_row_step<N, J, 2>(W, P, P2, xv[J], c);
+            icw_row_block_lim<N, J + 1>(W, P, P2, xv, c, lim);
+        }
+    }
+}
+
+template <int N>
+__device__ __forceinline__ void icw_row_store(const double (&W)[N], double *wo, bool writer)
+{
+    if (writer) {
+#pragma unroll
+        for (int j = 0; j < N; ++j) wo[j] = W[j];
+    }
+}
+
+/* Row layout: wave v holds filter f = v & 1 of the four chain slots 4 (v >> 1) + r, r = row;
+ * slot = 2 stream + channel (stream, left channel under the dedup).  The two channels of a
+ * stream are rows r, r ^ 1 of one wave; a wave's chains share a filter kind, hence the
+ * zero-input parity whenever their Hilbert phases agree in parity. */
+template <int N>
+__global__ __launch_bounds__(256) void icw_iir_row(IcwK1Args a)
+{
+    const int gl = blockIdx.x * blockDim.x + threadIdx.x;
+    const int wv = gl >> 6, r = (gl >> 4) & 3, lr = gl & 15;
+    const int f = wv & 1;
+    const int slot = (wv >> 1) * 4 + r;
+    const bool dedup = a.dedup != 0;
+    const int s = dedup ? slot : (slot >> 1), ch = dedup ? 0 : (slot & 1);
+    if (s >= a.n_streams) return;
+    const int g = s * 4 + ch * 2 + f;
+    const bool writer = lr == 0;
+
+    IcwRowC c;
+    c.c0 = a.pc[0];
+    c.c1 = a.pc[1];
+    c.pl = (lr + 1 < N) ? a.pc[lr + 1] : 0.0;
+    c.pl2 = (lr + 17 < N) ? a.pc[lr + 17] : 0.0;
+    c.one = 1.0;
+
+    double W[N], P[N], P2[N];
+#pragma unroll
+    for (int i = 0; i < N; ++i) W[N - 1 - i] = a.hist[(size_t)g * ICW_HIST_PITCH + i];
+    if constexpr (N > 17) {
+#pragma unroll
+        for (int k = 0; k < N; ++k) P2[k] = icw_vmul(c.pl2, W[k]);
+    }
+#pragma unroll
+    for (int k = 0; k < N; ++k) P[k] = icw_vmul(c.pl, W[k]);
+    asm volatile("s_nop 1");
+
+    if (writer && ch == 0) a.info_dup[s * 2 + f] = a.lr_equal[s * 2 + f];
+    const double *xp = a.xd + (size_t)g * a.x_pitch;
+    double *wrow = a.w + (size_t)g * a.w_pitch;
+    icw_row_store<N>(W, wrow, writer);
+
+    const int T = a.T;
+    int t = 0;
+    if (T >= N) {
+        double xv[N];
+        icw_load_x<N>(xv, xp);
+        /* block-relative sample n has a zero input iff (phi + n) is odd (see icw_iir_state) */
+        const unsigned phi = (a.hq_phase[s * 2 + ch] + (unsigned)a.t0 + (unsigned)f) & 1u;
+        const unsigned phi0 = __builtin_amdgcn_readfirstlane(phi);
+        if (__all(phi == phi0) && T >= 3 * N) {
+            if constexpr (N & 1) {
+                /* odd order: the zero parity alternates block to block */
+                if (phi0) {
+                    icw_row_block<N, 0, 0, 1>(W, P, P2, xv, xp + t + N, c);
+                    icw_row_store<N>(W, wrow + N + t, writer);
+                    t += N;
+                }
+                for (; t + 2 * N <= T; t += 2 * N) {
+                    icw_row_block<N, 0, 1, 0>(W, P, P2, xv, xp + t + N, c);
+                    icw_row_store<N>(W, wrow + N + t, writer);
+                    icw_row_block<N, 0, 0, 1>(W, P, P2, xv, xp + t + 2 * N, c);
+                    icw_row_store<N>(W, wrow + 2 * N + t, writer);
+                }
+            } else if (phi0) {
+                /* even order: the same zero steps in every block */
+                for (; t + N <= T; t += N) {
+                    icw_row_block<N, 0, 0, 0>(W, P, P2, xv, xp + t + N, c);
+                    icw_row_store<N>(W, wrow + N + t, writer);
+                }
+            } else {
+                for (; t + N <= T; t += N) {
+                    icw_row_block<N, 0, 1, 1>(W, P, P2, xv, xp + t + N, c);
+                    icw_row_store<N>(W, wrow + N + t, writer);
+                }
+            }
+            icw_load_x<N>(xv, xp + t);   /* the zero steps left part of xv unloaded */
+        }
+        for (; t + N <= T; t += N) {
+            icw_row_block<N, 0, 2, 2>(W, P, P2, xv, xp + t + N, c);
+            icw_row_store<N>(W, wrow + N + t, writer);
+        }
+    }
+    const int rem = T - t;
+    if (rem > 0) {
+        double xv[N];
+#pragma unroll
+        for (int j = 0; j < N; ++j) xv[j] = (j < rem) ? xp[t + j] : 0.0;
+        icw_row_block_lim<N, 0>(W, P, P2, xv, c, rem);
+        if (writer) {
+            double *wo = wrow + N + t;
+#pragma unroll
+            for (int j = 0; j < N; ++j)
+                if (j < rem) wo[j] = W[j];
+        }
+        icw_normalise_ring<N>(W, rem);
+    }
+    if (writer) {
+        icw_store_hist<N, 0>(W, a.hist, g, a.n_chains);
+        if (dedup) icw_store_hist<N, 0>(W, a.hist, g + 2, a.n_chains);
+    }
+    if (dedup) {
+        if (writer) a.lr_equal[s * 2 + f] = 1u;
+        return;
+    }
+    /* right converter still bit-identical to the left one?  Its row is r ^ 1 (lane ^ 16) */
+    bool eq = true;
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+        const double o = __shfl_xor(W[i], 16);
+        eq = eq && (__double_as_longlong(o) == __double_as_longlong(W[i]));
+    }
+    if (writer && ch == 0) a.lr_equal[s * 2 + f] = eq ? 1u : 0u;
+}
+
 /* ------------------------------------------- IIR state kernel, MFMA product feed (K1m) ---- */
 /* Same recurrence as icw_iir_state, but the products c_i * w[n-1-i], i >= 1, which are off the
  * critical path, come from the matrix core instead of the chain's own VALU issue slots.  A wave
@@ -799,6 +1018,30 @@ extern "C" hipError_t icw_launch_iir_pair(const IcwK1Args *a, int nord, int kaha
     case 18: return launch_k1p_n<18>(*a, kahan, subn, st);
     case 19: return launch_k1p_n<19>(*a, kahan, subn, st);
     case 20: return launch_k1p_n<20>(*a, kahan, subn, st);
+    }
+    return hipErrorInvalidValue;
+}
+
+/* K1r: four chain slots per wave and filter (see icw_iir_row); Kahan with the reject only */
+template <int N>
+static hipError_t launch_k1r_t(const IcwK1Args &a, hipStream_t st)
+{
+    const long slots = a.dedup ? a.n_streams : 2L * a.n_streams;
+    const long lanes = ((slots + 3) / 4) * 2 * 64;
+    const int tpb = 64 * a.wg_waves;
+    const int blocks = (int)((lanes + tpb - 1) / tpb);
+    hipLaunchKernelGGL((icw_iir_row<N>), dim3(blocks), dim3(tpb), 0, st, a);
+    return hipGetLastError();
+}
+
+extern "C" hipError_t icw_launch_iir_row(const IcwK1Args *a, int nord, int kahan, int subn, hipStream_t st)
+{
+    if (!kahan || !subn) return hipErrorInvalidValue;
+    switch (nord) {
+    case 15: return launch_k1r_t<15>(*a, st);
+    case 18: return launch_k1r_t<18>(*a, st);
+    case 19: return launch_k1r_t<19>(*a, st);
+    case 20: return launch_k1r_t<20>(*a, st);
     }
     return hipErrorInvalidValue;
 }

@@ -148,6 +148,10 @@ class Context:
         buf = (C.c_uint8 * len(blob)).from_buffer_copy(blob)
         _check(self._lib.icw_set_state(self.h, s, buf, len(blob)), "icw_set_state")
 
+    def last_k1_kernel(self):
+        """ICW_K1_* of the last real-input call: 0 lane-per-chain, 1 pair, 2 MFMA, 3 row broadcast"""
+        return int(self._lib.icw_last_k1_kernel(self.h))
+
     def last_timing(self):
         ms = (C.c_double * 2)()
         n = (C.c_int * 2)()

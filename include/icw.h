@@ -207,6 +207,16 @@ int icw_set_state(icw_ctx *ctx, int s, const void *blob, size_t size);
  * total, launches[0..1] = launch counts. */
 int icw_last_timing(icw_ctx *ctx, double ms[2], int launches[2]);
 
+/* IIR state kernel (the serial recurrence) the last real-input icw_process_* call ran: ICW_K1_*.
+ * The host picks the row-broadcast kernel for small batches (its waves fit one per SIMD on half
+ * the chip, Kahan sum with the reject, no serial render) and the lane-per-chain kernel otherwise;
+ * ICW_K1_MODE=plain|row|pair|mfma in the environment at icw_create forces one (A/B runs). */
+#define ICW_K1_LANE   0   /* icw_iir_state: one lane per DF-II chain */
+#define ICW_K1_PAIR   1   /* icw_iir_pair: chain + helper wave (experimental) */
+#define ICW_K1_MFMA   2   /* icw_iir_state_mf: MFMA product feed (experimental) */
+#define ICW_K1_ROW    3   /* icw_iir_row: one 16-lane DPP row per chain */
+int icw_last_k1_kernel(const icw_ctx *ctx);
+
 const char *icw_version(void);
 const char *icw_strerror(int status);
 

@@ -20,7 +20,7 @@ pytestmark = pytest.mark.gpu
 CW = [abi.FMT_CW_F64, abi.FMT_CW_I16, abi.FMT_CW_I16_F32, abi.FMT_CW_F32]
 
 
-@pytest.fixture(autouse=True, params=["plain"])
+@pytest.fixture(autouse=True, params=["plain", "row"])
 def k1_mode(request, monkeypatch):
     monkeypatch.setenv("ICW_K1_MODE", request.param)
     return request.param

@@ -12,10 +12,12 @@ pytestmark = pytest.mark.gpu
 REL_TOL = 1e-6   # north_star: "within 1e-6 relative for the float Hilbert/modulator stages"
 
 
-@pytest.fixture(autouse=True, params=["pair", "plain", "mfma"])
+@pytest.fixture(autouse=True, params=["pair", "plain", "mfma", "row"])
 def k1_mode(request, monkeypatch):
-    """run every case through every IIR-state kernel: the plain lane-per-chain kernel (default),
-    the chain+helper wave pair and the MFMA product feed (both experimental, kept bit-exact)"""
+    """run every case through every IIR-state kernel: the lane-per-chain kernel (large batches),
+    the row-broadcast kernel (small batches; Kahan + reject only, other modes fall back to the
+    lane-per-chain kernel), the chain+helper wave pair and the MFMA product feed (both
+    experimental, kept bit-exact)"""
     monkeypatch.setenv("ICW_K1_MODE", request.param)
     return request.param
 
