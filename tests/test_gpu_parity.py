@@ -96,12 +96,25 @@ def test_all_filters_modes(oracle, icw, htype, kahan, subn):
     assert_parity(out, pre, ro, rp, 2, exact_pre=True)
 
 
-def test_block_split_invariance(oracle, icw):
-    """state carried across blocks of odd sizes == one pass (and == oracle)"""
-    cfg = graph.default_config(48000)
+@pytest.mark.parametrize("htype", [0, 1, 2, 4])
+def test_block_split_invariance(oracle, icw, htype):
+    """state carried across blocks of odd sizes == one pass (and == oracle); orders 15 / 19 / 18 /
+    20, block lengths around the zero-input path's 3N minimum, both start parities"""
+    cfg = graph.default_config(48000, hilbert_type=htype)
     raw = synth.batch_pcm(4, 5000, 48000)
     _, out, pre, ro, rp = run_both(oracle, icw, cfg, graph.graph_master_only(), raw, 5000,
-                                   blocks=[576, 1, 18, 19, 20, 2000, 2366])
+                                   blocks=[576, 1, 18, 19, 20, 44, 45, 54, 57, 60, 61, 2000, 2045])
+    assert_parity(out, pre, ro, rp, 2, exact_pre=True)
+
+
+@pytest.mark.parametrize("htype", [1, 2])
+def test_launch_blocks_inside_one_call(oracle, icw, htype, monkeypatch):
+    """one call cut into many 263-frame launch blocks (ICW_BLOCK): every K1 launch starts at a block
+    offset t0 of either parity and reads the call-start phases"""
+    monkeypatch.setenv("ICW_BLOCK", "263")
+    cfg = graph.default_config(48000, hilbert_type=htype)
+    raw = synth.batch_pcm(6, 3001, 48000)
+    _, out, pre, ro, rp = run_both(oracle, icw, cfg, graph.graph_master_only(), raw, 3001)
     assert_parity(out, pre, ro, rp, 2, exact_pre=True)
 
 
