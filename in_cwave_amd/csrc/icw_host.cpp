@@ -73,7 +73,7 @@ struct DevState {
  * the other CUs (hipExtStreamCreateWithCUMask) */
 struct CuSplit {
     int k1_cus = 0;
-    hipStream_t k1 = nullptr, rest = nullptr, dith = nullptr;
+    hipStream_t k1 = nullptr, rest = nullptr, dith = nullptr, render = nullptr;
 };
 
 }  // namespace
@@ -118,10 +118,14 @@ struct icw_ctx {
     size_t d_in_bytes = 0, d_out_bytes = 0;
     double *d_pre = nullptr;
     size_t d_pre_bytes = 0;
-    double *rpre = nullptr;               /* per-block pre-render buffer for the serial render */
-    size_t rpre_bytes = 0;
-    double *iq = nullptr;                 /* per-block `in` buffer for the bus-form graph */
-    size_t iq_bytes = 0;
+    /* the serial render (K4 bus-form graph + K3b) runs on a fourth stream, one block behind K2:
+     * its inputs are double-buffered like the block scratch */
+    hipStream_t stream4 = nullptr;
+    hipEvent_t k3done[kSets] = {};
+    double *rpre[kSets] = {};             /* per-block pre-render buffer for the serial render */
+    size_t rpre_bytes[kSets] = {};
+    double *iq[kSets] = {};               /* per-block `in` buffer for the bus-form graph */
+    size_t iq_bytes[kSets] = {};
     double *trig = nullptr;               /* per-block rotation table [T][2 * n_trig] */
     size_t trig_bytes = 0;
     /* per stream: known on the host to have bit-identical left / right converters (fresh or reset
@@ -419,8 +423,9 @@ const CuSplit *cu_split(icw_ctx *c, int k1_cus)
     x.k1_cus = k1_cus;
     if (hipExtStreamCreateWithCUMask(&x.k1, (uint32_t)words, mk.data()) != hipSuccess ||
         hipExtStreamCreateWithCUMask(&x.rest, (uint32_t)words, mr.data()) != hipSuccess ||
-        hipExtStreamCreateWithCUMask(&x.dith, (uint32_t)words, mr.data()) != hipSuccess) {
-        for (hipStream_t q : {x.k1, x.rest, x.dith})
+        hipExtStreamCreateWithCUMask(&x.dith, (uint32_t)words, mr.data()) != hipSuccess ||
+        hipExtStreamCreateWithCUMask(&x.render, (uint32_t)words, mr.data()) != hipSuccess) {
+        for (hipStream_t q : {x.k1, x.rest, x.dith, x.render})
             if (q) hipStreamDestroy(q);
         return nullptr;
     }
@@ -431,20 +436,22 @@ const CuSplit *cu_split(icw_ctx *c, int k1_cus)
 void free_all(icw_ctx *c)
 {
     DevState &s = c->st;
-    void *ptrs[] = {s.mt, s.mt_idx, s.rs, s.lr_equal, c->rpre, c->iq, s.err, s.hist, s.sncnt, s.hq_phase, s.pos, s.fade,
+    void *ptrs[] = {s.mt, s.mt_idx, s.rs, s.lr_equal, s.err, s.hist, s.sncnt, s.hq_phase, s.pos, s.fade,
                     s.n_frame, s.bus, s.clips, s.peak_bits, c->d_prog, c->trig, c->d_in, c->d_out, c->d_pre};
     for (void *p : ptrs)
         if (p) hipFree(p);
     for (int p = 0; p < kSets; ++p) {
-        for (void *q : {(void *)c->info_dup[p], (void *)c->w[p], (void *)c->xd[p], (void *)c->dith[p]})
+        for (void *q : {(void *)c->info_dup[p], (void *)c->w[p], (void *)c->xd[p], (void *)c->dith[p],
+                        (void *)c->rpre[p], (void *)c->iq[p]})
             if (q) hipFree(q);
-        for (hipEvent_t e : {c->ditdone[p], c->k1done[p], c->k2done[p], c->k0done[p]})
+        for (hipEvent_t e : {c->ditdone[p], c->k1done[p], c->k2done[p], c->k0done[p], c->k3done[p]})
             if (e) hipEventDestroy(e);
     }
     if (c->stream3) hipStreamDestroy(c->stream3);
+    if (c->stream4) hipStreamDestroy(c->stream4);
     if (c->join) hipEventDestroy(c->join);
     for (auto &x : c->splits)
-        for (hipStream_t q : {x.k1, x.rest, x.dith})
+        for (hipStream_t q : {x.k1, x.rest, x.dith, x.render})
             if (q) hipStreamDestroy(q);
     if (c->stream2) hipStreamDestroy(c->stream2);
     for (auto e : c->ev) hipEventDestroy(e);
@@ -557,11 +564,13 @@ int icw_create(const icw_config *cfg, const icw_node *nodes, int n_nodes, int n_
     if (rc == ICW_OK && hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) rc = ICW_EDEVICE;
     if (rc == ICW_OK && hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking) != hipSuccess) rc = ICW_EDEVICE;
     if (rc == ICW_OK && hipStreamCreateWithFlags(&c->stream3, hipStreamNonBlocking) != hipSuccess) rc = ICW_EDEVICE;
+    if (rc == ICW_OK && hipStreamCreateWithFlags(&c->stream4, hipStreamNonBlocking) != hipSuccess) rc = ICW_EDEVICE;
     for (int p = 0; p < kSets && rc == ICW_OK; ++p)
         if (hipEventCreateWithFlags(&c->k1done[p], hipEventDisableTiming) != hipSuccess ||
             hipEventCreateWithFlags(&c->k2done[p], hipEventDisableTiming) != hipSuccess ||
             hipEventCreateWithFlags(&c->ditdone[p], hipEventDisableTiming) != hipSuccess ||
-            hipEventCreateWithFlags(&c->k0done[p], hipEventDisableTiming) != hipSuccess)
+            hipEventCreateWithFlags(&c->k0done[p], hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&c->k3done[p], hipEventDisableTiming) != hipSuccess)
             rc = ICW_EDEVICE;
     if (rc == ICW_OK && hipEventCreateWithFlags(&c->join, hipEventDisableTiming) != hipSuccess) rc = ICW_EDEVICE;
     if (rc != ICW_OK) {
@@ -802,8 +811,9 @@ int icw_process_streams(icw_ctx *c, int first, int count, const void *in, size_t
         if (grow((void **)&c->w[p], &c->w_bytes[p], S * 4 * w_pitch * sizeof(double))) return ICW_ENOMEM;
         if (grow((void **)&c->xd[p], &c->xd_bytes[p], S * 4 * x_pitch * sizeof(double))) return ICW_ENOMEM;
     }
-    if (c->serial_render && !d_pre && grow((void **)&c->rpre, &c->rpre_bytes, S * (size_t)Tb * 2 * sizeof(double)))
-        return ICW_ENOMEM;
+    if (c->serial_render && !d_pre)
+        for (int p = 0; p < n_sets; ++p)
+            if (grow((void **)&c->rpre[p], &c->rpre_bytes[p], S * (size_t)Tb * 2 * sizeof(double))) return ICW_ENOMEM;
     const bool cw = cfg.in_format >= ICW_FMT_CW_F64;
     const bool bus = c->prog.is_bus;
     /* mono dedup: every stream of the call known to hold identical left / right converters */
@@ -821,7 +831,9 @@ int icw_process_streams(icw_ctx *c, int first, int count, const void *in, size_t
     const bool table = c->prog.needs_omega && !bus && c->prog.n_trig > 0;
     if (table && grow((void **)&c->trig, &c->trig_bytes, (size_t)Tb * 2 * c->prog.n_trig * sizeof(double)))
         return ICW_ENOMEM;
-    if (bus && grow((void **)&c->iq, &c->iq_bytes, S * (size_t)Tb * 4 * sizeof(double))) return ICW_ENOMEM;
+    if (bus)
+        for (int p = 0; p < n_sets; ++p)
+            if (grow((void **)&c->iq[p], &c->iq_bytes[p], S * (size_t)Tb * 4 * sizeof(double))) return ICW_ENOMEM;
     const bool dither = c->serial_render && cfg.render.render_type != ICW_RENDER_ROUND;
     if (dither)
         for (int p = 0; p < n_sets; ++p)
@@ -831,9 +843,9 @@ int icw_process_streams(icw_ctx *c, int first, int count, const void *in, size_t
      * prep K0, the output kernel K2 and the serial graph / render; sD the dither generator.  When
      * K1 needs few CUs (4 waves per CU, one per SIMD) sK is confined to those CUs and sA / sD to
      * the rest, so the frame-parallel kernels never share a SIMD with a recurrence. */
-    hipStream_t sK = st, sA = c->stream2, sD = c->stream3;
+    hipStream_t sK = st, sA = c->stream2, sD = c->stream3, sR = c->stream4;
     if (c->serialize) {
-        sA = sD = st;
+        sA = sD = sR = st;
     } else if (!cw) {
         /* plain K1: 128-lane groups of 32 streams (64 with the dedup); the variants: a lane per chain */
         const int k1_waves = k1_mode == 0 ? ((count + (dedup ? 63 : 31)) / (dedup ? 64 : 32)) * 2
@@ -845,12 +857,13 @@ int icw_process_streams(icw_ctx *c, int first, int count, const void *in, size_t
             sK = cs->k1;
             sA = cs->rest;
             sD = cs->dith;
+            sR = cs->render;
         }
     }
     /* every stream starts after everything already queued on st (inputs, previous calls) */
     if (hipEventRecord(c->join, st) != hipSuccess)
         return ICW_EDEVICE;
-    for (hipStream_t x : {sK, sA, sD})
+    for (hipStream_t x : {sK, sA, sD, sR})
         if (x != st && hipStreamWaitEvent(x, c->join, 0) != hipSuccess) return ICW_EDEVICE;
 
     DevState &ds = c->st;
@@ -966,7 +979,7 @@ int icw_process_streams(icw_ctx *c, int first, int count, const void *in, size_t
             a2.pre = d_pre + (size_t)t0 * 2;
             a2.pre_stride = (size_t)n_frames * 2;
         } else if (c->serial_render) {
-            a2.pre = c->rpre;
+            a2.pre = c->rpre[p];
             a2.pre_stride = (size_t)T * 2;
         }
         a2.do_render = c->serial_render ? 0 : 1;
@@ -981,7 +994,7 @@ int icw_process_streams(icw_ctx *c, int first, int count, const void *in, size_t
         a2.info_dup = cw ? nullptr : c->info_dup[p];
         a2.xin = c->xd[p];
         a2.x_pitch = x_pitch;
-        if (bus) a2.iq_out = c->iq;
+        if (bus) a2.iq_out = c->iq[p];
         a2.trig = c->prog.needs_omega;
         a2.sncnt = (!cw && cfg.iir_subnorm_reject) ? ds.sncnt + f0 * 4 : nullptr;
         if (table) {
@@ -1001,12 +1014,19 @@ int icw_process_streams(icw_ctx *c, int first, int count, const void *in, size_t
             a2.trig_tab = c->trig;
             a2.trig_pitch = at.trig_pitch;
         }
+        /* rpre[p] / iq[p] were last read by the serial render of block b - n_sets (on sR) */
+        if (c->serial_render && b >= n_sets && sR != sA && hipStreamWaitEvent(sA, c->k3done[p], 0) != hipSuccess)
+            return ICW_EDEVICE;
         if (timing) hipEventRecord(c->ev[4 * b + 2], sA);
         if (icw_launch_output(&a2, N, cfg.iir_kahan, sA) != hipSuccess) return ICW_EDEVICE;
+        if (hipEventRecord(c->k2done[p], sA) != hipSuccess) return ICW_EDEVICE;
+        /* the serial part (K4, K3b) on sR after K2(b): it then overlaps K2(b+1) instead of
+         * delaying it on sA */
+        if (c->serial_render && sR != sA && hipStreamWaitEvent(sR, c->k2done[p], 0) != hipSuccess) return ICW_EDEVICE;
         if (bus) {
             IcwK4Args a4;
             memset(&a4, 0, sizeof(a4));
-            a4.iq = c->iq;
+            a4.iq = c->iq[p];
             a4.n_streams = count;
             a4.T = T;
             a4.t0 = t0;
@@ -1018,7 +1038,7 @@ int icw_process_streams(icw_ctx *c, int first, int count, const void *in, size_t
             a4.bus = a2.bus;
             a4.pre = a2.pre;
             a4.pre_stride = a2.pre_stride;
-            if (icw_launch_graph_serial(&a4, sA) != hipSuccess) return ICW_EDEVICE;
+            if (icw_launch_graph_serial(&a4, sR) != hipSuccess) return ICW_EDEVICE;
         }
         if (c->serial_render) {
             IcwK3Args a3;
@@ -1041,16 +1061,16 @@ int icw_process_streams(icw_ctx *c, int first, int count, const void *in, size_t
                 /* K3a for this block on its own stream: dith[p] was last read by K3b of block b-2 */
                 a3.dith = c->dith[p];
                 a3.dith_pitch = (size_t)count * 2;    /* time-major [T][count*2] */
-                if (b >= n_sets && sD != sA && hipStreamWaitEvent(sD, c->k2done[p], 0) != hipSuccess) return ICW_EDEVICE;
+                if (b >= n_sets && sD != sR && hipStreamWaitEvent(sD, c->k3done[p], 0) != hipSuccess) return ICW_EDEVICE;
                 const hipError_t ed = c->dither_lane ? icw_launch_dither_lane(&a3, sD) : icw_launch_dither(&a3, sD);
                 if (ed != hipSuccess || hipEventRecord(c->ditdone[p], sD) != hipSuccess ||
-                    (sD != sA && hipStreamWaitEvent(sA, c->ditdone[p], 0) != hipSuccess))
+                    (sD != sR && hipStreamWaitEvent(sR, c->ditdone[p], 0) != hipSuccess))
                     return ICW_EDEVICE;
             }
-            if (icw_launch_render(&a3, sA) != hipSuccess) return ICW_EDEVICE;
+            if (icw_launch_render(&a3, sR) != hipSuccess) return ICW_EDEVICE;
+            if (hipEventRecord(c->k3done[p], sR) != hipSuccess) return ICW_EDEVICE;
         }
-        if (timing) hipEventRecord(c->ev[4 * b + 3], sA);
-        if (hipEventRecord(c->k2done[p], sA) != hipSuccess) return ICW_EDEVICE;
+        if (timing) hipEventRecord(c->ev[4 * b + 3], c->serial_render ? sR : sA);
         /* complex input: K0(b + n_sets) reuses xd[p], which K2(b) read */
         if (cw && b + n_sets < n_blocks && (rc0 = launch_k0(b + n_sets)) != ICW_OK) return rc0;
     }
@@ -1058,7 +1078,7 @@ int icw_process_streams(icw_ctx *c, int first, int count, const void *in, size_t
         for (int i = 0; i < count; ++i) c->lr_known[first + i] = 0;   /* stereo: the halves diverge */
     /* join: the caller's stream continues after every kernel of the call, then the call-start
      * position / phases / frame counters advance (icw_advance) */
-    for (hipStream_t x : {sK, sA, sD})
+    for (hipStream_t x : {sK, sA, sD, sR})
         if (x != st && (hipEventRecord(c->join, x) != hipSuccess || hipStreamWaitEvent(st, c->join, 0) != hipSuccess))
             return ICW_EDEVICE;
     {
