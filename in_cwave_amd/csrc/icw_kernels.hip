@@ -395,7 +395,10 @@ __device__ __forceinline__ bool icw_exec_op(const IcwOp &op, IcwLR d, double ome
  * other half of a double-buffered LDS window: the global-load latency hides behind FP64 work and
  * the meters reduce once per workgroup.  TRIG = the program has an active Shift / PM node. */
 template <int N, bool KAHAN, bool TRIG>
-__global__ __launch_bounds__(ICW_K2_TILE) void icw_output(IcwK2Args a)
+#ifndef ICW_K2_MINWG
+#define ICW_K2_MINWG 1
+#endif
+__global__ __launch_bounds__(ICW_K2_TILE, ICW_K2_MINWG) void icw_output(IcwK2Args a)
 {
     constexpr int TILE = ICW_K2_TILE;
     constexpr int NR = N + 1;                        /* window rows past the tile (row N+t: w[t]) */

@@ -10,6 +10,9 @@ import numpy as np
 from . import abi
 
 LIB_PATH = Path(__file__).resolve().parent / "libicw.so"
+# A/B runs only: ICW_LIB=<name> loads in_cwave_amd/<name> (an alternative in-tree build) instead
+if os.environ.get("ICW_LIB"):
+    LIB_PATH = Path(__file__).resolve().parent / Path(os.environ["ICW_LIB"]).name
 _lib = None
 
 
