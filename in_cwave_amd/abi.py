@@ -14,7 +14,8 @@ S_ADD_REIM, S_SUB_REIM, S_RE, S_IM = 0, 1, 2, 3
 XCH_NORMAL, XCH_SWAP, XCH_LEFTONLY, XCH_RIGHTONLY, XCH_MIXLR = 0, 1, 2, 3, 4
 # input formats (HRW_FMT_*)
 FMT_U8, FMT_I16, FMT_I24, FMT_I32, FMT_F32 = 0, 1, 2, 3, 4
-K1_LANE, K1_PAIR, K1_MFMA, K1_ROW = 0, 1, 2, 3      # icw_last_k1_kernel (include/icw.h)
+K1_LANE, K1_PAIR, K1_MFMA, K1_ROW, K1_FC = 0, 1, 2, 3, 4      # icw_last_k1_kernel (include/icw.h)
+FES_N = 7     # FP_EXCEPT_STATS counters: total, snan, qnan, ninf, nden, pden, pinf
 # complex CWAVE formats: ICW_FMT_CW_F64 + HCW_FMT_* (cwave.h:70-80), Hilbert bypassed
 FMT_CW_F64, FMT_CW_I16, FMT_CW_I16_F32, FMT_CW_F32 = 5, 6, 7, 8
 FMT_BYTES = {FMT_U8: 1, FMT_I16: 2, FMT_I24: 3, FMT_I32: 4, FMT_F32: 4,
@@ -60,6 +61,7 @@ class Config(C.Structure):
         ("frmod_scaled", C.c_int32), ("need24bits", C.c_int32), ("bypass_list", C.c_int32),
         ("seed_left", C.c_uint32), ("seed_right", C.c_uint32),
         ("render", RenderCfg),
+        ("fp_check", C.c_int32),
     ]
 
 
@@ -148,6 +150,7 @@ SIGNATURES = {
     "icw_set_state": (_i, [_vp, _i, _vp, _sz]),
     "icw_last_timing": (_i, [_vp, C.POINTER(C.c_double), C.POINTER(_i)]),
     "icw_last_k1_kernel": (_i, [_vp]),
+    "icw_get_fp_census": (_i, [_vp, _i, _i, C.POINTER(C.c_uint32)]),
     "icw_cwave_parse": (_i, [_vp, _sz, C.c_int64, C.POINTER(CwaveHeader), C.POINTER(C.c_uint32),
                              C.POINTER(C.c_uint32)]),
     "icw_crc32_batch": (_i, [_vp, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64), _i, C.POINTER(C.c_uint32),

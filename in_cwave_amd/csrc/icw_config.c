@@ -362,5 +362,6 @@ int icw_config_load(const char *text, size_t len, icw_file_config *out, int *bad
         out->ver_config = ICW_CFG_VERSION;
         return ICW_EINVAL;
     }
+    out->cfg.fp_check = out->fp_check;                         /* FP_CHECK -> the device path */
     return ICW_OK;
 }

@@ -16,6 +16,7 @@
 #define ICW_K2_TPW    4      /* consecutive tiles per output-kernel workgroup */
 #define ICW_HIST_PITCH 20    /* doubles per chain in the delay-line state */
 #define ICW_RSTATE    42     /* doubles of render state per channel: prev_rnd, prev_ns_err, E[20], O[20] */
+#define ICW_FES_PITCH 8      /* u32 per FP-exception census (7 used: FP_EXCEPT_STATS, fp_check.h:62-72) */
 
 struct IcwProg;
 
@@ -82,6 +83,8 @@ struct IcwK1Args {
     int32_t wg_waves;              /* waves per workgroup of the plain / MFMA kernels (1..4) */
     int32_t dedup;                 /* mono, every stream's converters identical: left chains only */
     double pc[20];                 /* loop-back coefficients -a[i+1]/a0 */
+    uint32_t *fes;                 /* FP_CHECK: [n_streams][4][ICW_FES_PITCH] census (Hilbert L, R,
+                                      render L, R); null: no FC() arithmetic */
 };
 
 /* One compiled DSP node (adv_modulator.c:637-751), executed in list order tail -> head. */
@@ -146,6 +149,7 @@ struct IcwK3Args {
     IcwRenderK rk;
     double *dith;                  /* [T][dith_pitch] rnd * dth_mul per sample, time-major (K3a -> K3b); null: ROUND */
     size_t dith_pitch;
+    uint32_t *fes;                 /* FP_CHECK census, as in IcwK1Args; null: no FC() */
 };
 
 /* Arguments of the output kernel (frame-parallel: Kahan output sums, unmix, graph, render). */
@@ -183,6 +187,7 @@ struct IcwK2Args {
                                       for streams whose call-start counter equals stream 0's */
     int32_t trig_pitch;
     int32_t zero;                  /* always 0: an offset the compiler cannot fold (keeps loads in a loop) */
+    uint32_t *fes;                 /* FP_CHECK census, as in IcwK1Args; null: no FC() */
 };
 
 /* Per-frame rotation table (one thread per frame): the Shift / PM factors depend only on the frame
@@ -196,5 +201,49 @@ struct IcwTrigArgs {
     uint32_t sample_rate;
     double *tab;                   /* [T][trig_pitch] */
 };
+
+/* FC() of fp_check.c:52-100 (except_stats_check): a NaN or a denormal becomes 0.0, an infinity
+ * +-INF_HUGE_VALUE (65535.0, fp_check.h:60); each is counted in FP_EXCEPT_STATS order total, snan,
+ * qnan, ninf, nden, pden, pinf.  _fpclass calls a NaN with the quiet bit (mantissa bit 51) clear
+ * signaling.  Counters are per thread; the kernels add them to the census at the end. */
+struct IcwFes {
+    uint32_t c[7];
+};
+
+#if defined(__HIPCC__) || defined(__HIP__)
+/* not inlined: FP_CHECK is a diagnostic mode, and inlined FC() branches at every operation of the
+ * unrolled sums multiply the code size (and the build time) of the FC kernels */
+__device__ __noinline__ double icw_fc(double v, IcwFes &f)
+{
+    const unsigned long long u = (unsigned long long)__double_as_longlong(v);
+    const unsigned ex = (unsigned)((u >> 52) & 0x7ffu);
+    const unsigned long long man = u & 0xfffffffffffffull;
+    if (ex == 0x7ffu) {
+        ++f.c[0];
+        if (man) { ++f.c[((man >> 51) & 1u) ? 2 : 1]; return 0.0; }
+        if (u >> 63) { ++f.c[3]; return -65535.0; }
+        ++f.c[6];
+        return 65535.0;
+    }
+    if (ex == 0u && man) { ++f.c[0]; ++f.c[(u >> 63) ? 4 : 5]; return 0.0; }
+    return v;
+}
+
+/* the same value without counting (a product whose FC() another kernel already counted) */
+__device__ __forceinline__ double icw_fc_nc(double v)
+{
+    const unsigned long long u = (unsigned long long)__double_as_longlong(v);
+    const unsigned ex = (unsigned)((u >> 52) & 0x7ffu);
+    if (ex == 0x7ffu) return (u & 0xfffffffffffffull) ? 0.0 : ((u >> 63) ? -65535.0 : 65535.0);
+    return ex == 0u ? (v == 0.0 ? v : 0.0) : v;
+}
+
+__device__ __forceinline__ void icw_fes_flush(const IcwFes &f, uint32_t *dst)
+{
+#pragma unroll
+    for (int k = 0; k < 7; ++k)
+        if (f.c[k]) atomicAdd(dst + k, f.c[k]);
+}
+#endif
 
 #endif

@@ -27,6 +27,7 @@ extern "C" hipError_t icw_launch_iir_pair(const IcwK1Args *a, int nord, int kaha
 extern "C" hipError_t icw_launch_iir_state(const IcwK1Args *a, int nord, int kahan, int subn, hipStream_t st);
 extern "C" hipError_t icw_launch_iir_mfma(const IcwK1Args *a, int nord, int kahan, int subn, hipStream_t st);
 extern "C" hipError_t icw_launch_iir_row(const IcwK1Args *a, int nord, int kahan, int subn, hipStream_t st);
+extern "C" hipError_t icw_launch_iir_fc(const IcwK1Args *a, int nord, int kahan, int subn, hipStream_t st);
 extern "C" hipError_t icw_launch_render(const IcwK3Args *a, hipStream_t st);
 extern "C" hipError_t icw_launch_dither(const IcwK3Args *a, hipStream_t st);
 extern "C" hipError_t icw_launch_dither_lane(const IcwK3Args *a, hipStream_t st);
@@ -67,6 +68,7 @@ struct DevState {
     int32_t *mt_idx = nullptr;            /* [2*streams] */
     double *rs = nullptr;                 /* [2*streams][ICW_RSTATE] */
     uint32_t *lr_equal = nullptr;         /* [streams][2] right converters bit-identical to left ones, per filter */
+    uint32_t *fes = nullptr;              /* FP_CHECK: [streams][4][ICW_FES_PITCH] FP-exception census */
 };
 
 /* streams confined to disjoint CU sets: K1 on k1_cus CUs spread over the device, the rest on
@@ -436,7 +438,7 @@ const CuSplit *cu_split(icw_ctx *c, int k1_cus)
 void free_all(icw_ctx *c)
 {
     DevState &s = c->st;
-    void *ptrs[] = {s.mt, s.mt_idx, s.rs, s.lr_equal, s.err, s.hist, s.sncnt, s.hq_phase, s.pos, s.fade,
+    void *ptrs[] = {s.mt, s.mt_idx, s.rs, s.lr_equal, s.fes, s.err, s.hist, s.sncnt, s.hq_phase, s.pos, s.fade,
                     s.n_frame, s.bus, s.clips, s.peak_bits, c->d_prog, c->trig, c->d_in, c->d_out, c->d_pre};
     for (void *p : ptrs)
         if (p) hipFree(p);
@@ -532,6 +534,8 @@ int icw_create(const icw_config *cfg, const icw_node *nodes, int n_nodes, int n_
     c->serial_render = !(cfg->render.render_type == ICW_RENDER_ROUND && c->rk.ns_kind == 0);
     /* the bus-form graph runs frame-serially and hands lOut/rOut to the serial render */
     if (c->prog.is_bus) c->serial_render = true;
+    /* FP_CHECK: the FC() render arithmetic lives in the serial render kernel only */
+    if (cfg->fp_check) c->serial_render = true;
     for (int ch = 0; ch < 2; ++ch) {
         uint32_t *st = c->mt_seed_state[ch];
         st[0] = ch ? cfg->seed_right : cfg->seed_left;         /* mtrnd_init_seed, mt_jrnd.c:28-47 */
@@ -557,6 +561,7 @@ int icw_create(const icw_config *cfg, const icw_node *nodes, int n_nodes, int n_
         rc |= dalloc(&s.rs, S * 2 * ICW_RSTATE);
     }
     rc |= dalloc(&s.lr_equal, S * 2);
+    if (cfg->fp_check) rc |= dalloc(&s.fes, S * 4 * ICW_FES_PITCH);
     for (int p = 0; p < kSets; ++p) rc |= dalloc(&c->info_dup[p], S * 2);
     rc |= dalloc(&c->d_prog, 1);
     if (rc == ICW_OK && hipMemcpy(c->d_prog, &c->prog, sizeof(IcwProg), hipMemcpyHostToDevice) != hipSuccess)
@@ -648,6 +653,7 @@ int icw_stream_init(icw_ctx *c, int first, int count)
     ok &= hipMemsetAsync(s.bus + f * ICW_N_INPUTS * 4, 0, n * ICW_N_INPUTS * 4 * sizeof(double), st) == hipSuccess;
     ok &= hipMemsetAsync(s.clips + f * 2, 0, n * 2 * sizeof(uint32_t), st) == hipSuccess;
     ok &= hipMemsetAsync(s.peak_bits + f * 2, 0, n * 2 * sizeof(unsigned long long), st) == hipSuccess;
+    if (s.fes) ok &= hipMemsetAsync(s.fes + f * 4 * ICW_FES_PITCH, 0, n * 4 * ICW_FES_PITCH * 4, st) == hipSuccess;
     /* no track open: n_samples "infinite", no fades (xwave_unpack_csample never fades) */
     std::vector<long long> fd(n * 3);
     for (size_t i = 0; i < n; ++i) { fd[i * 3] = (long long)1 << 62; fd[i * 3 + 1] = 0; fd[i * 3 + 2] = 0; }
@@ -817,7 +823,8 @@ int icw_process_streams(icw_ctx *c, int first, int count, const void *in, size_t
     const bool cw = cfg.in_format >= ICW_FMT_CW_F64;
     const bool bus = c->prog.is_bus;
     /* mono dedup: every stream of the call known to hold identical left / right converters */
-    bool dedup = !cw && nch == 1 && c->dedup_ok && (c->k1_mode <= 0 || c->k1_mode == 3);   /* plain / row K1 */
+    const bool fcm = c->cfg.fp_check != 0;                /* FP_CHECK: FC() kernels, no shortcuts */
+    bool dedup = !cw && !fcm && nch == 1 && c->dedup_ok && (c->k1_mode <= 0 || c->k1_mode == 3);   /* plain / row K1 */
     for (int i = 0; dedup && i < count; ++i) dedup = c->lr_known[first + i] != 0;
     /* K1 variant of this call.  Auto: the row-broadcast kernel (4 chains per wave, ~17 % fewer
      * instructions per sample) when its waves fit one per SIMD on at most half the chip, else the
@@ -827,6 +834,7 @@ int icw_process_streams(icw_ctx *c, int first, int count, const void *in, size_t
     int k1_mode = c->k1_mode;
     if (k1_mode < 0) k1_mode = (row_ok && !c->serial_render && row_waves * 2 <= c->n_cu * 4) ? 3 : 0;
     if (k1_mode == 3 && !row_ok) k1_mode = 0;
+    if (fcm) k1_mode = ICW_K1_FC;
     if (!cw) c->last_k1 = k1_mode;
     const bool table = c->prog.needs_omega && !bus && c->prog.n_trig > 0;
     if (table && grow((void **)&c->trig, &c->trig_bytes, (size_t)Tb * 2 * c->prog.n_trig * sizeof(double)))
@@ -848,7 +856,7 @@ int icw_process_streams(icw_ctx *c, int first, int count, const void *in, size_t
         sA = sD = sR = st;
     } else if (!cw) {
         /* plain K1: 128-lane groups of 32 streams (64 with the dedup); the variants: a lane per chain */
-        const int k1_waves = k1_mode == 0 ? ((count + (dedup ? 63 : 31)) / (dedup ? 64 : 32)) * 2
+        const int k1_waves = (k1_mode == 0 || k1_mode == ICW_K1_FC) ? ((count + (dedup ? 63 : 31)) / (dedup ? 64 : 32)) * 2
                            : k1_mode == 3 ? row_waves : (count * 4 + 63) / 64;
         const int k1_cus = (k1_waves + c->k1_wpc - 1) / c->k1_wpc;
         if (c->cu_split && k1_cus * 2 <= c->n_cu) {
@@ -937,11 +945,13 @@ int icw_process_streams(icw_ctx *c, int first, int count, const void *in, size_t
             memcpy(a1.pc, c->pc, sizeof(a1.pc));
             a1.wg_waves = c->k1_wg;
             a1.dedup = dedup ? 1 : 0;
+            a1.fes = fcm ? ds.fes + f0 * 4 * ICW_FES_PITCH : nullptr;
             /* K0(b) done, and K2(b-2), the last reader of w[p] / info_dup[p] */
             if (sK != sA && hipStreamWaitEvent(sK, c->k0done[p], 0) != hipSuccess) return ICW_EDEVICE;
             if (b >= n_sets && sK != sA && hipStreamWaitEvent(sK, c->k2done[p], 0) != hipSuccess) return ICW_EDEVICE;
             if (timing) hipEventRecord(c->ev[4 * b], sK);
-            const hipError_t e1 = k1_mode == 3 ? icw_launch_iir_row(&a1, N, cfg.iir_kahan, cfg.iir_subnorm_reject, sK)
+            const hipError_t e1 = k1_mode == ICW_K1_FC ? icw_launch_iir_fc(&a1, N, cfg.iir_kahan, cfg.iir_subnorm_reject, sK)
+                                : k1_mode == 3 ? icw_launch_iir_row(&a1, N, cfg.iir_kahan, cfg.iir_subnorm_reject, sK)
                                 : k1_mode == 2 ? icw_launch_iir_mfma(&a1, N, cfg.iir_kahan, cfg.iir_subnorm_reject, sK)
                                 : k1_mode == 1 ? icw_launch_iir_pair(&a1, N, cfg.iir_kahan, cfg.iir_subnorm_reject, sK)
                                                : icw_launch_iir_state(&a1, N, cfg.iir_kahan, cfg.iir_subnorm_reject, sK);
@@ -997,6 +1007,7 @@ int icw_process_streams(icw_ctx *c, int first, int count, const void *in, size_t
         if (bus) a2.iq_out = c->iq[p];
         a2.trig = c->prog.needs_omega;
         a2.sncnt = (!cw && cfg.iir_subnorm_reject) ? ds.sncnt + f0 * 4 : nullptr;
+        a2.fes = fcm ? ds.fes + f0 * 4 * ICW_FES_PITCH : nullptr;
         if (table) {
             IcwTrigArgs at;
             memset(&at, 0, sizeof(at));
@@ -1057,6 +1068,7 @@ int icw_process_streams(icw_ctx *c, int first, int count, const void *in, size_t
             a3.n_gen = count * 2;
             a3.mt_pitch = c->n_streams * 2;
             a3.rk = c->rk;
+            a3.fes = fcm ? ds.fes + f0 * 4 * ICW_FES_PITCH : nullptr;
             if (dither) {
                 /* K3a for this block on its own stream: dith[p] was last read by K3b of block b-2 */
                 a3.dith = c->dith[p];
@@ -1261,6 +1273,24 @@ int icw_set_state(icw_ctx *c, int s, const void *blob, size_t size)
         ok &= hipMemcpy(c->st.rs + (size_t)s * 2 * ICW_RSTATE, b.rs, sizeof(b.rs), hipMemcpyHostToDevice) == hipSuccess;
     }
     return ok ? ICW_OK : ICW_EDEVICE;
+}
+
+int icw_get_fp_census(icw_ctx *c, int s, int reset, uint32_t counts[4][ICW_FES_N])
+{
+    if (!c || !counts || s < 0 || s >= c->n_streams) return ICW_EINVAL;
+    if (!c->st.fes) {
+        memset(counts, 0, sizeof(uint32_t) * 4 * ICW_FES_N);
+        return ICW_OK;
+    }
+    std::lock_guard<std::mutex> lk(c->mu);
+    if (set_dev(c) || quiesce(c) != hipSuccess) return ICW_EDEVICE;
+    uint32_t buf[4 * ICW_FES_PITCH];
+    uint32_t *src = c->st.fes + (size_t)s * 4 * ICW_FES_PITCH;
+    if (hipMemcpy(buf, src, sizeof(buf), hipMemcpyDeviceToHost) != hipSuccess) return ICW_EDEVICE;
+    for (int i = 0; i < 4; ++i)
+        for (int k = 0; k < ICW_FES_N; ++k) counts[i][k] = buf[i * ICW_FES_PITCH + k];
+    if (reset && hipMemset(src, 0, sizeof(buf)) != hipSuccess) return ICW_EDEVICE;
+    return ICW_OK;
 }
 
 int icw_last_k1_kernel(const icw_ctx *c)

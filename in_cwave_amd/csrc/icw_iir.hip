@@ -278,6 +278,65 @@ __global__ __launch_bounds__(256) void icw_iir_state(IcwK1Args a)
     if (ch == 0) a.lr_equal[s * 2 + f] = eq ? 1u : 0u;
 }
 
+/* ----------------------------------------------- IIR state kernel with FC() (K1f) -------- */
+/* FP_CHECK on: the WITH FP CHECKS branches of iir_rp_process_kahan / _baseline for the loop-back
+ * sum (hblpf.c:1058-1095 / 928-950): ti = FC(z * c_i), kahan_step_fes (hblpf.c:995-1005), or
+ * sum_i = FC(sum_i + FC(z * c_i)).  A diagnostic mode, so the plain form: one lane per chain,
+ * no zero-input steps, no mono shortcuts (the census must count every converter's own events). */
+/* one sample; the delay line is a ring in private memory indexed at run time (this mode favours
+ * code size over speed): logical z_i = R[(j - 1 - i) mod N] at step j, the new w goes to R[j mod N] */
+template <bool KAHAN, bool SUBN>
+__device__ __noinline__ double icw_iir_step_fc(double *R, int N, int j, double xin, const double *pc, IcwFes &fe)
+{
+    double S = xin;
+    if (KAHAN) {
+        double C = 0.0, Y, T;
+#pragma unroll 1
+        for (int i = 0; i < N; ++i) {
+            const double ti = icw_fc(R[(j - 1 - i + 2 * N) % N] * pc[i], fe);
+            Y = icw_fc(ti - C, fe);
+            T = icw_fc(S + Y, fe);
+            C = icw_fc(icw_fc(T - S, fe) - Y, fe);
+            S = T;
+        }
+    } else {
+#pragma unroll 1
+        for (int i = 0; i < N; ++i) S = icw_fc(S + icw_fc(R[(j - 1 - i + 2 * N) % N] * pc[i], fe), fe);
+    }
+    if (SUBN && fabs(S) < 1.0) S = 0.0;
+    R[j % N] = S;
+    return S;
+}
+
+template <bool KAHAN, bool SUBN>
+__global__ __launch_bounds__(64) void icw_iir_state_fc(IcwK1Args a, int N)
+{
+    const int g = blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= a.n_chains) return;
+    const int s = g >> 2, ch = (g >> 1) & 1, f = g & 1;
+    double pc[20], R[20];
+#pragma unroll 1
+    for (int i = 0; i < 20; ++i) pc[i] = a.pc[i];
+#pragma unroll 1
+    for (int i = 0; i < N; ++i) R[N - 1 - i] = a.hist[(size_t)g * ICW_HIST_PITCH + i];
+    const double *xp = a.xd + (size_t)g * a.x_pitch;
+    double *wrow = a.w + (size_t)g * a.w_pitch;
+#pragma unroll 1
+    for (int j = 0; j < N; ++j) wrow[j] = R[j];
+    IcwFes fe = {};
+    const int T = a.T;
+#pragma unroll 1
+    for (int t = 0; t < T; ++t) wrow[N + t] = icw_iir_step_fc<KAHAN, SUBN>(R, N, t, xp[t], pc, fe);
+    /* after T steps logical z_i = R[(T - 1 - i) mod N] */
+#pragma unroll 1
+    for (int i = 0; i < N; ++i) a.hist[(size_t)g * ICW_HIST_PITCH + i] = R[((T - 1 - i) % N + N) % N];
+    if (ch == 0) {                /* no converter-identity shortcuts in this mode */
+        a.info_dup[s * 2 + f] = 0u;
+        a.lr_equal[s * 2 + f] = 0u;
+    }
+    icw_fes_flush(fe, a.fes + ((size_t)s * 4 + ch) * ICW_FES_PITCH);
+}
+
 /* ------------------------------------------ IIR state kernel, row broadcast (K1r) -------- */
 /* The same Kahan loop-back sum (iir_rp_process_kahan, hblpf.c:1017-1046, subnorm reject on) with
  * one DF-II chain per 16-lane DPP row instead of one per lane.  What it buys: a wave issues ~one
@@ -1020,6 +1079,20 @@ extern "C" hipError_t icw_launch_iir_pair(const IcwK1Args *a, int nord, int kaha
     case 20: return launch_k1p_n<20>(*a, kahan, subn, st);
     }
     return hipErrorInvalidValue;
+}
+
+template <bool K, bool S>
+static hipError_t launch_k1f_t(const IcwK1Args &a, int N, hipStream_t st)
+{
+    hipLaunchKernelGGL((icw_iir_state_fc<K, S>), dim3((a.n_chains + 63) / 64), dim3(64), 0, st, a, N);
+    return hipGetLastError();
+}
+
+extern "C" hipError_t icw_launch_iir_fc(const IcwK1Args *a, int nord, int kahan, int subn, hipStream_t st)
+{
+    if (!a->fes || a->dedup || nord < 1 || nord > 20) return hipErrorInvalidValue;
+    if (kahan) return subn ? launch_k1f_t<true, true>(*a, nord, st) : launch_k1f_t<true, false>(*a, nord, st);
+    return subn ? launch_k1f_t<false, true>(*a, nord, st) : launch_k1f_t<false, false>(*a, nord, st);
 }
 
 /* K1r: four chain slots per wave and filter (see icw_iir_row); Kahan with the reject only */

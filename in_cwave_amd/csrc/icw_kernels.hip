@@ -159,6 +159,38 @@ struct IcwLR { double lre, lim, rre, rim; };
 /* the same sums for NC chains at once, interleaved by term: each coefficient is live for one
  * term of all NC chains instead of across NC whole sums (with the chains back to back, all 2N
  * coefficients stay live in SGPRs and spill to VGPR lanes -- a v_readlane per use) */
+/* FP_CHECK on: the output half of the WITH FP CHECKS branches of iir_rp_process_kahan / _baseline
+ * (hblpf.c:1058-1095, 928-950) for one chain, whose delay line is z_i = win[N-1-i].  ti = FC(z * c_i)
+ * is the loop-back kernel's product (counted there), so here it is only applied.  Compact on
+ * purpose (run-time loops, FC() not inlined): a diagnostic mode. */
+__device__ __noinline__ double icw_iir_out_fc(const double *win, int N, int kahan, const double *pc,
+                                              const double *pd, double d0, IcwFes &f)
+{
+    if (kahan) {
+        double z = win[N - 1];
+        double t = icw_fc_nc(z * pc[0]);
+        double S = icw_fc(z * pd[0], f), C = 0.0, Y, T;
+#pragma unroll 1
+        for (int k = 0; k < 2 * N - 1; ++k) {
+            /* steps: t0 * d0, then per i >= 1: z * d_i, t_i * d0 */
+            const int i = (k + 1) >> 1;
+            double x;
+            if (k == 0) x = icw_fc(t * d0, f);
+            else if (k & 1) { z = win[N - 1 - i]; t = icw_fc_nc(z * pc[i]); x = icw_fc(z * pd[i], f); }
+            else x = icw_fc(t * d0, f);
+            Y = icw_fc(x - C, f);                            /* kahan_step_fes, hblpf.c:995-1005 */
+            T = icw_fc(S + Y, f);
+            C = icw_fc(icw_fc(T - S, f) - Y, f);
+            S = T;
+        }
+        return S;
+    }
+    double so = 0.0;
+#pragma unroll 1
+    for (int i = 0; i < N; ++i) so = icw_fc(so + icw_fc(win[N - 1 - i] * pd[i], f), f);
+    return icw_fc(icw_fc(win[N] * d0, f) + so, f);
+}
+
 template <int N, bool KAHAN, int NC>
 __device__ __forceinline__ void icw_iir_out_n(const double *const (&win)[NC], const double *pc, const double *pd,
                                               double d0, double (&y)[NC])
@@ -394,10 +426,10 @@ __device__ __forceinline__ bool icw_exec_op(const IcwOp &op, IcwLR d, double ome
  * The w window of tile k+1 is loaded into registers while tile k is computed, then written to the
  * other half of a double-buffered LDS window: the global-load latency hides behind FP64 work and
  * the meters reduce once per workgroup.  TRIG = the program has an active Shift / PM node. */
-template <int N, bool KAHAN, bool TRIG>
 #ifndef ICW_K2_MINWG
 #define ICW_K2_MINWG 1
 #endif
+template <int N, bool KAHAN, bool TRIG, bool FCK = false>
 __global__ __launch_bounds__(ICW_K2_TILE, ICW_K2_MINWG) void icw_output(IcwK2Args a)
 {
     constexpr int TILE = ICW_K2_TILE;
@@ -414,8 +446,9 @@ __global__ __launch_bounds__(ICW_K2_TILE, ICW_K2_MINWG) void icw_output(IcwK2Arg
 
     /* mono input, converters bit-identical at block start (K1's flag) and in phase: the right
      * filter outputs are copies of the left ones this block */
-    const bool dup = !a.cw && a.nch == 1 && a.info_dup && a.info_dup[s * 2] && a.info_dup[s * 2 + 1] &&
+    const bool dup = !FCK && !a.cw && a.nch == 1 && a.info_dup && a.info_dup[s * 2] && a.info_dup[s * 2 + 1] &&
                      a.hq_phase[s * 2] == a.hq_phase[s * 2 + 1];
+    IcwFes fes[2] = {};
     const int nc = dup ? 2 : 4;
     /* the per-frame rotation table holds this stream's factors when its counter is in step */
     const bool use_tab = TRIG && a.trig_tab && a.n_frame[s] == a.n_frame[0];
@@ -489,7 +522,11 @@ __global__ __launch_bounds__(ICW_K2_TILE, ICW_K2_MINWG) void icw_output(IcwK2Arg
                 }
                 /* filter outputs of the 4 chains (L-I, L-Q, R-I, R-Q) */
                 double y[4];
-                if (dup) {
+                if constexpr (FCK) {
+#pragma unroll 1
+                    for (int c = 0; c < 4; ++c)
+                        y[c] = icw_iir_out_fc(&W[c][tl], N, KAHAN, lcoef + zk, lcoef + 20 + zk, a.d0, fes[c >> 1]);
+                } else if (dup) {
                     const double *const wins[2] = {&W[0][tl], &W[1][tl]};
                     double y2[2];
                     icw_iir_out_n<N, KAHAN, 2>(wins, lcoef + zk, lcoef + 20 + zk, a.d0, y2);
@@ -580,6 +617,10 @@ __global__ __launch_bounds__(ICW_K2_TILE, ICW_K2_MINWG) void icw_output(IcwK2Arg
         }
     }
 
+    if constexpr (FCK) {
+        icw_fes_flush(fes[0], a.fes + (size_t)s * 4 * ICW_FES_PITCH);
+        icw_fes_flush(fes[1], a.fes + ((size_t)s * 4 + 1) * ICW_FES_PITCH);
+    }
     if (count_sn) {
         __shared__ unsigned red_sn[4][TILE / 64];
         const int wv = tl >> 6;
@@ -1231,6 +1272,82 @@ __global__ __launch_bounds__(64) void icw_render_serial(IcwK3Args a)
     if (pk > 0.0) atomicMax(&a.peak_bits[g], (unsigned long long)__double_as_longlong(pk));
 }
 
+/* Render with FP_CHECK (K3f): sound_render_value's WITH FC CHECKS arithmetic (sound_render.c:
+ * 857-903) and ns_fir / ns_iir's (428-433, 474-486), counting into the render census.  One lane per
+ * channel like K3b, but compact (run-time loops, the reference's own decrementing ring in private
+ * memory): a diagnostic mode.  The dither term comes from K3a; its FC() are identities (the sums of
+ * dsopen values are multiples of 2^-56 below 12 in magnitude, never special). */
+__global__ __launch_bounds__(64) void icw_render_fc(IcwK3Args a)
+{
+    constexpr int NM = ICW_MAX_NS_TAPS;
+    const int g = blockIdx.x * 64 + threadIdx.x;
+    if (g >= a.n_gen) return;
+    const int s = g >> 1, ch = g & 1;
+    const IcwRenderK &k = a.rk;
+    const int n = k.ns_n;
+    double *rs = a.rs + (size_t)g * ICW_RSTATE;
+    double prev_err = rs[1];
+    /* rs keeps the history by age (0 = newest); the reference ring: ebuf[(pos + age) mod n] */
+    double E[NM], O[NM];
+    int pos = 0;                                         /* E age j at slot (pos + j) mod n, O age j at (pos - 1 + j) */
+#pragma unroll 1
+    for (int i = 0; i < NM; ++i) E[i] = O[i] = 0.0;
+#pragma unroll 1
+    for (int i = 0; i < n; ++i) { E[i] = rs[2 + i]; O[(i - 1 + n) % n] = rs[2 + NM + i]; }
+    const double *pp = a.pre + (size_t)s * a.pre_stride + ch;
+    const double *dp = a.dith ? a.dith + g : nullptr;
+    unsigned char *op = a.out + (size_t)s * a.out_stride;
+    const int osz = k.is24 ? 3 : 2;
+    unsigned clips = 0;
+    double pk = 0.0;
+    IcwFes fe = {};
+#pragma unroll 1
+    for (int t = 0; t < a.T; ++t) {
+        const double d = dp ? dp[(size_t)t * a.dith_pitch] : 0.0;
+        const double input = icw_fc(icw_fc(pp[(size_t)t * 2] * k.norm_mul, fe) - prev_err, fe);
+        int delta;
+        double q = icw_fc(input + icw_fc(d, fe), fe);
+        q = icw_fc(icw_round_q(q, k.round_offset, k.sign_delta, delta), fe);
+        pk = fmax(pk, fabs(q));
+        const int vc = icw_clamp_int(q, k, clips);
+        const int val = (isnan(q) ? (int)0x80000000 : vc) + delta;
+        const double ev = icw_fc((double)val - input, fe);
+        double res = 0.0;
+        if (k.ns_kind != 0) {
+            pos = pos ? pos - 1 : n - 1;                 /* ns_ix_pos decrement (sound_render.c:410-413) */
+            /* ages shift by one: the ring slot of age j is (pos + j) mod n */
+            E[pos] = icw_fc(ev, fe);
+            int ib = pos;
+#pragma unroll 1
+            for (int ic = 0; ic < n; ++ic) {
+                if (k.ns_kind == 1) res = icw_fc(res + icw_fc(k.ns_c[ic] * E[ib], fe), fe);
+                else res = icw_fc(res + icw_fc(icw_fc(k.ns_c[ic] * E[ib], fe) - icw_fc(k.ns_c[ic + n] * O[ib], fe), fe), fe);
+                if (++ib >= n) ib = 0;
+            }
+            if (k.ns_kind == 2) O[(pos ? pos : n) - 1] = res;
+        }
+        prev_err = res;
+        const int v = val << k.norm_shift;
+        unsigned char *o = op + ((size_t)t * 2 + ch) * osz;
+        o[0] = (unsigned char)v;
+        o[1] = (unsigned char)(v >> 8);
+        if (osz == 3) o[2] = (unsigned char)(v >> 16);
+    }
+    rs[1] = prev_err;
+    /* back to the by-age layout: age j at slot (pos + j) mod n (E) and (pos - 1 + j) mod n (O: the
+     * newest output sits one slot behind the newest error) */
+    if (k.ns_kind != 0) {
+        double e2[NM], o2[NM];
+#pragma unroll 1
+        for (int j = 0; j < n; ++j) { e2[j] = E[(pos + j) % n]; o2[j] = O[(pos - 1 + n + j) % n]; }
+#pragma unroll 1
+        for (int j = 0; j < n; ++j) { rs[2 + j] = e2[j]; rs[2 + NM + j] = o2[j]; }
+    }
+    if (clips) atomicAdd(&a.clips[g], clips);
+    if (pk > 0.0) atomicMax(&a.peak_bits[g], (unsigned long long)__double_as_longlong(pk));
+    icw_fes_flush(fe, a.fes + ((size_t)s * 4 + 2 + ch) * ICW_FES_PITCH);
+}
+
 /* ---------------------------------------------------------------- launch wrappers ------- */
 extern "C" hipError_t icw_launch_unpack(const IcwK0Args *a, hipStream_t st)
 {
@@ -1245,7 +1362,8 @@ static hipError_t launch_k2_t(const IcwK2Args &a, hipStream_t st)
     constexpr int span = ICW_K2_TILE * ICW_K2_TPW;
     dim3 grid((a.T + span - 1) / span, a.n_streams);
     const size_t lds = (size_t)a.n_regs * 4 * ICW_K2_TILE * sizeof(double);
-    if (a.trig) hipLaunchKernelGGL((icw_output<N, K, true>), grid, dim3(ICW_K2_TILE), lds, st, a);
+    if (a.fes && !a.cw) hipLaunchKernelGGL((icw_output<N, K, true, true>), grid, dim3(ICW_K2_TILE), lds, st, a);
+    else if (a.trig) hipLaunchKernelGGL((icw_output<N, K, true>), grid, dim3(ICW_K2_TILE), lds, st, a);
     else hipLaunchKernelGGL((icw_output<N, K, false>), grid, dim3(ICW_K2_TILE), lds, st, a);
     return hipGetLastError();
 }
@@ -1280,6 +1398,10 @@ extern "C" hipError_t icw_launch_dither_lane(const IcwK3Args *a, hipStream_t st)
 extern "C" hipError_t icw_launch_render(const IcwK3Args *a, hipStream_t st)
 {
     const int blocks = (a->n_gen + 63) / 64;
+    if (a->fes) {
+        hipLaunchKernelGGL(icw_render_fc, dim3(blocks), dim3(64), 0, st, *a);
+        return hipGetLastError();
+    }
     /* the tap counts of the canned shapers (sound_render.c:75-235): FIR 5, 9, 15, 16, 20; IIR 4 */
     const int nn = a->rk.ns_n;
     if (a->rk.ns_kind == 0) {

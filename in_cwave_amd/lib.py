@@ -151,6 +151,13 @@ class Context:
         buf = (C.c_uint8 * len(blob)).from_buffer_copy(blob)
         _check(self._lib.icw_set_state(self.h, s, buf, len(blob)), "icw_set_state")
 
+    def fp_census(self, s, reset=False):
+        """icw_get_fp_census: uint32 [4, 7] (Hilbert L, R, render L, R) x (total, snan, qnan, ninf,
+        nden, pden, pinf)"""
+        buf = (C.c_uint32 * (4 * abi.FES_N))()
+        _check(self._lib.icw_get_fp_census(self.h, s, 1 if reset else 0, buf), "icw_get_fp_census")
+        return np.frombuffer(bytes(buf), dtype=np.uint32).reshape(4, abi.FES_N).copy()
+
     def last_k1_kernel(self):
         """ICW_K1_* of the last real-input call: 0 lane-per-chain, 1 pair, 2 MFMA, 3 row broadcast"""
         return int(self._lib.icw_last_k1_kernel(self.h))

@@ -135,6 +135,9 @@ typedef struct icw_config {
     int32_t  bypass_list;         /* am.is_bypass_list */
     uint32_t seed_left, seed_right;
     icw_render_cfg render;
+    int32_t  fp_check;            /* FP_CHECK (default 0): the FC() arithmetic and census of
+                                     fp_check.c:52-100 in the IIR (hblpf.c:928-950, 1058-1095) and
+                                     the render (sound_render.c:403-489, 815-903); icw_get_fp_census */
 } icw_config;
 
 /* Per-stream meters (the reference keeps them global in `am`, adv_modulator.c:54-56). */
@@ -215,7 +218,15 @@ int icw_last_timing(icw_ctx *ctx, double ms[2], int launches[2]);
 #define ICW_K1_PAIR   1   /* icw_iir_pair: chain + helper wave (experimental) */
 #define ICW_K1_MFMA   2   /* icw_iir_state_mf: MFMA product feed (experimental) */
 #define ICW_K1_ROW    3   /* icw_iir_row: one 16-lane DPP row per chain */
+#define ICW_K1_FC     4   /* icw_iir_state_fc: FP_CHECK (cfg.fp_check) arithmetic and census */
 int icw_last_k1_kernel(const icw_ctx *ctx);
+
+/* FP-exception census of stream s (FP_EXCEPT_STATS, fp_check.h:62-72) when cfg.fp_check is set:
+ * counts[0] Hilbert left (mc->fes_hilb_left), [1] Hilbert right, [2] render left (fes_sr_left),
+ * [3] render right; each {total, snan, qnan, ninf, nden, pden, pinf}.  reset != 0 clears them
+ * afterwards (except_stats_reset, fp_check.c:36-48). */
+#define ICW_FES_N 7
+int icw_get_fp_census(icw_ctx *ctx, int s, int reset, uint32_t counts[4][ICW_FES_N]);
 
 const char *icw_version(void);
 const char *icw_strerror(int status);

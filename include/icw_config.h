@@ -32,7 +32,7 @@ typedef struct icw_file_config {
     int32_t  clr_nframe, clr_hilb;               /* CLR_NFRAME_PT, CLR_HILB_PT */
     double   subnorm_thr;                        /* IIR_SUBN_THR: read and bounded, unused on the
                                                     path (the reject compares with 1.0, hblpf.c:1046) */
-    int32_t  fp_check;                           /* FP_CHECK: read; the FP census is not on the path */
+    int32_t  fp_check;                           /* FP_CHECK (also copied to cfg.fp_check) */
     uint32_t ver_config;                         /* VER_CONFIG */
     int32_t  n_nodes;                            /* NODE_DSP lines in file order = list head first */
     icw_node nodes[ICW_CFG_MAX_NODES];

@@ -114,11 +114,38 @@ static double mt_dsopen(orc_mt *m)
     return r;
 }
 
+/* ------------------------------------------ FP-exception census (fp_check.c:52-100) ------ */
+/* FP_EXCEPT_STATS (fp_check.h:62-72): total, snan, qnan, ninf, nden, pden, pinf.  FC(v) returns v
+ * unless it is a NaN / denormal (-> 0.0) or an infinity (-> +-INF_HUGE_VALUE = +-65535.0,
+ * fp_check.h:60), counting the class when the census is enabled.  _fpclass: a NaN with the quiet
+ * bit (mantissa bit 51) clear is signaling. */
+typedef struct { int on; uint32_t c[ICW_FES_N]; } orc_fes;
+
+static double fc(double v, orc_fes *f)
+{
+    if (!f->on) return v;
+    uint64_t u;
+    memcpy(&u, &v, 8);
+    const unsigned ex = (unsigned)((u >> 52) & 0x7ffu);
+    const uint64_t man = u & 0xfffffffffffffULL;
+    const int neg = (int)(u >> 63);
+    if (ex == 0x7ffu) {
+        ++f->c[0];
+        if (man) { ++f->c[(man >> 51) & 1u ? 2 : 1]; return 0.0; }
+        if (neg) { ++f->c[3]; return -65535.0; }
+        ++f->c[6];
+        return 65535.0;
+    }
+    if (ex == 0u && man) { ++f->c[0]; ++f->c[neg ? 4 : 5]; return 0.0; }
+    return v;
+}
+
 /* ------------------------------------------------------------ HB LPF IIR (hblpf.c) -------- */
 typedef struct {
     double pc[ICW_MAX_IIR_ORDER], pd[ICW_MAX_IIR_ORDER], pz[ICW_MAX_IIR_ORDER], d0;
     int nord, ix, kahan, subn;
     uint64_t sncnt;
+    orc_fes *fes;                      /* the converter's census (mc->fes_hilb_left / _right) */
 } orc_iir;
 
 static void iir_init(orc_iir *f, int type, int kahan, int subn)
@@ -149,6 +176,60 @@ static inline void kh_step(double x, kh *k)
     k->T = k->S + k->Y;
     k->C = (k->T - k->S) - k->Y;
     k->S = k->T;
+}
+
+/* kahan_step_fes (hblpf.c:995-1005) */
+static inline void kh_step_fc(double x, kh *k, orc_fes *fe)
+{
+    k->Y = fc(x - k->C, fe);
+    k->T = fc(k->S + k->Y, fe);
+    k->C = fc(fc(k->T - k->S, fe) - k->Y, fe);
+    k->S = k->T;
+}
+
+/* the WITH FP CHECKS branches of iir_rp_process_baseline / _kahan (hblpf.c:928-950, 1058-1095) */
+static double iir_baseline_fc(double x, orc_iir *f)
+{
+    orc_fes *fe = f->fes;
+    double si = x, so = 0.0;
+    int k = f->ix;
+    for (int i = 0; i < f->nord; ++i) {
+        if (k == 0) k = f->nord;
+        --k;
+        si = fc(si + fc(f->pz[k] * f->pc[i], fe), fe);
+        so = fc(so + fc(f->pz[k] * f->pd[i], fe), fe);
+    }
+    if (f->subn && fabs(si) < 1.0) { si = 0.0; ++f->sncnt; }
+    f->pz[f->ix] = si;
+    if (++f->ix >= f->nord) f->ix = 0;
+    return fc(fc(si * f->d0, fe) + so, fe);
+}
+
+static double iir_kahan_fc(double x, orc_iir *f)
+{
+    orc_fes *fe = f->fes;
+    kh si, so;
+    double t;
+    int k = f->ix;
+    si.S = x; si.C = 0.0;
+    if (k == 0) k = f->nord;
+    --k;
+    t = fc(f->pz[k] * f->pc[0], fe);
+    kh_step_fc(t, &si, fe);
+    so.S = fc(f->pz[k] * f->pd[0], fe); so.C = 0.0;
+    kh_step_fc(fc(t * f->d0, fe), &so, fe);
+    for (int i = 1; i < f->nord; ++i) {
+        if (k == 0) k = f->nord;
+        --k;
+        t = fc(f->pz[k] * f->pc[i], fe);
+        kh_step_fc(t, &si, fe);
+        kh_step_fc(fc(f->pz[k] * f->pd[i], fe), &so, fe);
+        kh_step_fc(fc(t * f->d0, fe), &so, fe);
+    }
+    if (f->subn && fabs(si.S) < 1.0) { si.S = 0.0; ++f->sncnt; }
+    f->pz[f->ix] = si.S;
+    if (++f->ix >= f->nord) f->ix = 0;
+    return so.S;
 }
 
 static double iir_baseline(double x, orc_iir *f)
@@ -193,7 +274,11 @@ static double iir_kahan(double x, orc_iir *f)
     return so.S;
 }
 
-static inline double iir_run(double x, orc_iir *f) { return f->kahan ? iir_kahan(x, f) : iir_baseline(x, f); }
+static inline double iir_run(double x, orc_iir *f)
+{
+    if (f->fes && f->fes->on) return f->kahan ? iir_kahan_fc(x, f) : iir_baseline_fc(x, f);
+    return f->kahan ? iir_kahan(x, f) : iir_baseline(x, f);
+}
 
 /* ------------------------------------------------- quadrature Hilbert (lpf_hilbert_quad.c) */
 typedef struct { orc_iir I, Q; unsigned k; } orc_hq;
@@ -218,6 +303,7 @@ typedef struct {
     int ns_kind, ns_n, ns_ix;
     double ns_c[2 * ICW_MAX_NS_TAPS], ns_e[ICW_MAX_NS_TAPS], ns_o[ICW_MAX_NS_TAPS];
     orc_mt mt;
+    orc_fes fes;                       /* mc->fes_sr_left / _right */
 } orc_render;
 
 static void render_recalc(orc_render *r)
@@ -263,12 +349,30 @@ static void render_init(orc_render *r, const icw_render_cfg *cfg, int is24, uint
     render_recalc(r);
 }
 
+/* ns_empty / ns_fir / ns_iir (sound_render.c:396-489); FC branches at 428-433, 474-486 */
 static double ns_filter(double val, orc_render *r)
 {
     double res = 0.0;
     unsigned ib, ic, n = (unsigned)r->ns_n;
+    orc_fes *fe = &r->fes;
     if (r->ns_kind == 0) return 0.0;
     if (r->ns_ix) --r->ns_ix; else r->ns_ix = (int)n - 1;
+    if (fe->on) {
+        r->ns_e[ib = (unsigned)r->ns_ix] = fc(val, fe);
+        if (r->ns_kind == 1) {
+            for (ic = 0; ic < n; ++ic) {
+                res = fc(res + fc(r->ns_c[ic] * r->ns_e[ib], fe), fe);
+                if (++ib >= n) ib = 0;
+            }
+        } else {
+            for (ic = 0; ic < n; ++ic) {
+                res = fc(res + fc(fc(r->ns_c[ic] * r->ns_e[ib], fe) - fc(r->ns_c[ic + n] * r->ns_o[ib], fe), fe), fe);
+                if (++ib >= n) ib = 0;
+            }
+            r->ns_o[(r->ns_ix ? r->ns_ix : (int)n) - 1] = res;
+        }
+        return res;
+    }
     r->ns_e[ib = (unsigned)r->ns_ix] = val;
     if (r->ns_kind == 1) {
         for (ic = 0; ic < n; ++ic) {
@@ -301,10 +405,20 @@ static int render_value(unsigned char **buf, double input, uint32_t *clips, doub
         break;
     default: break;
     }
-    input = (input * r->norm_mul) - r->prev_ns_err;
-    q = input + (rnd * r->dth_mul);
-    if (q < 0.0) { q -= r->round_offset; delta = r->sign_delta; }
-    else { q += r->round_offset; delta = 0; }
+    orc_fes *fe = &r->fes;
+    if (fe->on) {
+        /* sound_render.c:815-870 with FC: the dither sums are multiples of 2^-53 below 12 in
+         * magnitude (never special), so their FC() are identities and are not restated */
+        input = fc(fc(input * r->norm_mul, fe) - r->prev_ns_err, fe);
+        q = fc(input + fc(rnd * r->dth_mul, fe), fe);
+        if (q < 0.0) { q = fc(q - r->round_offset, fe); delta = r->sign_delta; }
+        else { q = fc(q + r->round_offset, fe); delta = 0; }
+    } else {
+        input = (input * r->norm_mul) - r->prev_ns_err;
+        q = input + (rnd * r->dth_mul);
+        if (q < 0.0) { q -= r->round_offset; delta = r->sign_delta; }
+        else { q += r->round_offset; delta = 0; }
+    }
     if (peak) {
         double cv = fabs(q) / r->hi;
         cv = cv ? 20.0 * log10(cv) : ICW_SR_ZERO_SIGNAL_DB;
@@ -313,7 +427,7 @@ static int render_value(unsigned char **buf, double input, uint32_t *clips, doub
     if (q >= r->hi) { q = r->hi - 1.0; if (clips) ++*clips; }
     if (q <= r->lo) { q = r->lo + 1.0; if (clips) ++*clips; }
     val = ((int)q) + delta;
-    r->prev_ns_err = ns_filter((double)val - input, r);
+    r->prev_ns_err = ns_filter(fe->on ? fc((double)val - input, fe) : (double)val - input, r);
     val <<= r->norm_shift;
     *(*buf)++ = (unsigned char)(val);
     *(*buf)++ = (unsigned char)(val >> 8);
@@ -326,6 +440,7 @@ typedef struct { double lre, lim, rre, rim; } lrc;
 
 typedef struct orc_stream {
     icw_config cfg;
+    orc_fes fes_hilb[2];               /* mc->fes_hilb_left / _right (in_cwave.c:72-79) */
     icw_node nodes[64];
     int n_nodes;
     uint64_t n_frame;
@@ -458,9 +573,12 @@ orc_stream *orc_stream_new(const icw_config *cfg, const icw_node *nodes, int n_n
         iir_init(&s->hq[c].I, (int)cfg->hilbert_type, cfg->iir_kahan, cfg->iir_subnorm_reject);
         iir_init(&s->hq[c].Q, (int)cfg->hilbert_type, cfg->iir_kahan, cfg->iir_subnorm_reject);
         s->hq[c].k = 0;
+        s->fes_hilb[c].on = cfg->fp_check != 0;
+        s->hq[c].I.fes = s->hq[c].Q.fes = &s->fes_hilb[c];
     }
     render_init(&s->rd[0], &cfg->render, cfg->need24bits, cfg->seed_left);
     render_init(&s->rd[1], &cfg->render, cfg->need24bits, cfg->seed_right);
+    s->rd[0].fes.on = s->rd[1].fes.on = cfg->fp_check != 0;
     s->peak[0] = s->peak[1] = ICW_SR_ZERO_SIGNAL_DB;
     s->n_samples = INT64_MAX / 4;
     return s;
@@ -666,6 +784,14 @@ void orc_get_meters(orc_stream *s, icw_meters *m)
 }
 
 uint64_t orc_stream_nframe(orc_stream *s) { return s->n_frame; }
+
+/* census [4][ICW_FES_N]: Hilbert left, right, render left, right */
+void orc_get_fp_census(orc_stream *s, uint32_t *out)
+{
+    const orc_fes *f[4] = {&s->fes_hilb[0], &s->fes_hilb[1], &s->rd[0].fes, &s->rd[1].fes};
+    for (int i = 0; i < 4; ++i)
+        for (int k = 0; k < ICW_FES_N; ++k) out[i * ICW_FES_N + k] = f[i]->c[k];
+}
 
 /* Process many independent streams back to back (the timed CPU baseline, bench.py). */
 int orc_process_many(orc_stream **ss, int n_streams, const void *in, size_t in_stride,

@@ -42,6 +42,7 @@ def load():
         lib.orc_process_many.restype = C.c_int
         lib.orc_process_many.argtypes = [C.POINTER(vp), C.c_int, vp, C.c_size_t, vp, C.c_size_t, C.c_uint]
         lib.orc_get_meters.argtypes = [vp, C.POINTER(abi.Meters)]
+        lib.orc_get_fp_census.argtypes = [vp, C.POINTER(C.c_uint32)]
         lib.orc_stream_nframe.restype = C.c_uint64
         lib.orc_stream_nframe.argtypes = [vp]
         lib.orc_iir_block.argtypes = [C.c_int, C.c_int, C.c_int, vp, C.c_int, vp, vp, C.POINTER(C.c_uint64)]
@@ -115,6 +116,12 @@ class Stream:
     def n_frame(self):
         return load().orc_stream_nframe(self.h)
 
+    def fp_census(self):
+        """FP_EXCEPT_STATS [4, 7]: Hilbert L, R, render L, R (fp_check.h:62-72)"""
+        buf = (C.c_uint32 * (4 * abi.FES_N))()
+        load().orc_get_fp_census(self.h, buf)
+        return np.frombuffer(bytes(buf), dtype=np.uint32).reshape(4, abi.FES_N).copy()
+
 
 def iir_block(x, type_=1, kahan=1, subn=1):
     x = np.ascontiguousarray(x, dtype=np.float64)
@@ -178,8 +185,9 @@ class MT:
         return self.lib.orc_mt_dsopen(self.h)
 
 
-def process_streams(cfg, nodes, raw, n_frames, want_pre=False, n_samples=None):
-    """Run every row of raw [S, bytes] through its own fresh oracle stream."""
+def process_streams(cfg, nodes, raw, n_frames, want_pre=False, n_samples=None, census=None):
+    """Run every row of raw [S, bytes] through its own fresh oracle stream.  census (a list):
+    receives each stream's FP-exception census [4, 7]."""
     outs, pres = [], []
     for s in range(raw.shape[0]):
         st = Stream(cfg, nodes)
@@ -188,4 +196,6 @@ def process_streams(cfg, nodes, raw, n_frames, want_pre=False, n_samples=None):
         o, p = st.process(raw[s], n_frames, want_pre)
         outs.append(o)
         pres.append(p)
+        if census is not None:
+            census.append(st.fp_census())
     return np.stack(outs), (np.stack(pres) if want_pre else None)

@@ -10,6 +10,7 @@ checks.  These are what pins the oracle before it is trusted as the GPU checker:
   * render / reader / graph arithmetic: quirks stated in SURVEY 0 (subnorm threshold 1.0,
     MID_RISER range [-32767, 32767], clip counting).
 """
+import ctypes as C
 import json
 import struct
 from pathlib import Path
@@ -162,7 +163,8 @@ def test_e2e_golden_regression(oracle):
     """the committed oracle vectors still reproduce (guards the restatement against drift)"""
     for p in sorted(GOLD.glob("e2e_*.npz")):
         g = np.load(p)
-        cfg = abi.Config.from_buffer_copy(g["cfg"].tobytes())
+        raw_cfg = g["cfg"].tobytes()        # fixtures predate cfg.fp_check: zero-extend (off)
+        cfg = abi.Config.from_buffer_copy(raw_cfg + bytes(C.sizeof(abi.Config) - len(raw_cfg)))
         nodes = list((abi.Node * (g["nodes"].size // C_sizeof_node())).from_buffer_copy(g["nodes"].tobytes()))
         raw = g["raw"]
         fsz = abi.FMT_BYTES[cfg.in_format] * cfg.in_channels
