@@ -14,7 +14,7 @@ S_ADD_REIM, S_SUB_REIM, S_RE, S_IM = 0, 1, 2, 3
 XCH_NORMAL, XCH_SWAP, XCH_LEFTONLY, XCH_RIGHTONLY, XCH_MIXLR = 0, 1, 2, 3, 4
 # input formats (HRW_FMT_*)
 FMT_U8, FMT_I16, FMT_I24, FMT_I32, FMT_F32 = 0, 1, 2, 3, 4
-K1_LANE, K1_PAIR, K1_MFMA, K1_ROW, K1_FC = 0, 1, 2, 3, 4      # icw_last_k1_kernel (include/icw.h)
+K1_LANE, K1_ROW, K1_FC = 0, 3, 4      # icw_last_k1_kernel (include/icw.h)
 FES_N = 7     # FP_EXCEPT_STATS counters: total, snan, qnan, ninf, nden, pden, pinf
 # complex CWAVE formats: ICW_FMT_CW_F64 + HCW_FMT_* (cwave.h:70-80), Hilbert bypassed
 FMT_CW_F64, FMT_CW_I16, FMT_CW_I16_F32, FMT_CW_F32 = 5, 6, 7, 8

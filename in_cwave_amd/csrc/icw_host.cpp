@@ -23,9 +23,7 @@
 #include "icw_tables.inc"
 
 extern "C" hipError_t icw_launch_unpack(const IcwK0Args *a, hipStream_t st);
-extern "C" hipError_t icw_launch_iir_pair(const IcwK1Args *a, int nord, int kahan, int subn, hipStream_t st);
 extern "C" hipError_t icw_launch_iir_state(const IcwK1Args *a, int nord, int kahan, int subn, hipStream_t st);
-extern "C" hipError_t icw_launch_iir_mfma(const IcwK1Args *a, int nord, int kahan, int subn, hipStream_t st);
 extern "C" hipError_t icw_launch_iir_row(const IcwK1Args *a, int nord, int kahan, int subn, hipStream_t st);
 extern "C" hipError_t icw_launch_iir_fc(const IcwK1Args *a, int nord, int kahan, int subn, hipStream_t st);
 extern "C" hipError_t icw_launch_render(const IcwK3Args *a, hipStream_t st);
@@ -139,8 +137,8 @@ struct icw_ctx {
     hipStream_t stream = nullptr;
     std::vector<hipEvent_t> ev;
     int n_cu = 256;
-    int k1_mode = -1;         /* K1 variant: -1 auto (row / plain), 0 plain lanes, 1 chain+helper wave
-                                 pairs, 2 MFMA product feed, 3 row broadcast (ICW_K1_MODE) */
+    int k1_mode = -1;         /* K1 variant: -1 auto (row / plain), 0 plain lanes, 3 row broadcast
+                                 (ICW_K1_MODE=plain|row, A/B runs) */
     bool dither_lane = false; /* ICW_DITHER=lane: lane-per-channel dither generator (A/B only) */
     bool serialize = false;   /* ICW_SERIALIZE=1: every kernel on the caller's stream (profiling) */
     double last_ms[2]{};
@@ -588,17 +586,9 @@ int icw_create(const icw_config *cfg, const icw_node *nodes, int n_nodes, int n_
     {
         hipDeviceProp_t prop;
         if (hipGetDeviceProperties(&prop, c->device) == hipSuccess) c->n_cu = prop.multiProcessorCount;
-        /* the pair kernel holds ~150 KB LDS -> one 64-chain workgroup per CU; beyond that many
-         * chains the plain kernel (several waves per SIMD, throughput-bound) is the better fit */
-        const long wgs = ((long)S * 4 + 63) / 64;
-        /* measured (profiles/r01_*): the pair kernel's hand-off protocol still costs more than the
-         * instructions it removes from the chain wave, so the plain kernel is the default */
-        (void)wgs;
         c->k1_mode = -1;
         const char *m = getenv("ICW_K1_MODE");
         if (m && !strcmp(m, "plain")) c->k1_mode = 0;
-        if (m && !strcmp(m, "pair")) c->k1_mode = 1;
-        if (m && !strcmp(m, "mfma")) c->k1_mode = 2;
         if (m && !strcmp(m, "row")) c->k1_mode = 3;
         const char *d = getenv("ICW_DITHER");
         c->dither_lane = d && !strcmp(d, "lane");
@@ -769,6 +759,12 @@ int icw_process_streams(icw_ctx *c, int first, int count, const void *in, size_t
     std::lock_guard<std::mutex> lk(c->mu);
     if (set_dev(c)) return ICW_EDEVICE;
     hipStream_t st = hip_stream ? (hipStream_t)hip_stream : c->stream;
+    /* a NULL handle with device pointers means the legacy default stream (what torch's default
+     * stream is): the call starts after the work already queued there and that stream's later work
+     * waits for the call, although the kernels run on the context's own non-blocking streams */
+    const bool legacy = !hip_stream && (flags & ICW_F_DEVICE_PTRS);
+    if (legacy && (hipEventRecord(c->join, nullptr) != hipSuccess || hipStreamWaitEvent(st, c->join, 0) != hipSuccess))
+        return ICW_EDEVICE;
     const icw_config &cfg = c->cfg;
     const unsigned csz = fmt_size(cfg.in_format);
     const unsigned nch = cfg.in_channels;
@@ -857,7 +853,7 @@ int icw_process_streams(icw_ctx *c, int first, int count, const void *in, size_t
     } else if (!cw) {
         /* plain K1: 128-lane groups of 32 streams (64 with the dedup); the variants: a lane per chain */
         const int k1_waves = (k1_mode == 0 || k1_mode == ICW_K1_FC) ? ((count + (dedup ? 63 : 31)) / (dedup ? 64 : 32)) * 2
-                           : k1_mode == 3 ? row_waves : (count * 4 + 63) / 64;
+                           : row_waves;
         const int k1_cus = (k1_waves + c->k1_wpc - 1) / c->k1_wpc;
         if (c->cu_split && k1_cus * 2 <= c->n_cu) {
             const CuSplit *cs = cu_split(c, k1_cus);
@@ -952,8 +948,6 @@ int icw_process_streams(icw_ctx *c, int first, int count, const void *in, size_t
             if (timing) hipEventRecord(c->ev[4 * b], sK);
             const hipError_t e1 = k1_mode == ICW_K1_FC ? icw_launch_iir_fc(&a1, N, cfg.iir_kahan, cfg.iir_subnorm_reject, sK)
                                 : k1_mode == 3 ? icw_launch_iir_row(&a1, N, cfg.iir_kahan, cfg.iir_subnorm_reject, sK)
-                                : k1_mode == 2 ? icw_launch_iir_mfma(&a1, N, cfg.iir_kahan, cfg.iir_subnorm_reject, sK)
-                                : k1_mode == 1 ? icw_launch_iir_pair(&a1, N, cfg.iir_kahan, cfg.iir_subnorm_reject, sK)
                                                : icw_launch_iir_state(&a1, N, cfg.iir_kahan, cfg.iir_subnorm_reject, sK);
             if (e1 != hipSuccess) return ICW_EDEVICE;
             if (timing) hipEventRecord(c->ev[4 * b + 1], sK);
@@ -1106,6 +1100,8 @@ int icw_process_streams(icw_ctx *c, int first, int count, const void *in, size_t
         av.scaled = cfg.frmod_scaled;
         if (icw_launch_advance(&av, st) != hipSuccess) return ICW_EDEVICE;
     }
+    if (legacy && (hipEventRecord(c->join, st) != hipSuccess || hipStreamWaitEvent(nullptr, c->join, 0) != hipSuccess))
+        return ICW_EDEVICE;
     if (!dev) {
         if (hipMemcpy2DAsync(out, out_stride, d_out, dos, dos, S, hipMemcpyDeviceToHost, st) != hipSuccess)
             return ICW_EDEVICE;
@@ -1149,14 +1145,25 @@ int icw_synchronize(icw_ctx *c)
     return ICW_OK;
 }
 
+/* amod_get_clips_peaks (adv_modulator.c:445-465): with isReset the clip counters and peaks are
+ * cleared FIRST and the cleared values (0, SR_ZERO_SIGNAL_DB) are returned; the de-subnorm count
+ * (mod_context_get_desubnorm_counter, in_cwave.c:300-310) is not reset by it.  The meters are
+ * written by kernels that may still run (ICW_F_DEVICE_PTRS calls return early, on several
+ * streams), so the read waits for the context's work first, as get_state does. */
 int icw_get_meters(icw_ctx *c, int s, int reset, icw_meters *m)
 {
     if (!c || !m || s < 0 || s >= c->n_streams) return ICW_EINVAL;
     std::lock_guard<std::mutex> lk(c->mu);
-    if (set_dev(c)) return ICW_EDEVICE;
+    if (set_dev(c) || quiesce(c) != hipSuccess) return ICW_EDEVICE;
     uint32_t cl[2];
     unsigned long long pb[2], sn[4];
-    bool ok = hipMemcpy(cl, c->st.clips + (size_t)s * 2, sizeof(cl), hipMemcpyDeviceToHost) == hipSuccess;
+    bool ok = true;
+    if (reset) {
+        ok &= hipMemset(c->st.clips + (size_t)s * 2, 0, sizeof(cl)) == hipSuccess;
+        ok &= hipMemset(c->st.peak_bits + (size_t)s * 2, 0, sizeof(pb)) == hipSuccess;
+        c->peak_db[(size_t)s * 2] = c->peak_db[(size_t)s * 2 + 1] = ICW_SR_ZERO_SIGNAL_DB;
+    }
+    ok &= hipMemcpy(cl, c->st.clips + (size_t)s * 2, sizeof(cl), hipMemcpyDeviceToHost) == hipSuccess;
     ok &= hipMemcpy(pb, c->st.peak_bits + (size_t)s * 2, sizeof(pb), hipMemcpyDeviceToHost) == hipSuccess;
     ok &= hipMemcpy(sn, c->st.sncnt + (size_t)s * 4, sizeof(sn), hipMemcpyDeviceToHost) == hipSuccess;
     if (!ok) return ICW_EDEVICE;
@@ -1173,12 +1180,6 @@ int icw_get_meters(icw_ctx *c, int s, int reset, icw_meters *m)
         m->peak_db[ch] = pv;
     }
     m->desubnorm = sn[0] + sn[1] + sn[2] + sn[3];
-    if (reset) {
-        ok = hipMemset(c->st.clips + (size_t)s * 2, 0, sizeof(cl)) == hipSuccess;
-        ok &= hipMemset(c->st.peak_bits + (size_t)s * 2, 0, sizeof(pb)) == hipSuccess;
-        c->peak_db[(size_t)s * 2] = c->peak_db[(size_t)s * 2 + 1] = ICW_SR_ZERO_SIGNAL_DB;
-        if (!ok) return ICW_EDEVICE;
-    }
     return ICW_OK;
 }
 
@@ -1186,7 +1187,7 @@ int icw_n_frame(icw_ctx *c, int s, uint64_t *nf)
 {
     if (!c || !nf || s < 0 || s >= c->n_streams) return ICW_EINVAL;
     std::lock_guard<std::mutex> lk(c->mu);
-    if (set_dev(c)) return ICW_EDEVICE;
+    if (set_dev(c) || quiesce(c) != hipSuccess) return ICW_EDEVICE;
     unsigned long long v = 0;
     if (hipMemcpy(&v, c->st.n_frame + s, sizeof(v), hipMemcpyDeviceToHost) != hipSuccess) return ICW_EDEVICE;
     *nf = v;

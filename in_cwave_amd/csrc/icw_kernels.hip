@@ -20,6 +20,7 @@
 
 #include "../../include/icw.h"
 #include "icw_device.h"
+#include "icw_libm.h"
 
 #pragma clang fp contract(off)
 
@@ -339,17 +340,19 @@ __device__ __forceinline__ int icw_render_round(double input, const IcwRenderK &
     return (v + delta) << k.norm_shift;
 }
 
-/* modulator frame counter -> norm_omega of frame t of the block (adv_modulator.c:611-625);
- * n0 is the block-start counter (< ssr in scaled mode) */
+/* modulator frame counter -> norm_omega of frame t of the call (adv_modulator.c:611-625).
+ * n0 is the call-start counter.  In scaled mode the reference takes the first frame's omega from
+ * the raw counter and wraps only when it advances (n = (n + 1) % scale_sr), so a counter left at or
+ * above a new, lower scale by a track switch (icw_set_input without clr_nframe) is used as is once,
+ * and frame t >= 1 sees (n0 + t) mod scale_sr. */
 __device__ __forceinline__ double icw_omega(unsigned long long n0, long long t, int scaled, unsigned long long ssr,
                                             uint32_t sample_rate)
 {
-    /* n0: the counter at the call's start (< ssr when scaled); t: frames since then */
     if (scaled) {
-        /* (n0 + t) mod ssr; n0 < ssr, so one subtraction covers any call shorter than ssr frames
-         * (1000 s of audio) -- the 64-bit remainder is the rare path */
+        /* n0 < ssr except after a rate change, so one subtraction covers any call shorter than ssr
+         * frames (1000 s of audio) -- the 64-bit remainder is the rare path */
         unsigned long long n = n0 + (unsigned long long)t;
-        if (n >= ssr) n = (n - ssr < ssr) ? n - ssr : n % ssr;
+        if (t != 0 && n >= ssr) n = (n - ssr < ssr) ? n - ssr : n % ssr;
         return (2.0 * ICW_PI) * ((double)n) / ((double)ssr);
     }
     return (2.0 * ICW_PI) * ((double)(n0 + (unsigned long long)t)) / (double)sample_rate;
@@ -357,16 +360,19 @@ __device__ __forceinline__ double icw_omega(unsigned long long n0, long long t, 
 
 /* The rotation factor e^{j phi} of channel c of an active Shift / PM node at norm_omega
  * (dsp_shift adv_modulator.c:519-550, dsp_pm adv_modulator.c:554-583).  The one definition used by
- * the per-frame table kernel and by the inline path, so both produce the same bits. */
+ * the per-frame table kernel and by the inline path, so both produce the same bits.  fmod is exact;
+ * cos / sin are glibc's own (icw_libm.h): the reference's cos + sin pair is one sincos() call in a
+ * gcc build, PM's inner sin() is glibc's FMA variant -- so the factors, and everything after them,
+ * are bit-identical to the CPU path. */
 __device__ __forceinline__ void icw_trig(const IcwOp &op, int c, double omega, double &cs, double &sn)
 {
     const double ph = fmod(omega * op.f[c], 2.0 * ICW_PI);
     if (op.mode == ICW_MODE_SHIFT) {
-        sincos(ph, &sn, &cs);
+        icw_lm_sincos(ph, sn, cs);
         if (op.neg[c]) sn = -sn;
     } else {
-        const double psi = op.lp[c] * (sin(ph + op.pp[c]) + op.fa[c]);
-        sincos(psi, &sn, &cs);
+        const double psi = op.lp[c] * (icw_lm_sin_fma(ph + op.pp[c]) + op.fa[c]);
+        icw_lm_sincos(psi, sn, cs);
     }
 }
 

@@ -185,7 +185,11 @@ int icw_set_input(icw_ctx *ctx, uint32_t sample_rate, uint32_t fmt, uint32_t cha
  *   out : stream s starts at (char*)out + s*out_stride_bytes, interleaved L,R, 2 or 3 bytes LE.
  *   dbg : ICW_F_DEBUG_PRE only -- double[n_streams][n_frames][2] pre-render values (lOut,rOut).
  * Host pointers are staged through pinned buffers; with ICW_F_DEVICE_PTRS nothing crosses
- * PCIe.  hip_stream: a hipStream_t or NULL for the context's own stream.  Returns ICW_OK. */
+ * PCIe.  hip_stream: the hipStream_t the call is ordered on (it starts after the work queued there,
+ * and the stream's later work sees its results).  NULL: with host pointers the context's own
+ * stream (the call returns when its output is in `out`); with ICW_F_DEVICE_PTRS the legacy default
+ * stream (stream 0, torch's default stream) -- the call returns before the kernels finish.
+ * icw_get_meters / icw_n_frame / icw_get_state wait for the context's work.  Returns ICW_OK. */
 int icw_process_batch(icw_ctx *ctx, const void *in, size_t in_stride_bytes, void *out,
                       size_t out_stride_bytes, int n_frames, unsigned flags, void *dbg,
                       void *hip_stream);
@@ -195,6 +199,10 @@ int icw_process_streams(icw_ctx *ctx, int first, int count, const void *in,
                         int n_frames, unsigned flags, void *dbg, void *hip_stream);
 
 int icw_synchronize(icw_ctx *ctx);
+/* Meters of stream s (amod_get_clips_peaks, adv_modulator.c:445-465).  reset != 0 clears the clip
+ * counters and peaks FIRST, as the reference does, so the call returns 0 clips and
+ * ICW_SR_ZERO_SIGNAL_DB peaks; the de-subnorm count is not reset (mod_context_get_desubnorm_counter,
+ * in_cwave.c:300-310).  Waits for the context's running work. */
 int icw_get_meters(icw_ctx *ctx, int s, int reset, icw_meters *m);
 int icw_render_size(const icw_ctx *ctx);     /* bytes per output channel-sample: 2 or 3 */
 int icw_n_frame(icw_ctx *ctx, int s, uint64_t *n_frame);
@@ -213,10 +221,9 @@ int icw_last_timing(icw_ctx *ctx, double ms[2], int launches[2]);
 /* IIR state kernel (the serial recurrence) the last real-input icw_process_* call ran: ICW_K1_*.
  * The host picks the row-broadcast kernel for small batches (its waves fit one per SIMD on half
  * the chip, Kahan sum with the reject, no serial render) and the lane-per-chain kernel otherwise;
- * ICW_K1_MODE=plain|row|pair|mfma in the environment at icw_create forces one (A/B runs). */
+ * ICW_K1_MODE=plain|row in the environment at icw_create forces one (A/B runs).  Codes 1 and 2
+ * named two archived experiments (tools/k1_experimental.hip) and are no longer returned. */
 #define ICW_K1_LANE   0   /* icw_iir_state: one lane per DF-II chain */
-#define ICW_K1_PAIR   1   /* icw_iir_pair: chain + helper wave (experimental) */
-#define ICW_K1_MFMA   2   /* icw_iir_state_mf: MFMA product feed (experimental) */
 #define ICW_K1_ROW    3   /* icw_iir_row: one 16-lane DPP row per chain */
 #define ICW_K1_FC     4   /* icw_iir_state_fc: FP_CHECK (cfg.fp_check) arithmetic and census */
 int icw_last_k1_kernel(const icw_ctx *ctx);

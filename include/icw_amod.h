@@ -52,7 +52,8 @@ int icw_mod_context_seek(icw_mod_context *mc, int64_t frame_pos, int reset_hilb)
 /* sound_render_size(L) + sound_render_size(R): output bytes per frame (4 or 6) */
 int icw_mod_context_out_size(const icw_mod_context *mc);
 
-/* amod_get_clips_peaks (adv_modulator.c:445-465) + de-subnorm counter */
+/* amod_get_clips_peaks (adv_modulator.c:445-465): reset clears the clips / peaks first and returns
+ * the cleared values, as the reference does; the de-subnorm count is kept. */
 int icw_mod_context_meters(icw_mod_context *mc, int reset, icw_meters *m);
 
 #ifdef __cplusplus

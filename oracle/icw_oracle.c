@@ -784,6 +784,9 @@ void orc_get_meters(orc_stream *s, icw_meters *m)
 }
 
 uint64_t orc_stream_nframe(orc_stream *s) { return s->n_frame; }
+/* test hook: place the modulator frame counter (mc->n_frame, in_cwave.h:413) anywhere, e.g. just
+ * below the scaled-mode wrap or above a lower rate's scale after a track switch */
+void orc_set_nframe(orc_stream *s, uint64_t n) { s->n_frame = n; }
 
 /* census [4][ICW_FES_N]: Hilbert left, right, render left, right */
 void orc_get_fp_census(orc_stream *s, uint32_t *out)

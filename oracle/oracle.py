@@ -45,6 +45,7 @@ def load():
         lib.orc_get_fp_census.argtypes = [vp, C.POINTER(C.c_uint32)]
         lib.orc_stream_nframe.restype = C.c_uint64
         lib.orc_stream_nframe.argtypes = [vp]
+        lib.orc_set_nframe.argtypes = [vp, C.c_uint64]
         lib.orc_iir_block.argtypes = [C.c_int, C.c_int, C.c_int, vp, C.c_int, vp, vp, C.POINTER(C.c_uint64)]
         lib.orc_iir_coeffs.restype = C.c_int
         lib.orc_iir_coeffs.argtypes = [C.c_int, vp, vp, C.POINTER(C.c_double)]
@@ -115,6 +116,9 @@ class Stream:
 
     def n_frame(self):
         return load().orc_stream_nframe(self.h)
+
+    def set_n_frame(self, n):
+        load().orc_set_nframe(self.h, n)
 
     def fp_census(self):
         """FP_EXCEPT_STATS [4, 7]: Hilbert L, R, render L, R (fp_check.h:62-72)"""

@@ -1,0 +1,170 @@
+"""GPU parity over the modulator's option space: seeded random DSP lists (tests/graphgen.py) through
+libicw against the oracle, bit for bit -- the pre-render doubles and the rendered bytes.
+
+Covers adv_modulator.c:216-299 (amod_init locks), 485-583 (Master conversions, Shift, PM),
+611-751 (frame counter in both modes, list bypass, mix, channel exchange, I/Q inversion, gains).
+The Shift / PM factors are glibc-identical on the device (icw_libm.h), so no case needs a
+tolerance.  Some cases start the frame counter a few hundred frames below the scaled-mode wrap
+(fs * 1000) or far out in exact mode, with all streams in step (the per-frame rotation table)
+or each at its own counter (K2's inline factors / the serial graph kernel)."""
+import numpy as np
+import pytest
+
+from in_cwave_amd import abi, graph, synth
+from tests import graphgen
+
+pytestmark = pytest.mark.gpu
+
+N_CASES = 240
+BATCH = 24
+N_STREAMS = 3
+CALLS = (317, 400)          # two calls: state carried across a call boundary
+
+
+def bus_form(nodes, bypass):
+    """the host's choice (icw_host.cpp compile_graph): a slot read before its writer runs in the
+    tail -> head order is a one-frame delay, and the register program holds <= 16 ops, 8 regs"""
+    if bypass:
+        return False
+    order = list(range(len(nodes) - 1, -1, -1))
+    written = {nodes[i].n_out for i in order if nodes[i].mode != abi.MODE_MASTER}
+    done, regs = set(), 1
+    if len(order) > 16:
+        return True
+    persist = set()
+    for i in order:
+        n = nodes[i]
+        for k in range(abi.N_INPUTS):
+            if not n.inputs[k] or k == 0 or k in done:
+                continue
+            if k in written:
+                return True
+            if k not in persist:
+                persist.add(k)
+                regs += 1
+        if n.mode != abi.MODE_MASTER:
+            done.add(n.n_out)
+            regs += 1
+        if regs > 8:
+            return True
+    return False
+
+
+def counter_start(rng, cfg):
+    """(kind, [n_frame per stream]) -- 0: fresh; near the scaled wrap; far out in exact mode"""
+    r = rng.random()
+    if r < 0.5:
+        return "fresh", [0] * N_STREAMS
+    ssr = cfg.sample_rate * 1000
+    if cfg.frmod_scaled:
+        base = ssr - int(rng.integers(1, 600))
+    else:
+        base = int(rng.integers(1, 1 << 40))
+    if r < 0.75:
+        return "in-step", [base] * N_STREAMS
+    return "staggered", [(base + 97 * s) % ssr if cfg.frmod_scaled else base + 97 * s for s in range(N_STREAMS)]
+
+
+def differing(a, b):
+    """indices where two double arrays differ bit for bit -- except that any NaN equals any NaN:
+    a list with gain > 1 in a feedback loop overflows to inf and then NaN, and a NaN made from
+    inf - inf carries the sign x86 gives its default NaN (negative) on the CPU and the positive
+    canonical NaN on the GPU; the render maps every NaN to the same integer (sound_render.c:800)"""
+    bad = a.view(np.uint64) != b.view(np.uint64)
+    return np.flatnonzero(bad & ~(np.isnan(a) & np.isnan(b)))
+
+
+def set_counter(ctx, s, n):
+    b = abi.StateBlob.from_buffer_copy(ctx.get_state(s))
+    b.n_frame = n
+    ctx.set_state(s, bytes(b))
+
+
+def run_case(oracle, icw, seed):
+    rng = np.random.default_rng(1_000_003 * seed + 17)
+    cfg = graphgen.random_config(rng)
+    nodes = graphgen.random_list(rng)
+    kind, n0 = counter_start(rng, cfg)
+    n_frames = sum(CALLS)
+    raw = synth.batch_pcm(N_STREAMS, n_frames, cfg.sample_rate, first=seed * N_STREAMS)
+    ctx = icw.Context(cfg, nodes, N_STREAMS)
+    if kind != "fresh":
+        for s in range(N_STREAMS):
+            set_counter(ctx, s, n0[s])
+    outs, pres, t = [], [], 0
+    for n in CALLS:
+        o, p = ctx.process(np.ascontiguousarray(raw[:, t * 4:(t + n) * 4]), n, want_pre=True)
+        outs.append(o)
+        pres.append(p)
+        t += n
+    out, pre = np.concatenate(outs, axis=1), np.concatenate(pres, axis=1)
+    for s in range(N_STREAMS):
+        st = oracle.Stream(cfg, nodes)
+        assert st.accepted == ctx.accepted
+        st.set_n_frame(n0[s])
+        ro, rp = st.process(raw[s], n_frames, want_pre=True)
+        bad = differing(pre[s], rp)
+        assert bad.size == 0, (f"seed {seed} stream {s} ({kind}, scaled={cfg.frmod_scaled}, "
+                               f"bypass={cfg.bypass_list}, {len(nodes)} nodes): {bad.size} pre-render "
+                               f"doubles differ, first {bad[:4]}")
+        assert np.array_equal(out[s], ro), f"seed {seed} stream {s}: rendered bytes differ"
+        assert ctx.n_frame(s) == st.n_frame()
+    ctx.close()
+    return bus_form(nodes, cfg.bypass_list), kind, cfg
+
+
+_SEEN = {"bus": 0, "reg": 0, "bypass": 0, "exact": 0, "staggered": 0, "in-step": 0}
+
+
+@pytest.mark.parametrize("batch", range(N_CASES // BATCH))
+def test_random_graphs(oracle, icw, batch):
+    for seed in range(batch * BATCH, (batch + 1) * BATCH):
+        bus, kind, cfg = run_case(oracle, icw, seed)
+        _SEEN["bus" if bus else "reg"] += 1
+        _SEEN["bypass"] += cfg.bypass_list
+        _SEEN["exact"] += 1 - cfg.frmod_scaled
+        if kind in _SEEN:
+            _SEEN[kind] += 1
+
+
+def test_random_graphs_covered_both_forms():
+    """the draw reaches every branch the test is meant for (runs after the batches)"""
+    if sum(_SEEN.values()) == 0:
+        pytest.skip("batches not run in this session")
+    for k, v in _SEEN.items():
+        assert v >= 5, (k, _SEEN)
+
+
+@pytest.mark.parametrize("n_nodes", [1, 2, 4])
+def test_track_switch_to_lower_rate_keeps_raw_counter(oracle, icw, n_nodes):
+    """a 96 kHz track leaves the scaled counter at 50e6 (< 96e6); the next track is 44.1 kHz
+    without clearing it (is_clr_nframe_trk FALSE): the reference takes the first frame's omega
+    from the raw counter, above the new scale 44.1e6, and wraps only when advancing
+    (adv_modulator.c:611-619)"""
+    rng = np.random.default_rng(77 + n_nodes)
+    nodes = [graph.master(inputs=("A",)), graph.shift(inputs=("in",), out="A", fr=3.7)]
+    if n_nodes > 2:
+        nodes = [graph.master(inputs=("C",)), graph.mix(inputs=("in", "B"), out="C"),
+                 graph.shift(inputs=("A",), out="B"), graph.pm(inputs=("in",), out="A", phase=0.3, angle=-0.2)]
+    if n_nodes == 1:
+        nodes = graphgen.random_list(rng, 1)
+    cfg = graph.default_config(96000)
+    raw96 = synth.batch_pcm(2, 500, 96000, first=5)
+    raw44 = synth.batch_pcm(2, 700, 44100, first=9)
+    ctx = icw.Context(cfg, nodes, 2)
+    ref = [oracle.Stream(cfg, nodes) for _ in range(2)]
+    for s in range(2):
+        set_counter(ctx, s, 50_000_000 - 250)
+        ref[s].set_n_frame(50_000_000 - 250)
+    o1, p1 = ctx.process(raw96, 500, want_pre=True)
+    ctx.set_input(44100, abi.FMT_I16, 2)
+    o2, p2 = ctx.process(raw44, 700, want_pre=True)
+    for s in range(2):
+        r1, q1 = ref[s].process(raw96[s], 500, want_pre=True)
+        ref[s].set_input(44100, abi.FMT_I16, 2)
+        r2, q2 = ref[s].process(raw44[s], 700, want_pre=True)
+        assert np.array_equal(p1[s].view(np.uint64), q1.view(np.uint64))
+        assert np.array_equal(p2[s].view(np.uint64), q2.view(np.uint64))
+        assert np.array_equal(o1[s], r1) and np.array_equal(o2[s], r2)
+        assert ctx.n_frame(s) == ref[s].n_frame()
+    ctx.close()

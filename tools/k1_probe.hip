@@ -2,7 +2,7 @@
 // Includes the kernels with ICW_STAMPS so workgroup 0 records s_memtime stamps per sample.
 // Build: hipcc --offload-arch=gfx950 -O3 -ffp-contract=off -std=c++17 -o tools/k1_probe tools/k1_probe.hip
 #define ICW_STAMPS
-#include "../in_cwave_amd/csrc/icw_iir.hip"
+#include "k1_experimental.hip"
 #include <stdio.h>
 #include <string.h>
 #include <stdlib.h>
