@@ -14,12 +14,25 @@ barrier + synchronize around the K timed steps, max elapsed over ranks.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c2|c3|c4|c5]
 
+--gpus N without a launcher (RANK unset) starts N rank processes itself, before anything here
+touches the GPU, and exits with the worst rank's status; under torch.distributed.run the world
+size must equal --gpus.  With fewer devices than ranks (the 1-GPU box) the ranks share devices
+and use gloo for the barrier and the timing reduce (RCCL needs a GPU per rank).
+
 --workload picks one of the BASELINE.json configs; the default, c2, is the one the
 headline metric is quoted on.  The others are measured for DESIGN.md, not for the bench line.
+
+Roofline: the dominant kernel is the serial IIR recurrence K1; its bound is FP64
+VALU issue, so `roofline` reports its algorithmic FP64 rate (the loop-back Kahan sum,
+hblpf.c:1017-1046: 5N flops per chain-sample, 95 for N = 19) against the FP64 vector peak, with
+the HBM rate and the per-wave issue floor as secondary fields.
 """
 import argparse
+import glob
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 from pathlib import Path
@@ -30,21 +43,22 @@ ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT))
 
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
-CLOCK_GHZ = 2.4                # MI355X max engine clock (MI355X_MICROARCH.md chip table)
-# Issue floor of icw_iir_state (DESIGN.md "Roofline"): a lone wave issues one FP64 VALU instruction
-# per ~5.0 cycles, dependent or not, add or mul, whatever the operand banks
-# (profiles/r01_fp64_bank_probe.txt: 5.00 and 5.25 s_memtime ticks per op on two boxes). The
-# recurrence compiles to 91 FP64 VALU per sample on average (71 v_add_f64 + 19 v_mul_f64 + 1
-# v_cmp_f64: the order-19 Kahan loop-back sum with the zero-input steps 4 adds shorter, ISA of
-# icw_iir_state<19,1,1>) plus 2 v_cndmask_b32 -> a floor of ~455 cycles per sample per chain.
-# The row-broadcast kernel icw_iir_row<19> (small batches: C2) issues 75.5 FP64 VALU per sample:
-# nonzero-input samples 1 + 3 + (18 v_fmac_f64_dpp + 52 v_add_f64) + 1 v_cmp + 2 product muls = 77,
-# zero-input samples 2 + 3 + (17 + 49) + 1 + 2 = 74 (plus 2 v_cndmask_b32, as above).
+FP64_PEAK_TFLOPS = 78.6        # MI355X FP64 vector (256 CU x 2.4 GHz x 128 flop/clk), MI355X_MICROARCH.md
+# effective engine clock under the C2 recurrence: SQ_BUSY_CYCLES / 32 shader engines / launch time
+# (profiles/r01_c2_sq_counters.json: 6.48 M cycles per 2.80 ms launch = 2.31 GHz)
+CLOCK_GHZ = 2.31
+# Issue floor of the recurrence: a lone wave issues one FP64 VALU instruction per
+# ~5.0 cycles, dependent or not (profiles/r01_fp64_bank_probe.txt).  icw_iir_state<19> issues 91
+# FP64 VALU per sample (zero-input steps included), icw_iir_row<19> 75.5 (products lane-parallel,
+# the Kahan steps through v_fmac_f64_dpp row_newbcast).
 K1_VALU_PER_SAMPLE = {0: 91, 3: 75.5}          # by ICW_K1_* (icw_last_k1_kernel)
-K1_KERNEL_NAME = {0: "icw_iir_state", 1: "icw_iir_pair", 2: "icw_iir_state_mf", 3: "icw_iir_row"}
+K1_KERNEL_NAME = {0: "icw_iir_state", 3: "icw_iir_row", 4: "icw_iir_state_fc"}
 CYC_PER_FP64_VALU = 5.0
-PMC_FILE = ROOT / "profiles" / "r01_c2_pmc.json"
-FP64_PEAK_TFLOPS = 78.6        # MI355X FP64 vector (256 CU x 2.4 GHz x 128 flop/clk), vendor figure
+
+
+def _latest(pattern):
+    files = sorted(glob.glob(str(ROOT / "profiles" / pattern)))
+    return Path(files[-1]) if files else None
 
 
 # SURVEY 8(d) configurations, per GPU: streams, frames per stream per step, fs, input format,
@@ -61,6 +75,7 @@ WORKLOADS = {
                bytes=14, desc="C5: 256 x 192kHz float32 stereo streams/GPU, Hilbert + Master, 24-bit TPDF + "
                               "MEW44 noise shaping"),
 }
+IIR_ORDER = 19                  # Type-1 filter of every workload (hblpf.c:740-820)
 
 
 def workload_config(w):
@@ -84,14 +99,92 @@ def parse():
     ap.add_argument("--streams", type=int, default=None, help="streams per GPU (default: the workload's)")
     ap.add_argument("--frames", type=int, default=None, help="frames per stream per step (default: the workload's)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-workers", type=int, default=16)
+    ap.add_argument("--cpu-workers", type=int, default=0, help="0: one per physical core available here")
     ap.add_argument("--cpu-frames", type=int, default=1 << 25)
+    ap.add_argument("--e2e-steps", type=int, default=2,
+                    help="extra steps with host buffers (H2D + D2H included), reported beside `value`")
     return ap.parse_args()
 
 
+# ----------------------------------------------------------------------------- launcher -----
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(n):
+    """--gpus N without a launcher: N fresh rank processes of this script (one per GPU), started
+    before this process touches the GPU; the first rank to fail stops the others.  Returns the
+    worst exit status."""
+    port = str(_free_port())
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
+        procs.append(subprocess.Popen([sys.executable, str(Path(__file__).resolve())] + sys.argv[1:], env=env))
+    worst = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            rc = p.poll()
+            if rc is None:
+                continue
+            live.remove(p)
+            if rc != 0:
+                worst = worst or rc
+                for q in live:          # a failed rank leaves the others waiting in a barrier
+                    q.terminate()
+        time.sleep(0.05)
+    for p in procs:
+        p.wait()
+    return worst if worst >= 0 else 128 - worst
+
+
+# ----------------------------------------------------------------------------- CPU leg ------
+def host_cores():
+    """physical cores this process may run on: the affinity set grouped by (package, core id),
+    capped by a cgroup CPU quota; plus the CPU model string"""
+    cpus = sorted(os.sched_getaffinity(0))
+    phys = {}
+    for c in cpus:
+        base = Path(f"/sys/devices/system/cpu/cpu{c}/topology")
+        try:
+            key = (base.joinpath("physical_package_id").read_text().strip(), base.joinpath("core_id").read_text().strip())
+        except OSError:
+            key = ("?", str(c))
+        phys.setdefault(key, c)
+    n = len(phys)
+    quota = None
+    try:
+        q, per = Path("/sys/fs/cgroup/cpu.max").read_text().split()[:2]
+        if q != "max":
+            quota = int(q) / int(per)
+    except (OSError, ValueError):
+        pass
+    if quota:
+        n = max(1, min(n, int(quota)))
+    model = "?"
+    try:
+        for line in Path("/proc/cpuinfo").read_text().splitlines():
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return n, sorted(phys.values())[:n], model, {"affinity_cpus": len(cpus), "physical_in_affinity": len(phys),
+                                                 "cgroup_cpu_quota": quota}
+
+
 def _cpu_worker(args):
-    """one CPU core: the oracle restatement (scalar C, -O2 -ffp-contract=off) over one stream"""
-    s, n_frames, wname = args
+    """one physical core: the oracle restatement (scalar C, -O2 -ffp-contract=off) over one stream"""
+    s, n_frames, wname, cpu = args
+    try:
+        os.sched_setaffinity(0, {cpu})
+    except OSError:
+        pass
     from in_cwave_amd import synth
     from oracle import oracle as O
     w = WORKLOADS[wname]
@@ -104,41 +197,53 @@ def _cpu_worker(args):
 
 
 def cpu_baseline(workers, n_frames, wname):
+    """the oracle's C restatement, one process per physical core, each on one stream of the
+    workload's shape; aggregate = all cores' samples over the slowest core's time"""
     import multiprocessing as mp
     from oracle import oracle as O
     O.load()
+    n_avail, cpus, model, topo = host_cores()
+    workers = workers or n_avail
+    cpus = (cpus * ((workers + len(cpus) - 1) // len(cpus)))[:workers]
     ctx = mp.get_context("spawn")
     t0 = time.perf_counter()
     with ctx.Pool(workers) as pool:
-        per = pool.map(_cpu_worker, [(s, n_frames, wname) for s in range(workers)])
+        per = pool.map(_cpu_worker, [(s, n_frames, wname, cpus[s]) for s in range(workers)])
     wall = time.perf_counter() - t0
-    busy = max(per)
     samples = 2.0 * n_frames * workers
-    return {"value": samples / busy / 1e6, "unit": "Msamples/s", "cores": workers, "kind": "port",
-            "sample": f"{workers} streams x {n_frames} frames ({wname} shape, oracle C restatement, one process "
-                      f"per core), per-core {2.0 * n_frames / np.mean(per) / 1e6:.3f} Msamples/s, wall {wall:.1f}s"}
+    return {"value": samples / max(per) / 1e6, "unit": "Msamples/s", "cores": workers, "kind": "port",
+            "cpu_model": model, "per_core": 2.0 * n_frames / float(np.mean(per)) / 1e6, "topology": topo,
+            "sample": f"{workers} streams x {n_frames} frames ({wname} shape), oracle C restatement "
+                      f"(-O2 -ffp-contract=off), one process pinned per physical core, wall {wall:.1f}s; "
+                      f"the reference's own IIR/graph/render need <windows.h> and are not built here"}
 
 
+# ----------------------------------------------------------------------------- GPU leg ------
 def main():
     a = parse()
-    import torch
-    rank = int(os.environ.get("RANK", "0"))
+    if "RANK" not in os.environ and a.gpus > 1:
+        sys.exit(launch_ranks(a.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != a.gpus:
+        print(f"bench.py: WORLD_SIZE={world} but --gpus {a.gpus}", file=sys.stderr)
+        sys.exit(2)
+    rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch
+    ndev = torch.cuda.device_count()          # counts without initialising the GPU
     dist = None
-    # one process per GPU; ICW_BENCH_BACKEND=gloo + fewer GPUs than ranks is the rehearsal mode of
-    # tests/test_gpu_bench.py (ranks share a device; RCCL needs one GPU per rank)
-    ndev = torch.cuda.device_count()
     local_dev = local % max(1, ndev)
     if world > 1:
         import torch.distributed as dist
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        # ranks sharing a device (the 1-GPU rehearsal) cannot use RCCL
+        backend = "gloo" if ndev < world else os.environ.get("ICW_BENCH_BACKEND", "nccl")
         torch.cuda.set_device(local_dev)
-        dist.init_process_group(os.environ.get("ICW_BENCH_BACKEND", "nccl"), rank=rank, world_size=world)
+        dist.init_process_group(backend, rank=rank, world_size=world)
     dev = torch.device("cuda", local_dev)
     torch.cuda.set_device(dev)
 
-    from in_cwave_amd import graph, synth
+    from in_cwave_amd import synth
     from in_cwave_amd import lib as L
 
     W = WORKLOADS[a.workload]
@@ -196,42 +301,62 @@ def main():
     value = 2.0 * frames_total / elapsed / 1e6
     ms_per_step = elapsed * 1e3 / a.steps
 
-    # roofline of the dominant kernel (icw_iir_state), algorithmic bytes per launch / avg duration
+    # ---- end to end from host memory (H2D + D2H in the loop), one rank's view, not `value`
+    e2e = None
+    if a.e2e_steps > 0 and rank == 0:
+        h_in = np.ascontiguousarray(np.tile(gen, ((S + n_gen - 1) // n_gen, 1))[:S])
+        h_out = np.empty((S, T * osz), dtype=np.uint8)
+        ctx.process(h_in, T, out=h_out)                       # warm the staging buffers
+        te = time.perf_counter()
+        for _ in range(a.e2e_steps):
+            ctx.process(h_in, T, out=h_out)
+        te = time.perf_counter() - te
+        del h_out
+        e2e = {"value": 2.0 * S * T * a.e2e_steps / te / 1e6, "unit": "Msamples/s",
+               "ms_per_step": te * 1e3 / a.e2e_steps, "steps": a.e2e_steps,
+               "note": "host (pageable numpy) input and output: the call stages them through the "
+                       "context's pinned buffers, H2D + kernels + D2H, one GPU"}
+
+    # ---- roofline of the dominant kernel K1 (the serial recurrence), per launch, from HIP events
+    # recorded on the stream K1 runs on (icw_last_timing)
+    k1_kind = ctx.last_k1_kernel()
+    k1_name = K1_KERNEL_NAME.get(k1_kind, "?")
     frames_per_launch = float(S) * T * a.steps / max(1, k1_n)
     k1_avg_s = k1_ms / 1e3 / max(1, k1_n)
     k2_avg_s = k2_ms / 1e3 / max(1, k2_n)
-    alg_bytes = W["bytes"]
-    achieved = alg_bytes * frames_per_launch / k1_avg_s / 1e9 if k1_avg_s > 0 else None
-    flops_per_frame = 4 * 2 * (15 * 19 - 4) / 2    # the recurrence half of 1124 flops/frame
-    k1_kind = ctx.last_k1_kernel()
-    k1_name = K1_KERNEL_NAME.get(k1_kind, "?")
-    valu = K1_VALU_PER_SAMPLE.get(k1_kind)
+    chains_per_stream = 2 if (W["ch"] == 1) else 4        # the mono dedup runs the left chains only
+    flops_per_frame = chains_per_stream * 5 * IIR_ORDER   # loop-back Kahan sum: N x (1 mul + 4 add)
+    achieved_tf = flops_per_frame * frames_per_launch / k1_avg_s / 1e12 if k1_avg_s > 0 else None
+    hbm_gbs = W["bytes"] * frames_per_launch / k1_avg_s / 1e9 if k1_avg_s > 0 else None
     traffic = None
+    pmc_file = _latest("r*_c2_pmc.json")
     try:   # HBM bytes per launch of the same kernel/config from the committed PMC passes
-        pmc = json.loads(PMC_FILE.read_text())
+        pmc = json.loads(pmc_file.read_text())
         if int(pmc["frames_per_launch"]) == int(frames_per_launch) and a.workload == "c2":
             traffic = next(v["hbm_bytes_corrected"] for k, v in pmc["kernels"].items()
-                           if k.split("<")[0].split("(")[0].endswith(k1_name))
+                           if k.split("<")[0].split("(")[0].split()[-1] == k1_name)
     except Exception:
         traffic = None
+    valu = K1_VALU_PER_SAMPLE.get(k1_kind)
     samples_per_chain = frames_per_launch / S
-    issue_floor_ms = (samples_per_chain * valu * CYC_PER_FP64_VALU / (CLOCK_GHZ * 1e6)) if valu else None
+    floor_ms = (samples_per_chain * valu * CYC_PER_FP64_VALU / (CLOCK_GHZ * 1e6)) if valu else None
     roof = {
-        "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-        "frac": (achieved / HBM_PEAK_GBS) if achieved else None, "traffic": traffic,
-        "issue_bound": {"valu_per_sample": valu, "cycles_per_valu": CYC_PER_FP64_VALU,
-                        "clock_ghz": CLOCK_GHZ, "floor_ms_per_launch": issue_floor_ms,
-                        "frac": (issue_floor_ms / (k1_avg_s * 1e3)) if (k1_avg_s and issue_floor_ms) else None},
-        "kernel": k1_name, "alg_bytes_per_frame": alg_bytes,
-        "frames_per_launch": frames_per_launch, "avg_launch_ms": k1_avg_s * 1e3,
-        "output_kernel_avg_launch_ms": k2_avg_s * 1e3,
-        "fp64_tflops_chain": (1124.0 * frames_per_launch / (k1_avg_s + k2_avg_s) / 1e12) if k1_avg_s else None,
-        "fp64_peak_tflops": FP64_PEAK_TFLOPS,
-        "note": f"issue-bound serial IIR recurrence ({4 * S} DF-II chains, 2 per stream with the mono dedup; "
-                f"{'one 16-lane DPP row' if k1_kind == 3 else 'one lane'} per chain), {valu} FP64 VALU per "
-                f"sample; frac ~1 = at the issue floor within the probe's few-% spread (DESIGN.md)",
+        "bound": "fp64", "achieved": achieved_tf, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+        "frac": (achieved_tf / FP64_PEAK_TFLOPS) if achieved_tf else None, "traffic": traffic,
+        "kernel": k1_name, "flops_per_frame": flops_per_frame, "frames_per_launch": frames_per_launch,
+        "avg_launch_ms": k1_avg_s * 1e3, "output_kernel_avg_launch_ms": k2_avg_s * 1e3,
+        "hbm": {"achieved": hbm_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": (hbm_gbs / HBM_PEAK_GBS) if hbm_gbs else None,
+                "alg_bytes_per_frame": W["bytes"], "traffic_source": pmc_file.name if (traffic and pmc_file) else None},
+        "issue_bound": {"valu_per_sample": valu, "cycles_per_valu": CYC_PER_FP64_VALU, "clock_ghz": CLOCK_GHZ,
+                        "floor_ms_per_launch": floor_ms,
+                        "frac": (floor_ms / (k1_avg_s * 1e3)) if (k1_avg_s and floor_ms) else None},
+        "note": f"serial IIR recurrence: {chains_per_stream * S} DF-II chains per GPU, each a dependent "
+                f"chain of ~{4 * IIR_ORDER} FP64 ops per sample ({'one 16-lane DPP row' if k1_kind == 3 else 'one lane'}"
+                f" per chain); `frac` is the algorithmic FP64 rate (5N = {5 * IIR_ORDER} flops per chain-sample) "
+                f"against the FP64 vector peak, small because {chains_per_stream * S} chains cannot fill "
+                f"1024 SIMDs; issue_bound.frac ~1 = at the per-wave issue floor (DESIGN.md 5)",
     }
-    del flops_per_frame
 
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
@@ -250,6 +375,7 @@ def main():
                        "streams_per_gpu": S, "frames_per_stream_per_step": T, "fs": fs,
                        "parallelism": f"stream-shard x{world}"},
             "roofline": roof,
+            "e2e_host_buffers": e2e,
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)

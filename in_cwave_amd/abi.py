@@ -164,6 +164,16 @@ SIGNATURES = {
     "icw_transcode_files": (_i, [C.POINTER(Config), C.POINTER(Node), _i, C.POINTER(C.c_char_p),
                                  C.POINTER(C.c_char_p), _i, C.POINTER(BatchOpts), C.POINTER(BatchStats),
                                  C.POINTER(_i)]),
+    "icw_group_create": (_i, [C.POINTER(Config), C.POINTER(Node), _i, _i, C.POINTER(_i), _i, C.POINTER(_vp),
+                              C.POINTER(_i)]),
+    "icw_group_destroy": (_i, [_vp]),
+    "icw_group_shard": (_i, [_vp, _i, C.POINTER(_i), C.POINTER(_i), C.POINTER(_i), C.POINTER(_vp)]),
+    "icw_group_process": (_i, [_vp, _vp, _sz, _vp, _sz, _i, _u, _vp]),
+    "icw_group_get_meters": (_i, [_vp, _i, _i, C.POINTER(Meters)]),
+    "icw_group_n_frame": (_i, [_vp, _i, C.POINTER(C.c_uint64)]),
+    "icw_transcode_files_devices": (_i, [C.POINTER(Config), C.POINTER(Node), _i, C.POINTER(C.c_char_p),
+                                         C.POINTER(C.c_char_p), _i, C.POINTER(BatchOpts), C.POINTER(_i), _i,
+                                         C.POINTER(BatchStats), C.POINTER(_i)]),
     "icw_version": (C.c_char_p, []),
     "icw_strerror": (C.c_char_p, [_i]),
 }

@@ -22,6 +22,7 @@ struct IcwProg;
 
 /* Arguments of the input prep kernel (one thread = one frame). */
 struct IcwK0Args {
+    uint32_t lds_guard;            /* dynamic LDS bytes: > 0 keeps the launch off the CUs K1 holds */
     const unsigned char *in;       /* stream s at in + s*in_stride */
     size_t in_stride;
     uint32_t fmt, csz, fsz, nch;   /* sample format, channel/frame bytes, channels */
@@ -40,6 +41,7 @@ struct IcwK0Args {
  * kernel reads the call-start position / phases / frame counter and adds its block offset; this
  * kernel advances them once, after the last block. */
 struct IcwAdvArgs {
+    uint32_t lds_guard;            /* dynamic LDS bytes: > 0 keeps the launch off the CUs K1 holds */
     int32_t n_streams, cw;
     long long n;                   /* frames processed by the call */
     uint32_t *hq_phase;
@@ -51,6 +53,7 @@ struct IcwAdvArgs {
 
 /* Arguments of the serial graph kernel (bus form; one lane = one stream, loops over frames). */
 struct IcwK4Args {
+    uint32_t lds_guard;            /* dynamic LDS bytes: > 0 keeps the launch off the CUs K1 holds */
     const double *iq;              /* [n_streams][T][4] `in` per frame (lre, lim, rre, rim) */
     int32_t n_streams, T;
     long long t0;
@@ -80,7 +83,9 @@ struct IcwK1Args {
     const uint32_t *hq_phase;      /* [n_streams][2] call-start Hilbert phases (zero-input parity) */
     long long t0;                  /* block offset into the call */
     int *err;                      /* set by a bounded spin that gave up (never in a healthy run) */
-    int32_t wg_waves;              /* waves per workgroup of the plain / MFMA kernels (1..4) */
+    int32_t wg_waves;              /* waves per workgroup of the plain / row kernels (1..4) */
+    uint32_t lds_hold;             /* LDS bytes a K1 workgroup holds (static + dynamic): the CU's whole
+                                      LDS keeps every LDS-using workgroup off K1's CUs; 0: static only */
     int32_t dedup;                 /* mono, every stream's converters identical: left chains only */
     double pc[20];                 /* loop-back coefficients -a[i+1]/a0 */
     uint32_t *fes;                 /* FP_CHECK: [n_streams][4][ICW_FES_PITCH] census (Hilbert L, R,
@@ -193,6 +198,7 @@ struct IcwK2Args {
 /* Per-frame rotation table (one thread per frame): the Shift / PM factors depend only on the frame
  * counter, so streams in step share them -- computed once per block, not once per stream. */
 struct IcwTrigArgs {
+    uint32_t lds_guard;            /* dynamic LDS bytes: > 0 keeps the launch off the CUs K1 holds */
     const IcwProg *prog;
     const unsigned long long *n_frame;   /* the reference stream's call-start counter (stream 0) */
     long long t0;

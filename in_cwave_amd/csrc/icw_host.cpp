@@ -106,6 +106,8 @@ struct icw_ctx {
     bool cu_split = true;                 /* ICW_CU_SPLIT=0 disables the partition */
     int k1_wpc = 4;                       /* ICW_K1_WPC: K1 waves per CU (one per SIMD) */
     int k1_wg = 1;                        /* ICW_K1_WG: K1 waves per workgroup */
+    bool k1_lds = false;                  /* ICW_K1_LDS=1: K1 workgroups hold the CU's LDS (A/B) */
+    uint32_t lds_cu = 0;                  /* LDS bytes per CU a workgroup may hold */
     int max_block = kDefBlockFrames;      /* ICW_BLOCK: frames per launch block */
     bool dedup_ok = true;                 /* ICW_DEDUP=0 disables the mono K1 dedup (A/B) */
     int max_sets = 2;                     /* ICW_SETS: block scratch sets (2..kSets) */
@@ -604,6 +606,17 @@ int icw_create(const icw_config *cfg, const icw_node *nodes, int n_nodes, int n_
         if (ns && atoi(ns) >= 2 && atoi(ns) <= kSets) c->max_sets = atoi(ns);
         const char *dd = getenv("ICW_DEDUP");
         if (dd && !strcmp(dd, "0")) c->dedup_ok = false;
+        const char *kl = getenv("ICW_K1_LDS");
+        c->k1_lds = kl && !strcmp(kl, "1");
+        {
+            hipDeviceProp_t p2;
+            if (hipGetDeviceProperties(&p2, c->device) == hipSuccess) {
+                size_t l = p2.sharedMemPerBlock;
+                if (p2.maxSharedMemoryPerMultiProcessor && p2.maxSharedMemoryPerMultiProcessor < l)
+                    l = p2.maxSharedMemoryPerMultiProcessor;
+                c->lds_cu = (uint32_t)l;
+            }
+        }
         const char *wg = getenv("ICW_K1_WG");
         if (wg && atoi(wg) >= 1 && atoi(wg) <= 4) c->k1_wg = atoi(wg);
     }
@@ -759,9 +772,11 @@ int icw_process_streams(icw_ctx *c, int first, int count, const void *in, size_t
     std::lock_guard<std::mutex> lk(c->mu);
     if (set_dev(c)) return ICW_EDEVICE;
     hipStream_t st = hip_stream ? (hipStream_t)hip_stream : c->stream;
-    /* a NULL handle with device pointers means the legacy default stream (what torch's default
-     * stream is): the call starts after the work already queued there and that stream's later work
-     * waits for the call, although the kernels run on the context's own non-blocking streams */
+    /* A NULL handle with device pointers means the legacy default stream (torch's default stream):
+     * the call starts after the work already queued there, and returns when its results are in
+     * place, so that stream's later work sees them.  The end is a host wait, not an operation on the
+     * null stream: a null-stream wait behind the context's CU-masked streams cost C2 13-25 % (its
+     * implicit synchronisation with every blocking stream serialises the block pipeline). */
     const bool legacy = !hip_stream && (flags & ICW_F_DEVICE_PTRS);
     if (legacy && (hipEventRecord(c->join, nullptr) != hipSuccess || hipStreamWaitEvent(st, c->join, 0) != hipSuccess))
         return ICW_EDEVICE;
@@ -855,7 +870,7 @@ int icw_process_streams(icw_ctx *c, int first, int count, const void *in, size_t
         const int k1_waves = (k1_mode == 0 || k1_mode == ICW_K1_FC) ? ((count + (dedup ? 63 : 31)) / (dedup ? 64 : 32)) * 2
                            : row_waves;
         const int k1_cus = (k1_waves + c->k1_wpc - 1) / c->k1_wpc;
-        if (c->cu_split && k1_cus * 2 <= c->n_cu) {
+        if (c->cu_split && !c->k1_lds && k1_cus * 2 <= c->n_cu) {
             const CuSplit *cs = cu_split(c, k1_cus);
             if (!cs) return ICW_EDEVICE;
             sK = cs->k1;
@@ -887,6 +902,7 @@ int icw_process_streams(icw_ctx *c, int first, int count, const void *in, size_t
         const int t0 = b * Tb, T = std::min(Tb, n_frames - t0), p = b % n_sets;
         IcwK0Args a0;
         memset(&a0, 0, sizeof(a0));
+        a0.lds_guard = c->k1_lds ? 256u : 0u;
         a0.in = d_in + (size_t)t0 * fsz;
         a0.in_stride = dis;
         a0.fmt = cfg.in_format;
@@ -939,7 +955,8 @@ int icw_process_streams(icw_ctx *c, int first, int count, const void *in, size_t
             a1.t0 = t0;
             a1.info_dup = c->info_dup[p];
             memcpy(a1.pc, c->pc, sizeof(a1.pc));
-            a1.wg_waves = c->k1_wg;
+            a1.wg_waves = c->k1_lds ? 4 : c->k1_wg;
+            a1.lds_hold = c->k1_lds ? c->lds_cu : 0;
             a1.dedup = dedup ? 1 : 0;
             a1.fes = fcm ? ds.fes + f0 * 4 * ICW_FES_PITCH : nullptr;
             /* K0(b) done, and K2(b-2), the last reader of w[p] / info_dup[p] */
@@ -1005,6 +1022,7 @@ int icw_process_streams(icw_ctx *c, int first, int count, const void *in, size_t
         if (table) {
             IcwTrigArgs at;
             memset(&at, 0, sizeof(at));
+            at.lds_guard = c->k1_lds ? 256u : 0u;
             at.prog = c->d_prog;
             at.n_frame = a2.n_frame;
             at.t0 = t0;
@@ -1031,6 +1049,7 @@ int icw_process_streams(icw_ctx *c, int first, int count, const void *in, size_t
         if (bus) {
             IcwK4Args a4;
             memset(&a4, 0, sizeof(a4));
+            a4.lds_guard = c->k1_lds ? 256u : 0u;
             a4.iq = c->iq[p];
             a4.n_streams = count;
             a4.T = T;
@@ -1090,6 +1109,7 @@ int icw_process_streams(icw_ctx *c, int first, int count, const void *in, size_t
     {
         IcwAdvArgs av;
         memset(&av, 0, sizeof(av));
+        av.lds_guard = c->k1_lds ? 256u : 0u;
         av.n_streams = count;
         av.cw = cw ? 1 : 0;
         av.n = n_frames;
@@ -1100,8 +1120,7 @@ int icw_process_streams(icw_ctx *c, int first, int count, const void *in, size_t
         av.scaled = cfg.frmod_scaled;
         if (icw_launch_advance(&av, st) != hipSuccess) return ICW_EDEVICE;
     }
-    if (legacy && (hipEventRecord(c->join, st) != hipSuccess || hipStreamWaitEvent(nullptr, c->join, 0) != hipSuccess))
-        return ICW_EDEVICE;
+    if (legacy && hipStreamSynchronize(st) != hipSuccess) return ICW_EDEVICE;
     if (!dev) {
         if (hipMemcpy2DAsync(out, out_stride, d_out, dos, dos, S, hipMemcpyDeviceToHost, st) != hipSuccess)
             return ICW_EDEVICE;

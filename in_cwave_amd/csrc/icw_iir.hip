@@ -559,6 +559,15 @@ __global__ __launch_bounds__(256) void icw_iir_row(IcwK1Args a)
 }
 
 /* ---------------------------------------------------------------- launch wrappers ------- */
+/* dynamic LDS that makes a workgroup of kernel f hold a.lds_hold bytes in all */
+static size_t k1_dyn_lds(const void *f, const IcwK1Args &a)
+{
+    if (!a.lds_hold) return 0;
+    hipFuncAttributes fa;
+    if (hipFuncGetAttributes(&fa, f) != hipSuccess) return 0;
+    return a.lds_hold > fa.sharedSizeBytes ? a.lds_hold - fa.sharedSizeBytes : 0;
+}
+
 template <int N, bool K, bool S>
 static hipError_t launch_k1_t(const IcwK1Args &a, hipStream_t st)
 {
@@ -567,7 +576,8 @@ static hipError_t launch_k1_t(const IcwK1Args &a, hipStream_t st)
     const long lanes = (long)((a.n_streams + spg - 1) / spg) * 128;
     const int tpb = 64 * a.wg_waves;
     const int blocks = (int)((lanes + tpb - 1) / tpb);
-    hipLaunchKernelGGL((icw_iir_state<N, K, S>), dim3(blocks), dim3(tpb), 0, st, a);
+    hipLaunchKernelGGL((icw_iir_state<N, K, S>), dim3(blocks), dim3(tpb),
+                       k1_dyn_lds((const void *)icw_iir_state<N, K, S>, a), st, a);
     return hipGetLastError();
 }
 
@@ -593,7 +603,7 @@ static hipError_t launch_k1r_t(const IcwK1Args &a, hipStream_t st)
     const long lanes = ((slots + 3) / 4) * 2 * 64;
     const int tpb = 64 * a.wg_waves;
     const int blocks = (int)((lanes + tpb - 1) / tpb);
-    hipLaunchKernelGGL((icw_iir_row<N>), dim3(blocks), dim3(tpb), 0, st, a);
+    hipLaunchKernelGGL((icw_iir_row<N>), dim3(blocks), dim3(tpb), k1_dyn_lds((const void *)icw_iir_row<N>, a), st, a);
     return hipGetLastError();
 }
 

@@ -1358,7 +1358,7 @@ __global__ __launch_bounds__(64) void icw_render_fc(IcwK3Args a)
 extern "C" hipError_t icw_launch_unpack(const IcwK0Args *a, hipStream_t st)
 {
     dim3 grid((a->T + 255) / 256, a->n_streams);
-    hipLaunchKernelGGL(icw_unpack_frames, grid, dim3(256), 0, st, *a);
+    hipLaunchKernelGGL(icw_unpack_frames, grid, dim3(256), a->lds_guard, st, *a);
     return hipGetLastError();
 }
 
@@ -1441,18 +1441,18 @@ extern "C" hipError_t icw_launch_output(const IcwK2Args *a, int nord, int kahan,
 
 extern "C" hipError_t icw_launch_trig_table(const IcwTrigArgs *a, hipStream_t st)
 {
-    hipLaunchKernelGGL(icw_trig_table, dim3((a->T + 255) / 256), dim3(256), 0, st, *a);
+    hipLaunchKernelGGL(icw_trig_table, dim3((a->T + 255) / 256), dim3(256), a->lds_guard, st, *a);
     return hipGetLastError();
 }
 
 extern "C" hipError_t icw_launch_graph_serial(const IcwK4Args *a, hipStream_t st)
 {
-    hipLaunchKernelGGL(icw_graph_serial, dim3((a->n_streams + 63) / 64), dim3(64), 0, st, *a);
+    hipLaunchKernelGGL(icw_graph_serial, dim3((a->n_streams + 63) / 64), dim3(64), a->lds_guard, st, *a);
     return hipGetLastError();
 }
 
 extern "C" hipError_t icw_launch_advance(const IcwAdvArgs *a, hipStream_t st)
 {
-    hipLaunchKernelGGL(icw_advance, dim3((a->n_streams + 63) / 64), dim3(64), 0, st, *a);
+    hipLaunchKernelGGL(icw_advance, dim3((a->n_streams + 63) / 64), dim3(64), a->lds_guard, st, *a);
     return hipGetLastError();
 }

@@ -34,7 +34,11 @@ def load():
             pass
         lib = C.CDLL(str(LIB_PATH))
         for name, (res, args) in abi.SIGNATURES.items():
-            fn = getattr(lib, name)
+            fn = getattr(lib, name, None)
+            if fn is None:
+                if os.environ.get("ICW_LIB"):      # an older A/B build may lack newer entry points
+                    continue
+                raise IcwError(f"{LIB_PATH} does not export {name}")
             fn.restype = res
             fn.argtypes = args
         _lib = lib
@@ -102,14 +106,17 @@ class Context:
         _check(self._lib.icw_stream_open(self.h, s, n_samples, fade_in_ms, fade_out_ms, sec_align,
                                          clr_nframe, clr_hilb), "icw_stream_open")
 
-    def process(self, inp, n_frames, first=0, count=None, want_pre=False):
+    def process(self, inp, n_frames, first=0, count=None, want_pre=False, out=None):
         """Host numpy path: inp uint8 [count, >= n_frames*fsz]; returns (out uint8 [count, n_frames*2*rs],
-        pre float64 [count, n_frames, 2] or None)."""
+        pre float64 [count, n_frames, 2] or None).  out: a preallocated output array (reused)."""
         count = self.n_streams - first if count is None else count
         inp = np.ascontiguousarray(inp)
         assert inp.dtype == np.uint8 and inp.shape[0] == count and inp.shape[1] >= n_frames * self.fsz
         osz = 2 * self.render_size
-        out = np.zeros((count, n_frames * osz), dtype=np.uint8)
+        if out is None:
+            out = np.zeros((count, n_frames * osz), dtype=np.uint8)
+        assert out.dtype == np.uint8 and out.flags.c_contiguous and out.shape[0] == count
+        assert out.shape[1] >= n_frames * osz
         pre = np.zeros((count, n_frames, 2), dtype=np.float64) if want_pre else None
         flags = abi.F_DEBUG_PRE if want_pre else 0
         # a length-1 leading axis may carry stride 0 (x[None, :]): the row length is the stride then
@@ -264,6 +271,77 @@ def transcode_files(cfg, nodes, in_paths, out_paths, fade_in_ms=0, fade_out_ms=0
     status = (C.c_int * max(1, n))()
     rc = load().icw_transcode_files(C.byref(cfg), arr, len(nodes), ins, outs, n, C.byref(o), C.byref(st), status)
     return rc, st, [status[i] for i in range(n)]
+
+
+def transcode_files_devices(cfg, nodes, in_paths, out_paths, devices, fade_in_ms=0, fade_out_ms=0, sec_align=0,
+                            block_frames=0):
+    """icw_transcode_files_devices: the files split over `devices` (one host thread each)"""
+    n = len(in_paths)
+    ins = (C.c_char_p * max(1, n))(*[str(p).encode() for p in in_paths])
+    outs = (C.c_char_p * max(1, n))(*[str(p).encode() for p in out_paths])
+    arr = graph_nodes(nodes)
+    o = abi.BatchOpts(fade_in_ms, fade_out_ms, sec_align, block_frames, -1, 0)
+    dv = (C.c_int * len(devices))(*devices)
+    st = abi.BatchStats()
+    status = (C.c_int * max(1, n))()
+    rc = load().icw_transcode_files_devices(C.byref(cfg), arr, len(nodes), ins, outs, n, C.byref(o), dv,
+                                            len(devices), C.byref(st), status)
+    return rc, st, [status[i] for i in range(n)]
+
+
+class Group:
+    """icw_group: n_streams streams sharded over several devices, one context and one host
+    thread per device (include/icw_group.h)"""
+
+    def __init__(self, cfg, nodes, n_streams, devices):
+        lib = load()
+        self._lib = lib
+        arr = graph_nodes(nodes)
+        dv = (C.c_int * len(devices))(*devices)
+        h = C.c_void_p()
+        acc = C.c_int()
+        _check(lib.icw_group_create(C.byref(cfg), arr, len(nodes), n_streams, dv, len(devices), C.byref(h),
+                                    C.byref(acc)), "icw_group_create")
+        self.h, self.accepted, self.n_streams = h, bool(acc.value), n_streams
+        self.fsz = abi.FMT_BYTES[cfg.in_format] * cfg.in_channels
+        self.osz = 2 * (3 if cfg.need24bits else 2)
+
+    def close(self):
+        if self.h:
+            self._lib.icw_group_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def shard(self, d):
+        f, c, dev, ctx = C.c_int(), C.c_int(), C.c_int(), C.c_void_p()
+        _check(self._lib.icw_group_shard(self.h, d, C.byref(f), C.byref(c), C.byref(dev), C.byref(ctx)),
+               "icw_group_shard")
+        return f.value, c.value, dev.value
+
+    def process(self, inp, n_frames, want_pre=False):
+        inp = np.ascontiguousarray(inp)
+        assert inp.dtype == np.uint8 and inp.shape[0] == self.n_streams and inp.shape[1] >= n_frames * self.fsz
+        out = np.zeros((self.n_streams, n_frames * self.osz), dtype=np.uint8)
+        pre = np.zeros((self.n_streams, n_frames, 2), dtype=np.float64) if want_pre else None
+        _check(self._lib.icw_group_process(self.h, _ptr(inp), inp.strides[0], _ptr(out), out.strides[0], n_frames,
+                                           abi.F_DEBUG_PRE if want_pre else 0, _ptr(pre)), "icw_group_process")
+        return out, pre
+
+    def meters(self, s, reset=False):
+        m = abi.Meters()
+        _check(self._lib.icw_group_get_meters(self.h, s, 1 if reset else 0, C.byref(m)), "icw_group_get_meters")
+        return {"clips": (m.clips[0], m.clips[1]), "peak_db": (m.peak_db[0], m.peak_db[1]),
+                "desubnorm": m.desubnorm}
+
+    def n_frame(self, s):
+        v = C.c_uint64()
+        _check(self._lib.icw_group_n_frame(self.h, s, C.byref(v)), "icw_group_n_frame")
+        return v.value
 
 
 def graph_nodes(nodes):

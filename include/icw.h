@@ -186,9 +186,10 @@ int icw_set_input(icw_ctx *ctx, uint32_t sample_rate, uint32_t fmt, uint32_t cha
  *   dbg : ICW_F_DEBUG_PRE only -- double[n_streams][n_frames][2] pre-render values (lOut,rOut).
  * Host pointers are staged through pinned buffers; with ICW_F_DEVICE_PTRS nothing crosses
  * PCIe.  hip_stream: the hipStream_t the call is ordered on (it starts after the work queued there,
- * and the stream's later work sees its results).  NULL: with host pointers the context's own
- * stream (the call returns when its output is in `out`); with ICW_F_DEVICE_PTRS the legacy default
- * stream (stream 0, torch's default stream) -- the call returns before the kernels finish.
+ * and the stream's later work sees its results; the call returns before the kernels finish).
+ * NULL: with host pointers the context's own stream (the call returns when its output is in
+ * `out`); with ICW_F_DEVICE_PTRS the legacy default stream (stream 0, torch's default stream): the
+ * call starts after the work queued there and returns when its output is in place.
  * icw_get_meters / icw_n_frame / icw_get_state wait for the context's work.  Returns ICW_OK. */
 int icw_process_batch(icw_ctx *ctx, const void *in, size_t in_stride_bytes, void *out,
                       size_t out_stride_bytes, int n_frames, unsigned flags, void *dbg,

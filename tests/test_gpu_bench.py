@@ -22,7 +22,8 @@ def _line(out):
 
 def test_bench_single_rank_line():
     r = subprocess.run([sys.executable, "bench.py", "--steps", "1", "--warmup", "1", "--frames", "65536",
-                        "--no-cpu-baseline"], cwd=ROOT, capture_output=True, text=True, timeout=300)
+                        "--no-cpu-baseline", "--e2e-steps", "0"], cwd=ROOT, capture_output=True, text=True,
+                       timeout=300)
     assert r.returncode == 0, r.stderr[-2000:]
     d = _line(r.stdout)
     assert d["n_gpus"] == 1 and d["unit"] == "Msamples/s" and d["higher_is_better"] is True
@@ -36,13 +37,42 @@ def test_bench_two_ranks_rehearsal():
     s.bind(("127.0.0.1", 0))
     port = s.getsockname()[1]
     s.close()
-    env = dict(os.environ, ICW_BENCH_BACKEND="gloo")
+    env = dict(os.environ)
     r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
                         "--master-addr", "127.0.0.1", "--master-port", str(port), "bench.py", "--gpus", "2",
-                        "--steps", "1", "--warmup", "1", "--frames", "32768", "--streams", "64"],
+                        "--steps", "1", "--warmup", "1", "--frames", "32768", "--streams", "64", "--e2e-steps", "0"],
                        cwd=ROOT, capture_output=True, text=True, timeout=300, env=env)
     assert r.returncode == 0, r.stderr[-3000:]
     d = _line(r.stdout)
     assert d["n_gpus"] == 2 and d["cpu_baseline"] is None
     # whole-job value: both ranks' streams over the max-over-ranks time
     assert abs(d["value"] - 2.0 * 2 * 64 * 32768 / (d["ms_per_step"] / 1e3) / 1e6) < 1e-6 * d["value"]
+
+
+def test_bench_gpus_flag_self_launches():
+    """python bench.py --gpus 2 with no launcher: two rank processes sharing the box's GPU (gloo),
+    n_gpus 2 in the one line rank 0 prints, whole-job value"""
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", "2", "--steps", "1", "--warmup", "1",
+                        "--frames", "32768", "--streams", "64", "--e2e-steps", "0"],
+                       cwd=ROOT, capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = _line(r.stdout)
+    assert d["n_gpus"] == 2 and d["cpu_baseline"] is None
+    assert abs(d["value"] - 2.0 * 2 * 64 * 32768 / (d["ms_per_step"] / 1e3) / 1e6) < 1e-6 * d["value"]
+
+
+def test_bench_line_fields():
+    """the roofline is FP64-bound with HBM and issue-floor fields, the e2e host-buffer rate is
+    reported beside `value`"""
+    r = subprocess.run([sys.executable, "bench.py", "--steps", "1", "--warmup", "1", "--frames", "65536",
+                        "--no-cpu-baseline", "--e2e-steps", "1"], cwd=ROOT, capture_output=True, text=True,
+                       timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    d = _line(r.stdout)
+    rf = d["roofline"]
+    assert rf["bound"] == "fp64" and rf["unit"] == "TFLOP/s" and 0 < rf["frac"] < 1
+    assert abs(rf["achieved"] - rf["flops_per_frame"] * rf["frames_per_launch"] / rf["avg_launch_ms"] / 1e9) \
+        < 1e-9 * rf["achieved"]
+    assert rf["hbm"]["unit"] == "GB/s" and rf["issue_bound"]["frac"] > 0
+    assert d["e2e_host_buffers"]["value"] > 0

@@ -1,0 +1,65 @@
+"""GPU: one host process driving several device shards (include/icw_group.h) -- contiguous stream
+ranges, one context and one host thread per shard.  On the one-GPU box every shard maps to device 0;
+the 8-GPU node runs the same code with devices 0..7.  Results must be byte-identical to one
+context over all streams and equal the oracle."""
+import numpy as np
+import pytest
+
+from in_cwave_amd import abi, graph, synth
+from in_cwave_amd import lib as L
+
+from test_gpu_transcode import make_inputs
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("shape", ["c4", "c5"])
+def test_group_equals_one_context_and_oracle(oracle, icw, shape):
+    if shape == "c4":
+        fs, fmt = 48000, abi.FMT_I16
+        cfg = graph.default_config(fs)
+        nodes = graph.graph_pm_shift_mix()
+    else:
+        fs, fmt = 192000, abi.FMT_F32
+        cfg = graph.default_config(fs, fmt=fmt, need24bits=True)
+        cfg.render.render_type = abi.RENDER_TPDF
+        cfg.render.nshape_type = abi.NSHAPE_MEW44
+        nodes = graph.graph_master_only()
+    S, n = 7, 2500
+    raw = synth.batch_pcm(S, n, fs, fmt=fmt)
+    grp = L.Group(cfg, nodes, S, [0, 0, 0])
+    assert [grp.shard(d)[:2] for d in range(3)] == [(0, 3), (3, 2), (5, 2)]
+    out, pre = grp.process(raw, n, want_pre=True)
+    ctx = icw.Context(cfg, nodes, S)
+    out1, pre1 = ctx.process(raw, n, want_pre=True)
+    assert np.array_equal(out, out1)
+    assert np.array_equal(pre.view(np.uint64), pre1.view(np.uint64))
+    for s in range(S):
+        st = oracle.Stream(cfg, nodes)
+        ro, rp = st.process(raw[s], n, want_pre=True)
+        assert np.array_equal(out[s], ro), s
+        assert np.array_equal(pre[s].view(np.uint64), rp.view(np.uint64)), s
+        assert grp.meters(s) == ctx.meters(s) and grp.meters(s)["clips"] == st.meters()["clips"]
+        assert grp.n_frame(s) == ctx.n_frame(s) == st.n_frame()
+    grp.close()
+    ctx.close()
+
+
+def test_transcode_files_devices_byte_identical(tmp_path):
+    """the many-file transcoder split over two 'devices' (both device 0) writes the same files as
+    one device"""
+    files = make_inputs(tmp_path)
+    cfg = graph.default_config(48000)
+    cfg.render.render_type = abi.RENDER_TPDF
+    nodes = graph.graph_shift_master()
+    ins = [f[0] for f in files]
+    one = [tmp_path / f"one_{i}.wav" for i in range(len(ins))]
+    two = [tmp_path / f"two_{i}.wav" for i in range(len(ins))]
+    rc1, st1, s1 = L.transcode_files(cfg, nodes, ins, one, fade_in_ms=30, fade_out_ms=30, sec_align=1,
+                                     block_frames=16384)
+    rc2, st2, s2 = L.transcode_files_devices(cfg, nodes, ins, two, [0, 0], fade_in_ms=30, fade_out_ms=30,
+                                             sec_align=1, block_frames=16384)
+    assert rc1 == rc2 == abi.OK and s1 == s2 == [abi.OK] * len(ins)
+    assert st2.n_files == st1.n_files == len(ins) and st2.frames_out == st1.frames_out
+    for a, b in zip(one, two):
+        assert a.read_bytes() == b.read_bytes(), a.name
