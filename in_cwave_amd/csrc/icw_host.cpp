@@ -107,6 +107,7 @@ struct icw_ctx {
     int k1_wpc = 4;                       /* ICW_K1_WPC: K1 waves per CU (one per SIMD) */
     int k1_wg = 1;                        /* ICW_K1_WG: K1 waves per workgroup */
     bool k1_lds = false;                  /* ICW_K1_LDS=1: K1 workgroups hold the CU's LDS (A/B) */
+    bool fill_drain = true;               /* ICW_FILL_DRAIN=0: first K0 / last K2 stay partitioned (A/B) */
     uint32_t lds_cu = 0;                  /* LDS bytes per CU a workgroup may hold */
     int max_block = kDefBlockFrames;      /* ICW_BLOCK: frames per launch block */
     bool dedup_ok = true;                 /* ICW_DEDUP=0 disables the mono K1 dedup (A/B) */
@@ -606,6 +607,8 @@ int icw_create(const icw_config *cfg, const icw_node *nodes, int n_nodes, int n_
         if (ns && atoi(ns) >= 2 && atoi(ns) <= kSets) c->max_sets = atoi(ns);
         const char *dd = getenv("ICW_DEDUP");
         if (dd && !strcmp(dd, "0")) c->dedup_ok = false;
+        const char *fd = getenv("ICW_FILL_DRAIN");
+        if (fd && !strcmp(fd, "0")) c->fill_drain = false;
         const char *kl = getenv("ICW_K1_LDS");
         c->k1_lds = kl && !strcmp(kl, "1");
         {
@@ -863,6 +866,10 @@ int icw_process_streams(icw_ctx *c, int first, int count, const void *in, size_t
      * K1 needs few CUs (4 waves per CU, one per SIMD) sK is confined to those CUs and sA / sD to
      * the rest, so the frame-parallel kernels never share a SIMD with a recurrence. */
     hipStream_t sK = st, sA = c->stream2, sD = c->stream3, sR = c->stream4;
+    /* sF: an unmasked stream for the pipeline's fill and drain under the CU partition -- K0 of the
+     * first block and K2 of the last run while no recurrence does, so they get the whole chip
+     * instead of the partition's share (C3 / C4: the drain was one partitioned K2, ~5 % of a step) */
+    hipStream_t sF = nullptr;
     if (c->serialize) {
         sA = sD = sR = st;
     } else if (!cw) {
@@ -877,13 +884,14 @@ int icw_process_streams(icw_ctx *c, int first, int count, const void *in, size_t
             sA = cs->rest;
             sD = cs->dith;
             sR = cs->render;
+            if (c->fill_drain) sF = c->stream2;
         }
     }
     /* every stream starts after everything already queued on st (inputs, previous calls) */
     if (hipEventRecord(c->join, st) != hipSuccess)
         return ICW_EDEVICE;
-    for (hipStream_t x : {sK, sA, sD, sR})
-        if (x != st && hipStreamWaitEvent(x, c->join, 0) != hipSuccess) return ICW_EDEVICE;
+    for (hipStream_t x : {sK, sA, sD, sR, sF})
+        if (x && x != st && hipStreamWaitEvent(x, c->join, 0) != hipSuccess) return ICW_EDEVICE;
 
     DevState &ds = c->st;
     const size_t f0 = (size_t)first;
@@ -919,8 +927,9 @@ int icw_process_streams(icw_ctx *c, int first, int count, const void *in, size_t
         a0.x_pitch = x_pitch;
         a0.dedup = dedup ? 1 : 0;
         if (b >= n_sets && !cw && sK != sA && hipStreamWaitEvent(sA, c->k1done[p], 0) != hipSuccess) return ICW_EDEVICE;
-        if (icw_launch_unpack(&a0, sA) != hipSuccess) return ICW_EDEVICE;
-        if (hipEventRecord(c->k0done[p], sA) != hipSuccess) return ICW_EDEVICE;
+        hipStream_t s0 = (b == 0 && sF) ? sF : sA;         /* the fill: nothing else runs yet */
+        if (icw_launch_unpack(&a0, s0) != hipSuccess) return ICW_EDEVICE;
+        if (hipEventRecord(c->k0done[p], s0) != hipSuccess) return ICW_EDEVICE;
         return ICW_OK;
     };
 
@@ -978,6 +987,13 @@ int icw_process_streams(icw_ctx *c, int first, int count, const void *in, size_t
             hipEventRecord(c->ev[4 * b + 1], sA);
         }
 
+        /* the drain: K2 of the last block on the unmasked stream, after K1 of the block and K2 of
+         * the one before it (the rotation table and the block order of the meters' owners) */
+        const bool drain = sF && b == n_blocks - 1;
+        hipStream_t s2 = drain ? sF : sA;
+        if (drain && (hipStreamWaitEvent(sF, c->k1done[p], 0) != hipSuccess ||
+                      (b >= 1 && hipStreamWaitEvent(sF, c->k2done[(b - 1) % n_sets], 0) != hipSuccess)))
+            return ICW_EDEVICE;
         IcwK2Args a2;
         memset(&a2, 0, sizeof(a2));
         a2.w = c->w[p];
@@ -1033,19 +1049,19 @@ int icw_process_streams(icw_ctx *c, int first, int count, const void *in, size_t
             at.sample_rate = cfg.sample_rate;
             at.tab = c->trig;
             /* same stream as K2: the previous block's K2 has read the table before it is rewritten */
-            if (icw_launch_trig_table(&at, sA) != hipSuccess) return ICW_EDEVICE;
+            if (icw_launch_trig_table(&at, s2) != hipSuccess) return ICW_EDEVICE;
             a2.trig_tab = c->trig;
             a2.trig_pitch = at.trig_pitch;
         }
         /* rpre[p] / iq[p] were last read by the serial render of block b - n_sets (on sR) */
-        if (c->serial_render && b >= n_sets && sR != sA && hipStreamWaitEvent(sA, c->k3done[p], 0) != hipSuccess)
+        if (c->serial_render && b >= n_sets && sR != s2 && hipStreamWaitEvent(s2, c->k3done[p], 0) != hipSuccess)
             return ICW_EDEVICE;
-        if (timing) hipEventRecord(c->ev[4 * b + 2], sA);
-        if (icw_launch_output(&a2, N, cfg.iir_kahan, sA) != hipSuccess) return ICW_EDEVICE;
-        if (hipEventRecord(c->k2done[p], sA) != hipSuccess) return ICW_EDEVICE;
+        if (timing) hipEventRecord(c->ev[4 * b + 2], s2);
+        if (icw_launch_output(&a2, N, cfg.iir_kahan, s2) != hipSuccess) return ICW_EDEVICE;
+        if (hipEventRecord(c->k2done[p], s2) != hipSuccess) return ICW_EDEVICE;
         /* the serial part (K4, K3b) on sR after K2(b): it then overlaps K2(b+1) instead of
          * delaying it on sA */
-        if (c->serial_render && sR != sA && hipStreamWaitEvent(sR, c->k2done[p], 0) != hipSuccess) return ICW_EDEVICE;
+        if (c->serial_render && sR != s2 && hipStreamWaitEvent(sR, c->k2done[p], 0) != hipSuccess) return ICW_EDEVICE;
         if (bus) {
             IcwK4Args a4;
             memset(&a4, 0, sizeof(a4));
@@ -1095,7 +1111,7 @@ int icw_process_streams(icw_ctx *c, int first, int count, const void *in, size_t
             if (icw_launch_render(&a3, sR) != hipSuccess) return ICW_EDEVICE;
             if (hipEventRecord(c->k3done[p], sR) != hipSuccess) return ICW_EDEVICE;
         }
-        if (timing) hipEventRecord(c->ev[4 * b + 3], c->serial_render ? sR : sA);
+        if (timing) hipEventRecord(c->ev[4 * b + 3], c->serial_render ? sR : s2);
         /* complex input: K0(b + n_sets) reuses xd[p], which K2(b) read */
         if (cw && b + n_sets < n_blocks && (rc0 = launch_k0(b + n_sets)) != ICW_OK) return rc0;
     }
@@ -1103,8 +1119,8 @@ int icw_process_streams(icw_ctx *c, int first, int count, const void *in, size_t
         for (int i = 0; i < count; ++i) c->lr_known[first + i] = 0;   /* stereo: the halves diverge */
     /* join: the caller's stream continues after every kernel of the call, then the call-start
      * position / phases / frame counters advance (icw_advance) */
-    for (hipStream_t x : {sK, sA, sD, sR})
-        if (x != st && (hipEventRecord(c->join, x) != hipSuccess || hipStreamWaitEvent(st, c->join, 0) != hipSuccess))
+    for (hipStream_t x : {sK, sA, sD, sR, sF})
+        if (x && x != st && (hipEventRecord(c->join, x) != hipSuccess || hipStreamWaitEvent(st, c->join, 0) != hipSuccess))
             return ICW_EDEVICE;
     {
         IcwAdvArgs av;
