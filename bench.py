@@ -12,7 +12,7 @@ Metric: rendered output channel-samples per second (2 x frames/s), whole job ove
 Multi-GPU: one process per GPU, streams sharded (weak scaling, no collective on the data path);
 barrier + synchronize around the K timed steps, max elapsed over ranks.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c2|c3|c4|c5]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c1|c2|c3|c4|c5]
 
 --gpus N without a launcher (RANK unset) starts N rank processes itself, before anything here
 touches the GPU, and exits with the worst rank's status; under torch.distributed.run the world
@@ -21,6 +21,10 @@ and use gloo for the barrier and the timing reduce (RCCL needs a GPU per rank).
 
 --workload picks one of the BASELINE.json configs; the default, c2, is the one the
 headline metric is quoted on.  The others are measured for DESIGN.md, not for the bench line.
+c1 is the single-stream drop-in: the C host examples/icw_transcode (no Python in its loop) decodes
+a 30 s 44.1 kHz stereo track through icw_amod_process_samples in 576-frame blocks from host
+memory, timing every call; its CPU baseline is the oracle on the same track on one core, and the
+two outputs are compared byte for byte.
 
 Roofline: the dominant kernel is the serial IIR recurrence K1; its bound is FP64
 VALU issue, so `roofline` reports its algorithmic FP64 rate (the loop-back Kahan sum,
@@ -64,6 +68,9 @@ def _latest(pattern):
 # SURVEY 8(d) configurations, per GPU: streams, frames per stream per step, fs, input format,
 # channels, DSP list, render, algorithmic bytes per frame (input + output)
 WORKLOADS = {
+    "c1": dict(streams=1, frames=1323000, fs=44100, fmt="i16", ch=2, graph="shift_master", render="round16",
+               bytes=8, desc="C1: 1 x 44.1kHz int16 stereo stream, 30 s, drop-in boundary in 576-frame blocks "
+                             "(host buffers), Type-1 Kahan Hilbert + Shift(+2/-2 Hz) + Master, 16-bit ROUND"),
     "c2": dict(streams=256, frames=1 << 20, fs=48000, fmt="i16", ch=2, graph="shift_master", render="round16",
                bytes=8, desc="C2: 256 x 48kHz int16 stereo streams/GPU, Type-1 (order 19) Kahan quadrature "
                              "Hilbert + Shift(+2/-2 Hz) + Master, 16-bit ROUND"),
@@ -101,6 +108,7 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-workers", type=int, default=0, help="0: one per physical core available here")
     ap.add_argument("--cpu-frames", type=int, default=1 << 25)
+    ap.add_argument("--block", type=int, default=576, help="c1: frames per boundary call (NS_PERTIME)")
     ap.add_argument("--e2e-steps", type=int, default=2,
                     help="extra steps with host buffers (H2D + D2H included), reported beside `value`")
     return ap.parse_args()
@@ -218,9 +226,87 @@ def cpu_baseline(workers, n_frames, wname):
                       f"the reference's own IIR/graph/render need <windows.h> and are not built here"}
 
 
+# ----------------------------------------------------------------------------- C1 leg -------
+def _wav_i16(path, raw, rate, ch):
+    import struct
+    data = raw.tobytes()
+    fmt = struct.pack("<HHIIHH", 1, ch, rate, rate * 2 * ch, 2 * ch, 16)
+    body = b"WAVE" + b"fmt " + struct.pack("<I", len(fmt)) + fmt + b"data" + struct.pack("<I", len(data)) + data
+    Path(path).write_bytes(b"RIFF" + struct.pack("<I", len(body)) + body)
+
+
+def bench_c1(a):
+    """single-stream drop-in: K runs of the C host over the track, W untimed"""
+    import tempfile
+    from in_cwave_amd import synth
+    W = WORKLOADS["c1"]
+    exe = ROOT / "examples" / "icw_transcode"
+    if not exe.exists():
+        raise SystemExit("bench.py c1: examples/icw_transcode is not built (make -C examples)")
+    raw = synth.stream_pcm(0, W["frames"], W["fs"])
+    tmp = Path(tempfile.mkdtemp(prefix="icw_c1_"))
+    src, dst = tmp / "c1.wav", tmp / "c1_out.wav"
+    _wav_i16(src, raw, W["fs"], 2)
+    env = dict(os.environ, ICW_TIMING="1")
+    runs = []
+    for i in range(a.warmup + a.steps):
+        r = subprocess.run([str(exe), str(src), str(dst), str(a.block), "shift", "16"], env=env,
+                           capture_output=True, text=True, timeout=600)
+        if r.returncode != 0:
+            raise SystemExit(f"icw_transcode failed ({r.returncode}): {r.stderr[-500:]}")
+        if i >= a.warmup:
+            runs.append(json.loads(r.stdout.strip().splitlines()[-1]))
+    out = np.frombuffer(dst.read_bytes()[44:], dtype=np.uint8)
+    decode_s = sum(x["decode_s"] for x in runs)
+    value = 2.0 * W["frames"] * len(runs) / decode_s / 1e6
+    cpu = parity = None
+    if not a.no_cpu_baseline:
+        from oracle import oracle as O
+        n_avail, cpus, model, topo = host_cores()
+        try:
+            os.sched_setaffinity(0, {cpus[0]})
+        except OSError:
+            pass
+        cfg, nodes, _ = workload_config(W)
+        st = O.Stream(cfg, nodes)
+        st.open(W["frames"])
+        outs = []
+        t0 = time.perf_counter()
+        for f0 in range(0, W["frames"], a.block):
+            n = min(a.block, W["frames"] - f0)
+            outs.append(st.process(raw[f0 * 4:(f0 + n) * 4], n)[0])
+        dt = time.perf_counter() - t0
+        ref = np.concatenate(outs)
+        parity = "bit-exact" if np.array_equal(ref, out) else "MISMATCH"
+        cpu = {"value": 2.0 * W["frames"] / dt / 1e6, "unit": "Msamples/s", "cores": 1, "kind": "port",
+               "cpu_model": model, "sample": f"the same 30 s track, oracle C restatement in {a.block}-frame "
+                                              f"blocks on one pinned core, {dt:.2f}s"}
+    last = runs[-1]
+    line = {
+        "metric": "Msamples/s through Hilbert+mod+render", "value": value, "unit": "Msamples/s", "n_gpus": 1,
+        "steps": len(runs), "warmup": a.warmup, "ms_per_step": decode_s * 1e3 / len(runs),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
+        "config": {"workload": W["desc"], "streams_per_gpu": 1, "frames_per_stream_per_step": W["frames"],
+                   "fs": W["fs"], "block_frames": a.block, "parallelism": "single stream"},
+        "block_latency_us": last["block_us"], "realtime_x": last["realtime_x"], "parity_vs_oracle": parity,
+        "cpu_baseline": cpu,
+        "note": "host pointers through the drop-in boundary: each call stages its block H2D, runs K0-K2 "
+                "and copies D2H before returning, as the DecodeThread needs; ms_per_step = time inside "
+                "the boundary calls (file I/O excluded)",
+    }
+    for f in (src, dst):
+        f.unlink()
+    tmp.rmdir()
+    print(json.dumps(line), flush=True)
+
+
 # ----------------------------------------------------------------------------- GPU leg ------
 def main():
     a = parse()
+    if a.workload == "c1":
+        if a.gpus != 1:
+            raise SystemExit("bench.py c1 is the single-stream drop-in: --gpus 1")
+        return bench_c1(a)
     if "RANK" not in os.environ and a.gpus > 1:
         sys.exit(launch_ranks(a.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))

@@ -5,13 +5,20 @@
  *
  *   icw_transcode in.wav out.wav [block_frames=576] [graph: master|shift|pmmix] [bits: 16|24]
  *
+ * With ICW_TIMING=1 in the environment it times every boundary call (host buffers in and out,
+ * the call returns when the block's bytes are in `out`, as the DecodeThread needs them) and prints
+ * one JSON line on stdout: decode throughput and the per-block latency distribution (C1 of
+ * SURVEY 8(d)).  File I/O is outside the timed calls.
+ *
  * The WAV reader handles PCM u8/16/24/32 and IEEE float32 (the RWAVE formats of
  * xwave_reader.c:205-239); the output is stereo 16- or 24-bit PCM like the plugin's.
  */
+#define _POSIX_C_SOURCE 199309L
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <time.h>
 
 #include "../include/icw_amod.h"
 
@@ -19,6 +26,19 @@ static uint32_t rd32(const unsigned char *p) { return p[0] | (p[1] << 8) | (p[2]
 static uint16_t rd16(const unsigned char *p) { return (uint16_t)(p[0] | (p[1] << 8)); }
 static void wr32(unsigned char *p, uint32_t v) { p[0] = v; p[1] = v >> 8; p[2] = v >> 16; p[3] = v >> 24; }
 static void wr16(unsigned char *p, uint16_t v) { p[0] = v; p[1] = v >> 8; }
+
+static double now_s(void)
+{
+    struct timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    return (double)ts.tv_sec + 1e-9 * (double)ts.tv_nsec;
+}
+
+static int cmp_d(const void *a, const void *b)
+{
+    double x = *(const double *)a, y = *(const double *)b;
+    return (x > y) - (x < y);
+}
 
 static void node_defaults(icw_node *n, int mode)
 {
@@ -138,11 +158,23 @@ int main(int argc, char **argv)
 
     unsigned char *in = (unsigned char *)malloc((size_t)block * fsz);
     char *out = (char *)malloc((size_t)block * osz);
+    const char *te = getenv("ICW_TIMING");
+    const int timing = te && te[0] == '1';
+    const int64_t n_blocks = (n_frames + block - 1) / block;
+    double *lat = timing ? (double *)malloc(sizeof(double) * (size_t)(n_blocks > 0 ? n_blocks : 1)) : NULL;
+    int64_t nb = 0;
+    double busy = 0.0;
     int64_t done = 0;
     while (done < n_frames) {                          /* the DecodeThread loop */
         unsigned n = (unsigned)((n_frames - done) < block ? (n_frames - done) : block);
         if (fread(in, fsz, n, f) != n) { fprintf(stderr, "short read\n"); return 1; }
+        double t0 = timing ? now_s() : 0.0;
         int r = icw_amod_process_samples(out, mc, in, n);
+        if (timing) {
+            double dt = now_s() - t0;
+            lat[nb++] = dt;
+            busy += dt;
+        }
         if (r < 0) { fprintf(stderr, "process: %s\n", icw_strerror(r)); return 1; }
         fwrite(out, (size_t)osz, (size_t)r, o);
         done += r;
@@ -151,6 +183,17 @@ int main(int argc, char **argv)
     icw_mod_context_meters(mc, 0, &m);
     fprintf(stderr, "%lld frames, clips %u/%u, peak %.2f/%.2f dB, desubnorm %llu\n", (long long)done, m.clips[0],
             m.clips[1], m.peak_db[0], m.peak_db[1], (unsigned long long)m.desubnorm);
+    if (timing && nb > 0) {
+        const double first = lat[0];
+        qsort(lat, (size_t)nb, sizeof(double), cmp_d);
+        printf("{\"frames\": %lld, \"block_frames\": %u, \"blocks\": %lld, \"decode_s\": %.6f, "
+               "\"msamples_per_s\": %.4f, \"block_us\": {\"min\": %.1f, \"p50\": %.1f, \"p99\": %.1f, "
+               "\"max\": %.1f, \"first\": %.1f}, \"realtime_x\": %.1f}\n",
+               (long long)done, block, (long long)nb, busy, 2.0 * (double)done / busy * 1e-6, lat[0] * 1e6,
+               lat[nb / 2] * 1e6, lat[(nb * 99) / 100] * 1e6, lat[nb - 1] * 1e6, first * 1e6,
+               (double)done / (double)rate / busy);
+    }
+    free(lat);
     fclose(o);
     fclose(f);
     free(in);

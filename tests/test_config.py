@@ -159,3 +159,23 @@ def test_config_drives_the_oracle_graph(oracle):
     ref_cfg.render.dth_bits, ref_cfg.render.sign_bits16 = 1.5, 14
     b = oracle.Stream(ref_cfg, nodes).process(raw, 2000, want_pre=True)
     assert np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1])
+
+
+def test_generated_config_texts_agree_with_restatement():
+    """the texts tests/test_gpu_config_device.py feeds to the GPU: the product reader and the
+    Python restatement give byte-identical icw_config / icw_node structures, equal to the graph
+    the text was written from"""
+    from tests import graphgen
+    from tests.cfggen import config_text, oracle_side
+    for seed in range(48):
+        rng = np.random.default_rng(4242 + seed)
+        fs = int(rng.choice(graphgen.RATES))
+        nodes = graphgen.random_list(rng)
+        text = config_text(rng, nodes)
+        ok, fc, bad = L.config_load(text, sample_rate=fs)
+        assert ok and bad == 0
+        cfg_o, nodes_o, _ = oracle_side(text, fs)
+        assert bytes(fc.cfg) == bytes(cfg_o)
+        assert fc.n_nodes == len(nodes_o) == len(nodes)
+        for i in range(fc.n_nodes):
+            assert bytes(fc.nodes[i]) == bytes(nodes_o[i]) == bytes(nodes[i])
