@@ -20,7 +20,10 @@ size must equal --gpus.  With fewer devices than ranks (the 1-GPU box) the ranks
 and use gloo for the barrier and the timing reduce (RCCL needs a GPU per rank).
 
 --workload picks one of the BASELINE.json configs; the default, c2, is the one the
-headline metric is quoted on.  The others are measured for DESIGN.md, not for the bench line.
+headline metric is quoted on.  A default run at N=1 also measures the other configs briefly
+(C3/C4/C5: 1 warmup + 2 steps each; C1: one pass) and reports them under `other_workloads` in the
+same line -- beside the headline, never in `value`; --no-other-workloads or --no-cpu-baseline skip
+them.
 c1 is the single-stream drop-in: the C host examples/icw_transcode (no Python in its loop) decodes
 a 30 s 44.1 kHz stereo track through icw_amod_process_samples in 576-frame blocks from host
 memory, timing every call; its CPU baseline is the oracle on the same track on one core, and the
@@ -106,6 +109,8 @@ def parse():
     ap.add_argument("--streams", type=int, default=None, help="streams per GPU (default: the workload's)")
     ap.add_argument("--frames", type=int, default=None, help="frames per stream per step (default: the workload's)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-other-workloads", action="store_true",
+                    help="c2 at N=1: skip the short C1/C3/C4/C5 runs reported under other_workloads")
     ap.add_argument("--cpu-workers", type=int, default=0, help="0: one per physical core available here")
     ap.add_argument("--cpu-frames", type=int, default=1 << 25)
     ap.add_argument("--block", type=int, default=576, help="c1: frames per boundary call (NS_PERTIME)")
@@ -236,6 +241,10 @@ def _wav_i16(path, raw, rate, ch):
 
 
 def bench_c1(a):
+    print(json.dumps(measure_c1(a.steps, a.warmup, a.block, not a.no_cpu_baseline)), flush=True)
+
+
+def measure_c1(steps, warmup, block, with_cpu):
     """single-stream drop-in: K runs of the C host over the track, W untimed"""
     import tempfile
     from in_cwave_amd import synth
@@ -249,20 +258,21 @@ def bench_c1(a):
     _wav_i16(src, raw, W["fs"], 2)
     env = dict(os.environ, ICW_TIMING="1")
     runs = []
-    for i in range(a.warmup + a.steps):
-        r = subprocess.run([str(exe), str(src), str(dst), str(a.block), "shift", "16"], env=env,
+    for i in range(warmup + steps):
+        r = subprocess.run([str(exe), str(src), str(dst), str(block), "shift", "16"], env=env,
                            capture_output=True, text=True, timeout=600)
         if r.returncode != 0:
             raise SystemExit(f"icw_transcode failed ({r.returncode}): {r.stderr[-500:]}")
-        if i >= a.warmup:
+        if i >= warmup:
             runs.append(json.loads(r.stdout.strip().splitlines()[-1]))
     out = np.frombuffer(dst.read_bytes()[44:], dtype=np.uint8)
     decode_s = sum(x["decode_s"] for x in runs)
     value = 2.0 * W["frames"] * len(runs) / decode_s / 1e6
     cpu = parity = None
-    if not a.no_cpu_baseline:
+    if with_cpu:
         from oracle import oracle as O
         n_avail, cpus, model, topo = host_cores()
+        old_aff = os.sched_getaffinity(0)
         try:
             os.sched_setaffinity(0, {cpus[0]})
         except OSError:
@@ -272,22 +282,26 @@ def bench_c1(a):
         st.open(W["frames"])
         outs = []
         t0 = time.perf_counter()
-        for f0 in range(0, W["frames"], a.block):
-            n = min(a.block, W["frames"] - f0)
+        for f0 in range(0, W["frames"], block):
+            n = min(block, W["frames"] - f0)
             outs.append(st.process(raw[f0 * 4:(f0 + n) * 4], n)[0])
         dt = time.perf_counter() - t0
+        try:
+            os.sched_setaffinity(0, old_aff)
+        except OSError:
+            pass
         ref = np.concatenate(outs)
         parity = "bit-exact" if np.array_equal(ref, out) else "MISMATCH"
         cpu = {"value": 2.0 * W["frames"] / dt / 1e6, "unit": "Msamples/s", "cores": 1, "kind": "port",
-               "cpu_model": model, "sample": f"the same 30 s track, oracle C restatement in {a.block}-frame "
+               "cpu_model": model, "sample": f"the same 30 s track, oracle C restatement in {block}-frame "
                                               f"blocks on one pinned core, {dt:.2f}s"}
     last = runs[-1]
     line = {
         "metric": "Msamples/s through Hilbert+mod+render", "value": value, "unit": "Msamples/s", "n_gpus": 1,
-        "steps": len(runs), "warmup": a.warmup, "ms_per_step": decode_s * 1e3 / len(runs),
+        "steps": len(runs), "warmup": warmup, "ms_per_step": decode_s * 1e3 / len(runs),
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
         "config": {"workload": W["desc"], "streams_per_gpu": 1, "frames_per_stream_per_step": W["frames"],
-                   "fs": W["fs"], "block_frames": a.block, "parallelism": "single stream"},
+                   "fs": W["fs"], "block_frames": block, "parallelism": "single stream"},
         "block_latency_us": last["block_us"], "realtime_x": last["realtime_x"], "parity_vs_oracle": parity,
         "cpu_baseline": cpu,
         "note": "host pointers through the drop-in boundary: each call stages its block H2D, runs K0-K2 "
@@ -297,10 +311,134 @@ def bench_c1(a):
     for f in (src, dst):
         f.unlink()
     tmp.rmdir()
-    print(json.dumps(line), flush=True)
+    return line
 
 
 # ----------------------------------------------------------------------------- GPU leg ------
+def measure_gpu(wname, streams, frames, steps, warmup, e2e_steps, dev, local_dev, dist, rank, world):
+    """one workload on this rank's device: W untimed steps, then K steps between barriers +
+    synchronize, max over ranks; the K1 roofline from the HIP-event timing of the timed steps"""
+    import torch
+    from in_cwave_amd import synth
+    from in_cwave_amd import lib as L
+
+    W = WORKLOADS[wname]
+    S = streams or W["streams"]
+    T = frames or W["frames"]
+    fs = W["fs"]
+    cfg, nodes, fmt = workload_config(W)
+    ctx = L.Context(cfg, nodes, S, device=local_dev)
+    # synthetic input of the workload's shape for this rank's shard of streams (SURVEY 8(d)
+    # generator); 16 distinct generated streams are tiled over the shard to bound setup time
+    n_gen = min(S, 16)
+    first = rank * S
+    gen = synth.batch_pcm(n_gen, T, fs, channels=W["ch"], fmt=fmt, first=first)   # uint8 [n_gen, T*fsz]
+    d_in = torch.empty((S, gen.shape[1]), dtype=torch.uint8, device=dev)
+    g = torch.from_numpy(gen).to(dev)
+    for s in range(S):
+        d_in[s].copy_(g[s % n_gen])
+    del g
+    osz = 2 * ctx.render_size
+    d_out = torch.empty((S, T * osz), dtype=torch.uint8, device=dev)
+    torch.cuda.synchronize()
+    hip_stream = torch.cuda.current_stream(dev).cuda_stream
+
+    def step(timing):
+        ctx.process_device(d_in, d_in.stride(0), d_out, d_out.stride(0), T, timing=timing, hip_stream=hip_stream)
+
+    for _ in range(warmup):
+        step(False)
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    k1_ms = k2_ms = 0.0
+    k1_n = k2_n = 0
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step(True)
+        (m1, m2), (n1, n2) = ctx.last_timing()
+        k1_ms += m1
+        k2_ms += m2
+        k1_n += n1
+        k2_n += n2
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    ctx.synchronize()     # raises if a kernel reported a failed hand-off
+    if dist:
+        t = torch.tensor([elapsed], dtype=torch.float64,
+                         device=dev if dist.get_backend() == "nccl" else "cpu")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    frames_total = float(S) * T * steps * world
+    value = 2.0 * frames_total / elapsed / 1e6
+    ms_per_step = elapsed * 1e3 / steps
+
+    # ---- end to end from host memory (H2D + D2H in the loop), one rank's view, not `value`
+    e2e = None
+    if e2e_steps > 0 and rank == 0:
+        h_in = np.ascontiguousarray(np.tile(gen, ((S + n_gen - 1) // n_gen, 1))[:S])
+        h_out = np.empty((S, T * osz), dtype=np.uint8)
+        ctx.process(h_in, T, out=h_out)                       # warm the staging buffers
+        te = time.perf_counter()
+        for _ in range(e2e_steps):
+            ctx.process(h_in, T, out=h_out)
+        te = time.perf_counter() - te
+        del h_out
+        e2e = {"value": 2.0 * S * T * e2e_steps / te / 1e6, "unit": "Msamples/s",
+               "ms_per_step": te * 1e3 / e2e_steps, "steps": e2e_steps,
+               "note": "host (pageable numpy) input and output: the call stages them through the "
+                       "context's pinned buffers, H2D + kernels + D2H, one GPU"}
+
+    # ---- roofline of the dominant kernel K1 (the serial recurrence), per launch, from HIP events
+    # recorded on the stream K1 runs on (icw_last_timing)
+    k1_kind = ctx.last_k1_kernel()
+    k1_name = K1_KERNEL_NAME.get(k1_kind, "?")
+    frames_per_launch = float(S) * T * steps / max(1, k1_n)
+    k1_avg_s = k1_ms / 1e3 / max(1, k1_n)
+    k2_avg_s = k2_ms / 1e3 / max(1, k2_n)
+    chains_per_stream = 2 if (W["ch"] == 1) else 4        # the mono dedup runs the left chains only
+    flops_per_frame = chains_per_stream * 5 * IIR_ORDER   # loop-back Kahan sum: N x (1 mul + 4 add)
+    achieved_tf = flops_per_frame * frames_per_launch / k1_avg_s / 1e12 if k1_avg_s > 0 else None
+    hbm_gbs = W["bytes"] * frames_per_launch / k1_avg_s / 1e9 if k1_avg_s > 0 else None
+    traffic = None
+    pmc_file = _latest("r*_c2_pmc.json")
+    try:   # HBM bytes per launch of the same kernel/config from the committed PMC passes
+        pmc = json.loads(pmc_file.read_text())
+        if int(pmc["frames_per_launch"]) == int(frames_per_launch) and wname == "c2":
+            traffic = next(v["hbm_bytes_corrected"] for k, v in pmc["kernels"].items()
+                           if k.split("<")[0].split("(")[0].split()[-1] == k1_name)
+    except Exception:
+        traffic = None
+    valu = K1_VALU_PER_SAMPLE.get(k1_kind)
+    samples_per_chain = frames_per_launch / S
+    floor_ms = (samples_per_chain * valu * CYC_PER_FP64_VALU / (CLOCK_GHZ * 1e6)) if valu else None
+    roof = {
+        "bound": "fp64", "achieved": achieved_tf, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+        "frac": (achieved_tf / FP64_PEAK_TFLOPS) if achieved_tf else None, "traffic": traffic,
+        "kernel": k1_name, "flops_per_frame": flops_per_frame, "frames_per_launch": frames_per_launch,
+        "avg_launch_ms": k1_avg_s * 1e3, "output_kernel_avg_launch_ms": k2_avg_s * 1e3,
+        "hbm": {"achieved": hbm_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": (hbm_gbs / HBM_PEAK_GBS) if hbm_gbs else None,
+                "alg_bytes_per_frame": W["bytes"], "traffic_source": pmc_file.name if (traffic and pmc_file) else None},
+        "issue_bound": {"valu_per_sample": valu, "cycles_per_valu": CYC_PER_FP64_VALU, "clock_ghz": CLOCK_GHZ,
+                        "floor_ms_per_launch": floor_ms,
+                        "frac": (floor_ms / (k1_avg_s * 1e3)) if (k1_avg_s and floor_ms) else None},
+        "note": f"serial IIR recurrence: {chains_per_stream * S} DF-II chains per GPU, each a dependent "
+                f"chain of ~{4 * IIR_ORDER} FP64 ops per sample ({'one 16-lane DPP row' if k1_kind == 3 else 'one lane'}"
+                f" per chain); `frac` is the algorithmic FP64 rate (5N = {5 * IIR_ORDER} flops per chain-sample) "
+                f"against the FP64 vector peak, small because {chains_per_stream * S} chains cannot fill "
+                f"1024 SIMDs; issue_bound.frac ~1 = at the per-wave issue floor (DESIGN.md 5)",
+    }
+
+    ctx.close()
+    return {"value": value, "ms_per_step": ms_per_step, "roofline": roof, "e2e": e2e, "W": W, "S": S, "T": T,
+            "fs": fs}
+
+
 def main():
     a = parse()
     if a.workload == "c1":
@@ -329,120 +467,36 @@ def main():
     dev = torch.device("cuda", local_dev)
     torch.cuda.set_device(dev)
 
-    from in_cwave_amd import synth
-    from in_cwave_amd import lib as L
+    r = measure_gpu(a.workload, a.streams, a.frames, a.steps, a.warmup, a.e2e_steps, dev, local_dev, dist, rank,
+                    world)
+    W, S, T, fs = r["W"], r["S"], r["T"], r["fs"]
+    value, ms_per_step, roof, e2e = r["value"], r["ms_per_step"], r["roofline"], r["e2e"]
 
-    W = WORKLOADS[a.workload]
-    S = a.streams or W["streams"]
-    T = a.frames or W["frames"]
-    fs = W["fs"]
-    cfg, nodes, fmt = workload_config(W)
-    ctx = L.Context(cfg, nodes, S, device=local_dev)
-    # synthetic input of the workload's shape for this rank's shard of streams (SURVEY 8(d)
-    # generator); 16 distinct generated streams are tiled over the shard to bound setup time
-    n_gen = min(S, 16)
-    first = rank * S
-    gen = synth.batch_pcm(n_gen, T, fs, channels=W["ch"], fmt=fmt, first=first)   # uint8 [n_gen, T*fsz]
-    d_in = torch.empty((S, gen.shape[1]), dtype=torch.uint8, device=dev)
-    g = torch.from_numpy(gen).to(dev)
-    for s in range(S):
-        d_in[s].copy_(g[s % n_gen])
-    del g
-    osz = 2 * ctx.render_size
-    d_out = torch.empty((S, T * osz), dtype=torch.uint8, device=dev)
-    torch.cuda.synchronize()
-    hip_stream = torch.cuda.current_stream(dev).cuda_stream
-
-    def step(timing):
-        ctx.process_device(d_in, d_in.stride(0), d_out, d_out.stride(0), T, timing=timing, hip_stream=hip_stream)
-
-    for _ in range(a.warmup):
-        step(False)
-    torch.cuda.synchronize()
-    if dist:
-        dist.barrier()
-    torch.cuda.synchronize()
-    k1_ms = k2_ms = 0.0
-    k1_n = k2_n = 0
-    t0 = time.perf_counter()
-    for _ in range(a.steps):
-        step(True)
-        (m1, m2), (n1, n2) = ctx.last_timing()
-        k1_ms += m1
-        k2_ms += m2
-        k1_n += n1
-        k2_n += n2
-    torch.cuda.synchronize()
-    if dist:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    ctx.synchronize()     # raises if a kernel reported a failed hand-off
-    if dist:
-        t = torch.tensor([elapsed], dtype=torch.float64,
-                         device=dev if dist.get_backend() == "nccl" else "cpu")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-
-    frames_total = float(S) * T * a.steps * world
-    value = 2.0 * frames_total / elapsed / 1e6
-    ms_per_step = elapsed * 1e3 / a.steps
-
-    # ---- end to end from host memory (H2D + D2H in the loop), one rank's view, not `value`
-    e2e = None
-    if a.e2e_steps > 0 and rank == 0:
-        h_in = np.ascontiguousarray(np.tile(gen, ((S + n_gen - 1) // n_gen, 1))[:S])
-        h_out = np.empty((S, T * osz), dtype=np.uint8)
-        ctx.process(h_in, T, out=h_out)                       # warm the staging buffers
-        te = time.perf_counter()
-        for _ in range(a.e2e_steps):
-            ctx.process(h_in, T, out=h_out)
-        te = time.perf_counter() - te
-        del h_out
-        e2e = {"value": 2.0 * S * T * a.e2e_steps / te / 1e6, "unit": "Msamples/s",
-               "ms_per_step": te * 1e3 / a.e2e_steps, "steps": a.e2e_steps,
-               "note": "host (pageable numpy) input and output: the call stages them through the "
-                       "context's pinned buffers, H2D + kernels + D2H, one GPU"}
-
-    # ---- roofline of the dominant kernel K1 (the serial recurrence), per launch, from HIP events
-    # recorded on the stream K1 runs on (icw_last_timing)
-    k1_kind = ctx.last_k1_kernel()
-    k1_name = K1_KERNEL_NAME.get(k1_kind, "?")
-    frames_per_launch = float(S) * T * a.steps / max(1, k1_n)
-    k1_avg_s = k1_ms / 1e3 / max(1, k1_n)
-    k2_avg_s = k2_ms / 1e3 / max(1, k2_n)
-    chains_per_stream = 2 if (W["ch"] == 1) else 4        # the mono dedup runs the left chains only
-    flops_per_frame = chains_per_stream * 5 * IIR_ORDER   # loop-back Kahan sum: N x (1 mul + 4 add)
-    achieved_tf = flops_per_frame * frames_per_launch / k1_avg_s / 1e12 if k1_avg_s > 0 else None
-    hbm_gbs = W["bytes"] * frames_per_launch / k1_avg_s / 1e9 if k1_avg_s > 0 else None
-    traffic = None
-    pmc_file = _latest("r*_c2_pmc.json")
-    try:   # HBM bytes per launch of the same kernel/config from the committed PMC passes
-        pmc = json.loads(pmc_file.read_text())
-        if int(pmc["frames_per_launch"]) == int(frames_per_launch) and a.workload == "c2":
-            traffic = next(v["hbm_bytes_corrected"] for k, v in pmc["kernels"].items()
-                           if k.split("<")[0].split("(")[0].split()[-1] == k1_name)
-    except Exception:
-        traffic = None
-    valu = K1_VALU_PER_SAMPLE.get(k1_kind)
-    samples_per_chain = frames_per_launch / S
-    floor_ms = (samples_per_chain * valu * CYC_PER_FP64_VALU / (CLOCK_GHZ * 1e6)) if valu else None
-    roof = {
-        "bound": "fp64", "achieved": achieved_tf, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
-        "frac": (achieved_tf / FP64_PEAK_TFLOPS) if achieved_tf else None, "traffic": traffic,
-        "kernel": k1_name, "flops_per_frame": flops_per_frame, "frames_per_launch": frames_per_launch,
-        "avg_launch_ms": k1_avg_s * 1e3, "output_kernel_avg_launch_ms": k2_avg_s * 1e3,
-        "hbm": {"achieved": hbm_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": (hbm_gbs / HBM_PEAK_GBS) if hbm_gbs else None,
-                "alg_bytes_per_frame": W["bytes"], "traffic_source": pmc_file.name if (traffic and pmc_file) else None},
-        "issue_bound": {"valu_per_sample": valu, "cycles_per_valu": CYC_PER_FP64_VALU, "clock_ghz": CLOCK_GHZ,
-                        "floor_ms_per_launch": floor_ms,
-                        "frac": (floor_ms / (k1_avg_s * 1e3)) if (k1_avg_s and floor_ms) else None},
-        "note": f"serial IIR recurrence: {chains_per_stream * S} DF-II chains per GPU, each a dependent "
-                f"chain of ~{4 * IIR_ORDER} FP64 ops per sample ({'one 16-lane DPP row' if k1_kind == 3 else 'one lane'}"
-                f" per chain); `frac` is the algorithmic FP64 rate (5N = {5 * IIR_ORDER} flops per chain-sample) "
-                f"against the FP64 vector peak, small because {chains_per_stream * S} chains cannot fill "
-                f"1024 SIMDs; issue_bound.frac ~1 = at the per-wave issue floor (DESIGN.md 5)",
-    }
+    # ---- the other BASELINE configs, measured in the same run (N=1 only): short runs of the same
+    # harness, reported beside the headline, never in `value`
+    others = None
+    if (world == 1 and a.workload == "c2" and not a.no_other_workloads and not a.no_cpu_baseline
+            and a.streams is None and a.frames is None):
+        others = {}
+        import gc
+        import torch
+        for w in os.environ.get("ICW_BENCH_OTHERS", "c3,c4,c5").split(","):
+            gc.collect()
+            torch.cuda.empty_cache()
+            o = measure_gpu(w, None, None, 2, 1, 0, dev, local_dev, None, 0, 1)
+            ro = o["roofline"]
+            others[w] = {"value": o["value"], "unit": "Msamples/s", "ms_per_step": o["ms_per_step"], "steps": 2,
+                         "warmup": 1, "workload": o["W"]["desc"], "streams_per_gpu": o["S"],
+                         "frames_per_stream_per_step": o["T"], "k1_kernel": ro["kernel"],
+                         "k1_avg_launch_ms": ro["avg_launch_ms"], "k2_avg_launch_ms": ro["output_kernel_avg_launch_ms"],
+                         "fp64_frac": ro["frac"]}
+        try:
+            c1 = measure_c1(1, 1, 576, True)
+            others["c1"] = {k: c1[k] for k in ("value", "unit", "ms_per_step", "block_latency_us", "realtime_x",
+                                               "parity_vs_oracle", "cpu_baseline")}
+            others["c1"]["workload"] = c1["config"]["workload"]
+        except (SystemExit, Exception) as e:      # reported, never silently replaced
+            others["c1"] = {"error": repr(e)}
 
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
@@ -463,9 +517,9 @@ def main():
             "roofline": roof,
             "e2e_host_buffers": e2e,
             "cpu_baseline": cpu,
+            "other_workloads": others,
         }
         print(json.dumps(line), flush=True)
-    ctx.close()
     if dist:
         dist.destroy_process_group()
 

@@ -14,6 +14,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <deque>
 #include <mutex>
 #include <new>
 #include <vector>
@@ -102,9 +103,11 @@ struct icw_ctx {
     hipStream_t stream2 = nullptr;
     hipEvent_t k1done[kSets] = {}, k2done[kSets] = {}, join = nullptr;
     hipEvent_t k0done[kSets] = {};
-    std::vector<CuSplit> splits;          /* cached CU-partitioned stream sets, by K1 CU count */
     bool cu_split = true;                 /* ICW_CU_SPLIT=0 disables the partition */
-    int k1_wpc = 4;                       /* ICW_K1_WPC: K1 waves per CU (one per SIMD) */
+    /* ICW_K1_WPC: K1 waves per CU.  Two: measured under a working partition, 4 per CU (one per
+     * SIMD) made K1 +21 % slower even alone (C3, 4-wave workgroups), 3 per CU +27 % beside K2, and 1
+     * per CU leaves the frame-parallel kernels too few CUs (C4 K2 2.57 -> 3.70 ms) */
+    int k1_wpc = 2;
     int k1_wg = 1;                        /* ICW_K1_WG: K1 waves per workgroup */
     bool k1_lds = false;                  /* ICW_K1_LDS=1: K1 workgroups hold the CU's LDS (A/B) */
     bool fill_drain = true;               /* ICW_FILL_DRAIN=0: first K0 / last K2 stay partitioned (A/B) */
@@ -403,8 +406,12 @@ int grow(void **p, size_t *cur, size_t need)
     return ICW_OK;
 }
 
-/* The stream set for a K1 of k1_cus CUs: K1's CUs are spread evenly over the device (every
- * n_cu / k1_cus-th CU, so each XCD gets its share), the other streams get the remaining CUs. */
+/* The stream set for a K1 of k1_cus CUs (a multiple of the XCD count): K1's CUs are spread evenly
+ * over the XCDs and their shader engines, the other streams get the remaining CUs.
+ * Queue CU-mask bits on gfx950 are dealt round-robin: bit b selects XCD b % 8, and within it the
+ * (b / 8)-th CU, whose shader-engine group is again (b / 8) % 4 (measured, tools/cumask_probe.hip).
+ * An XCD with no bit set in a mask runs that queue's work on ALL of its CUs, so each mask must
+ * name CUs in every XCD: the K1 mask is bits [0, k1_cus), the rest its complement. */
 /* wait for every kernel and copy of the context (they run on several streams, the caller's among
  * them); host-side state changes and reads happen only between calls */
 hipError_t quiesce(icw_ctx *c)
@@ -413,14 +420,23 @@ hipError_t quiesce(icw_ctx *c)
     return hipDeviceSynchronize();
 }
 
+/* The CU-masked stream sets live for the process, shared by every context of a device: measured,
+ * a second context's own masked streams did not keep K1 off the other kernels' CUs (C3 K1 3.1 ->
+ * 4.7 ms per launch in any context after the first of a process, C2 2.8 -> 4.1), while one set
+ * created once and reused keeps the partition.  Sharing only adds ordering between contexts that
+ * run on the same device at the same time. */
+std::mutex g_split_mu;
+std::deque<std::pair<int, CuSplit>> g_splits;    /* deque: entries never move */
+
 const CuSplit *cu_split(icw_ctx *c, int k1_cus)
 {
-    for (auto &x : c->splits)
-        if (x.k1_cus == k1_cus) return &x;
+    std::lock_guard<std::mutex> lk(g_split_mu);
+    for (auto &x : g_splits)
+        if (x.first == c->device && x.second.k1_cus == k1_cus) return &x.second;
     const int n = c->n_cu, words = (n + 31) / 32;
     std::vector<uint32_t> mk(words, 0u), mr(words, 0u);
     std::vector<char> used(n, 0);
-    for (int i = 0; i < k1_cus; ++i) used[(int)((long)i * n / k1_cus)] = 1;
+    for (int i = 0; i < k1_cus && i < n; ++i) used[i] = 1;
     for (int cu = 0; cu < n; ++cu) (used[cu] ? mk : mr)[cu / 32] |= 1u << (cu % 32);
     CuSplit x;
     x.k1_cus = k1_cus;
@@ -432,8 +448,8 @@ const CuSplit *cu_split(icw_ctx *c, int k1_cus)
             if (q) hipStreamDestroy(q);
         return nullptr;
     }
-    c->splits.push_back(x);
-    return &c->splits.back();
+    g_splits.emplace_back(c->device, x);
+    return &g_splits.back().second;
 }
 
 void free_all(icw_ctx *c)
@@ -453,9 +469,6 @@ void free_all(icw_ctx *c)
     if (c->stream3) hipStreamDestroy(c->stream3);
     if (c->stream4) hipStreamDestroy(c->stream4);
     if (c->join) hipEventDestroy(c->join);
-    for (auto &x : c->splits)
-        for (hipStream_t q : {x.k1, x.rest, x.dith, x.render})
-            if (q) hipStreamDestroy(q);
     if (c->stream2) hipStreamDestroy(c->stream2);
     for (auto e : c->ev) hipEventDestroy(e);
     if (c->stream) hipStreamDestroy(c->stream);
@@ -876,7 +889,8 @@ int icw_process_streams(icw_ctx *c, int first, int count, const void *in, size_t
         /* plain K1: 128-lane groups of 32 streams (64 with the dedup); the variants: a lane per chain */
         const int k1_waves = (k1_mode == 0 || k1_mode == ICW_K1_FC) ? ((count + (dedup ? 63 : 31)) / (dedup ? 64 : 32)) * 2
                            : row_waves;
-        const int k1_cus = (k1_waves + c->k1_wpc - 1) / c->k1_wpc;
+        constexpr int kXcd = 8;                               /* MI355X: 8 XCDs */
+        const int k1_cus = ((k1_waves + c->k1_wpc - 1) / c->k1_wpc + kXcd - 1) / kXcd * kXcd;
         if (c->cu_split && !c->k1_lds && k1_cus * 2 <= c->n_cu) {
             const CuSplit *cs = cu_split(c, k1_cus);
             if (!cs) return ICW_EDEVICE;

@@ -76,3 +76,13 @@ def test_bench_line_fields():
         < 1e-9 * rf["achieved"]
     assert rf["hbm"]["unit"] == "GB/s" and rf["issue_bound"]["frac"] > 0
     assert d["e2e_host_buffers"]["value"] > 0
+
+
+def test_bench_c1_drop_in_line():
+    """C1: the C host through the drop-in boundary in 576-frame blocks; its output equals the oracle's"""
+    r = subprocess.run([sys.executable, "bench.py", "--workload", "c1", "--steps", "1", "--warmup", "0"], cwd=ROOT,
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    d = _line(r.stdout)
+    assert d["parity_vs_oracle"] == "bit-exact"
+    assert d["value"] > 0 and d["block_latency_us"]["p50"] > 0 and d["cpu_baseline"]["cores"] == 1

@@ -281,3 +281,22 @@ def test_bus_pure_delay_is_one_frame_late(oracle):
     _, p2 = oracle.Stream(cfg, graph.graph_pure_delay()).process(raw, 1500, want_pre=True)
     assert np.all(p2[0] == 0.0)
     assert np.array_equal(p2[1:].view(np.uint64), p1[:-1].view(np.uint64))
+
+
+@pytest.mark.parametrize("type_", [0, 1, 4])
+def test_restarted_recurrence_never_resynchronizes(oracle, type_):
+    """Why K1 cannot split a stream's time axis: a chain restarted from a zero state part
+    way through a track never falls back onto the true trajectory bit for bit -- the DF-II states
+    are large (|w| ~ 1e7..1e13) and the rounding noise they carry keeps two trajectories apart at a
+    plateau, so no window of N equal states (which would make the rest identical) ever appears"""
+    fs, n, s0 = 48000, 160000, 40000
+    raw = synth.stream_pcm(3, n, fs).view("<i2").reshape(n, 2)[:, 0].astype(np.float64)
+    k = np.arange(n) % 4
+    x = np.where(k == 0, raw, np.where(k == 2, -raw, 0.0))          # the I chain's input
+    _, w, _ = oracle.iir_block(x, type_, 1, 1)
+    _, w2, _ = oracle.iir_block(x[s0:], type_, 1, 1)
+    eq = (w[s0:].view(np.uint64) == w2.view(np.uint64)).astype(np.int64)
+    run = np.convolve(eq, np.ones(20, dtype=np.int64), mode="valid")   # order <= 20
+    assert run.max() < 20
+    tail = slice(-20000, None)
+    assert np.max(np.abs(w[s0:][tail] - w2[tail])) > 0.0
