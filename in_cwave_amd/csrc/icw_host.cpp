@@ -854,12 +854,13 @@ int icw_process_streams(icw_ctx *c, int first, int count, const void *in, size_t
     bool dedup = !cw && !fcm && nch == 1 && c->dedup_ok && (c->k1_mode <= 0 || c->k1_mode == 3);   /* plain / row K1 */
     for (int i = 0; dedup && i < count; ++i) dedup = c->lr_known[first + i] != 0;
     /* K1 variant of this call.  Auto: the row-broadcast kernel (4 chains per wave, ~17 % fewer
-     * instructions per sample) when its waves fit one per SIMD on at most half the chip, else the
-     * lane-per-chain kernel (64 chains per wave).  The row kernel needs Kahan + the reject. */
+     * instructions per sample) when its waves fit k1_wpc per CU on at most half the chip, else the
+     * lane-per-chain kernel (64 chains per wave).  The row kernel needs Kahan + the reject.  (Round
+     * 1 kept it off with a serial render; with the partition working, C5 gains 9 % from it.) */
     const int row_waves = (int)(((dedup ? count : 2L * count) + 3) / 4) * 2;
     const bool row_ok = cfg.iir_kahan && cfg.iir_subnorm_reject;
     int k1_mode = c->k1_mode;
-    if (k1_mode < 0) k1_mode = (row_ok && !c->serial_render && row_waves * 2 <= c->n_cu * 4) ? 3 : 0;
+    if (k1_mode < 0) k1_mode = (row_ok && row_waves <= (c->n_cu / 2) * c->k1_wpc) ? 3 : 0;
     if (k1_mode == 3 && !row_ok) k1_mode = 0;
     if (fcm) k1_mode = ICW_K1_FC;
     if (!cw) c->last_k1 = k1_mode;

@@ -220,8 +220,8 @@ int icw_set_state(icw_ctx *ctx, int s, const void *blob, size_t size);
 int icw_last_timing(icw_ctx *ctx, double ms[2], int launches[2]);
 
 /* IIR state kernel (the serial recurrence) the last real-input icw_process_* call ran: ICW_K1_*.
- * The host picks the row-broadcast kernel for small batches (its waves fit one per SIMD on half
- * the chip, Kahan sum with the reject, no serial render) and the lane-per-chain kernel otherwise;
+ * The host picks the row-broadcast kernel for small batches (its waves fit two per CU on half
+ * the chip, Kahan sum with the reject) and the lane-per-chain kernel otherwise;
  * ICW_K1_MODE=plain|row in the environment at icw_create forces one (A/B runs).  Codes 1 and 2
  * named two archived experiments (tools/k1_experimental.hip) and are no longer returned. */
 #define ICW_K1_LANE   0   /* icw_iir_state: one lane per DF-II chain */
