@@ -49,6 +49,8 @@ struct IcwAdvArgs {
     unsigned long long *n_frame;
     unsigned long long ssr;
     int32_t scaled;
+    const int *err;                /* with err_copy: the hand-off flag is copied next to the output, */
+    int *err_copy;                 /* so a small host-pointer call reads both with one copy */
 };
 
 /* Arguments of the serial graph kernel (bus form; one lane = one stream, loops over frames). */
@@ -193,6 +195,7 @@ struct IcwK2Args {
     int32_t trig_pitch;
     int32_t zero;                  /* always 0: an offset the compiler cannot fold (keeps loads in a loop) */
     uint32_t *fes;                 /* FP_CHECK census, as in IcwK1Args; null: no FC() */
+    int32_t tpw;                   /* tiles per workgroup (1..ICW_K2_TPW), set by the launcher */
 };
 
 /* Per-frame rotation table (one thread per frame): the Shift / PM factors depend only on the frame

@@ -50,6 +50,7 @@ double u2d(unsigned long long u)
 constexpr int kMaxBlockFrames = 1 << 16;
 constexpr int kDefBlockFrames = 1 << 14;   /* launch block: shorter pipeline fill / drain */
 constexpr int kSets = 3;                    /* most block scratch sets (ICW_SETS); default 2 */
+constexpr size_t kPinnedStage = 1u << 20;   /* host-pointer calls up to this size stage through pinned memory */
 
 struct DevState {
     double *hist = nullptr;               /* [chains][20] */
@@ -124,6 +125,10 @@ struct icw_ctx {
     size_t d_in_bytes = 0, d_out_bytes = 0;
     double *d_pre = nullptr;
     size_t d_pre_bytes = 0;
+    /* small host-pointer calls (the one-stream drop-in, 576-frame blocks): inputs and outputs are
+     * staged through this pinned buffer, so the copies are asynchronous and the call waits once */
+    unsigned char *h_stage = nullptr;
+    size_t h_stage_bytes = 0;
     /* the serial render (K4 bus-form graph + K3b) runs on a fourth stream, one block behind K2:
      * its inputs are double-buffered like the block scratch */
     hipStream_t stream4 = nullptr;
@@ -466,6 +471,7 @@ void free_all(icw_ctx *c)
         for (hipEvent_t e : {c->ditdone[p], c->k1done[p], c->k2done[p], c->k0done[p], c->k3done[p]})
             if (e) hipEventDestroy(e);
     }
+    if (c->h_stage) hipHostFree(c->h_stage);
     if (c->stream3) hipStreamDestroy(c->stream3);
     if (c->stream4) hipStreamDestroy(c->stream4);
     if (c->join) hipEventDestroy(c->join);
@@ -809,6 +815,18 @@ int icw_process_streams(icw_ctx *c, int first, int count, const void *in, size_t
     const unsigned char *d_in;
     unsigned char *d_out;
     size_t dis, dos;
+    /* a small host-pointer call stages through pinned memory (asynchronous copies, one wait) */
+    const size_t stage_in = (size_t)n_frames * fsz * S, stage_out = (size_t)n_frames * osz * S;
+    const bool pinned = !dev && stage_in + stage_out + 16 <= kPinnedStage;
+    if (pinned) {
+        if (c->h_stage_bytes < stage_in + stage_out + 16) {
+            if (c->h_stage) hipHostFree(c->h_stage);
+            c->h_stage = nullptr;
+            c->h_stage_bytes = 0;
+            if (hipHostMalloc((void **)&c->h_stage, kPinnedStage, hipHostMallocDefault) != hipSuccess) return ICW_ENOMEM;
+            c->h_stage_bytes = kPinnedStage;
+        }
+    }
     if (dev) {
         d_in = (const unsigned char *)in;
         d_out = (unsigned char *)out;
@@ -818,9 +836,15 @@ int icw_process_streams(icw_ctx *c, int first, int count, const void *in, size_t
         dis = (size_t)n_frames * fsz;
         dos = (size_t)n_frames * osz;
         if (grow((void **)&c->d_in, &c->d_in_bytes, dis * S)) return ICW_ENOMEM;
-        if (grow((void **)&c->d_out, &c->d_out_bytes, dos * S)) return ICW_ENOMEM;
-        if (hipMemcpy2DAsync(c->d_in, dis, in, in_stride, dis, S, hipMemcpyHostToDevice, st) != hipSuccess)
+        if (grow((void **)&c->d_out, &c->d_out_bytes, dos * S + 16)) return ICW_ENOMEM;
+        if (pinned) {
+            for (size_t i = 0; i < S; ++i)
+                memcpy(c->h_stage + i * dis, (const unsigned char *)in + i * in_stride, dis);
+            if (hipMemcpyAsync(c->d_in, c->h_stage, dis * S, hipMemcpyHostToDevice, st) != hipSuccess)
+                return ICW_EDEVICE;
+        } else if (hipMemcpy2DAsync(c->d_in, dis, in, in_stride, dis, S, hipMemcpyHostToDevice, st) != hipSuccess) {
             return ICW_EDEVICE;
+        }
         d_in = c->d_in;
         d_out = c->d_out;
     }
@@ -864,7 +888,8 @@ int icw_process_streams(icw_ctx *c, int first, int count, const void *in, size_t
     if (k1_mode == 3 && !row_ok) k1_mode = 0;
     if (fcm) k1_mode = ICW_K1_FC;
     if (!cw) c->last_k1 = k1_mode;
-    const bool table = c->prog.needs_omega && !bus && c->prog.n_trig > 0;
+    /* the shared rotation table pays from two streams on; one stream computes its factors inline */
+    const bool table = c->prog.needs_omega && !bus && c->prog.n_trig > 0 && count > 1;
     if (table && grow((void **)&c->trig, &c->trig_bytes, (size_t)Tb * 2 * c->prog.n_trig * sizeof(double)))
         return ICW_ENOMEM;
     if (bus)
@@ -884,7 +909,10 @@ int icw_process_streams(icw_ctx *c, int first, int count, const void *in, size_t
      * first block and K2 of the last run while no recurrence does, so they get the whole chip
      * instead of the partition's share (C3 / C4: the drain was one partitioned K2, ~5 % of a step) */
     hipStream_t sF = nullptr;
-    if (c->serialize) {
+    /* One launch block: K0 -> K1 -> K2 run in sequence anyway, so everything goes on the caller's
+     * stream -- no cross-stream event waits, which cost the 576-frame drop-in call ~135 us (C1
+     * p50 361 -> 226 us per call). */
+    if (c->serialize || n_blocks == 1) {
         sA = sD = sR = st;
     } else if (!cw) {
         /* plain K1: 128-lane groups of 32 streams (64 with the dedup); the variants: a lane per chain */
@@ -1149,17 +1177,30 @@ int icw_process_streams(icw_ctx *c, int first, int count, const void *in, size_t
         av.n_frame = ds.n_frame + f0;
         av.ssr = ssr;
         av.scaled = cfg.frmod_scaled;
+        if (pinned) {
+            av.err = ds.err;
+            av.err_copy = (int *)(d_out + dos * S);        /* the output buffer has 16 spare bytes */
+        }
         if (icw_launch_advance(&av, st) != hipSuccess) return ICW_EDEVICE;
     }
     if (legacy && hipStreamSynchronize(st) != hipSuccess) return ICW_EDEVICE;
     if (!dev) {
-        if (hipMemcpy2DAsync(out, out_stride, d_out, dos, dos, S, hipMemcpyDeviceToHost, st) != hipSuccess)
+        unsigned char *h_out = pinned ? c->h_stage + stage_in : nullptr;
+        if (pinned ? hipMemcpyAsync(h_out, d_out, dos * S + sizeof(int), hipMemcpyDeviceToHost, st) != hipSuccess
+                   : hipMemcpy2DAsync(out, out_stride, d_out, dos, dos, S, hipMemcpyDeviceToHost, st) != hipSuccess)
             return ICW_EDEVICE;
         if (d_pre && hipMemcpyAsync(dbg, d_pre, S * (size_t)n_frames * 2 * sizeof(double), hipMemcpyDeviceToHost, st) != hipSuccess)
             return ICW_EDEVICE;
-        if (hipStreamSynchronize(st) != hipSuccess) return ICW_EDEVICE;
         int e = 0;
-        if (hipMemcpy(&e, ds.err, sizeof(int), hipMemcpyDeviceToHost) != hipSuccess || e) return ICW_EDEVICE;
+        if (pinned) {
+            if (hipStreamSynchronize(st) != hipSuccess) return ICW_EDEVICE;
+            memcpy(&e, h_out + dos * S, sizeof(int));     /* the flag icw_advance copied */
+            for (size_t i = 0; i < S; ++i) memcpy((unsigned char *)out + i * out_stride, h_out + i * dos, dos);
+        } else {
+            if (hipStreamSynchronize(st) != hipSuccess) return ICW_EDEVICE;
+            if (hipMemcpy(&e, ds.err, sizeof(int), hipMemcpyDeviceToHost) != hipSuccess) return ICW_EDEVICE;
+        }
+        if (e) return ICW_EDEVICE;
     }
     if (timing) {
         if (hipStreamSynchronize(st) != hipSuccess) return ICW_EDEVICE;

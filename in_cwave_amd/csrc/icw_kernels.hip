@@ -428,7 +428,8 @@ __device__ __forceinline__ bool icw_exec_op(const IcwOp &op, IcwLR d, double ome
     }
 }
 
-/* Output kernel (K2).  A workgroup owns ICW_K2_TPW consecutive 256-frame tiles of one stream.
+/* Output kernel (K2).  A workgroup owns a.tpw (<= ICW_K2_TPW) consecutive 256-frame tiles of one
+ * stream (fewer when a launch would have too few workgroups to spread over the chip).
  * The w window of tile k+1 is loaded into registers while tile k is computed, then written to the
  * other half of a double-buffered LDS window: the global-load latency hides behind FP64 work and
  * the meters reduce once per workgroup.  TRIG = the program has an active Shift / PM node. */
@@ -447,8 +448,8 @@ __global__ __launch_bounds__(ICW_K2_TILE, ICW_K2_MINWG) void icw_output(IcwK2Arg
     const int s = blockIdx.y;
     const int tl = threadIdx.x;
     const int T = a.T;
-    const int tw0 = blockIdx.x * TILE * ICW_K2_TPW;
-    const int ntile = min(ICW_K2_TPW, (T - tw0 + TILE - 1) / TILE);
+    const int tw0 = blockIdx.x * TILE * a.tpw;
+    const int ntile = min(a.tpw, (T - tw0 + TILE - 1) / TILE);
 
     /* mono input, converters bit-identical at block start (K1's flag) and in phase: the right
      * filter outputs are copies of the left ones this block */
@@ -755,6 +756,7 @@ __global__ __launch_bounds__(64) void icw_advance(IcwAdvArgs a)
     }
     const unsigned long long n0 = a.n_frame[s];
     a.n_frame[s] = a.scaled ? (n0 + (unsigned long long)a.n) % a.ssr : n0 + (unsigned long long)a.n;
+    if (s == 0 && a.err_copy) *a.err_copy = *a.err;
 }
 
 /* ------------------------------------------------------ serial render kernel (K3) ------ */
@@ -1363,9 +1365,15 @@ extern "C" hipError_t icw_launch_unpack(const IcwK0Args *a, hipStream_t st)
 }
 
 template <int N, bool K>
-static hipError_t launch_k2_t(const IcwK2Args &a, hipStream_t st)
+static hipError_t launch_k2_t(IcwK2Args a, hipStream_t st)
 {
-    constexpr int span = ICW_K2_TILE * ICW_K2_TPW;
+    /* ICW_K2_TPW tiles per workgroup (the next window loads hide behind a tile's work, one meter
+     * atomic per 1024 frames); a small launch (the one-stream drop-in: 576 frames) uses fewer
+     * tiles per workgroup so that its tiles run side by side */
+    int tpw = ICW_K2_TPW;
+    while (tpw > 1 && (long)((a.T + ICW_K2_TILE * tpw - 1) / (ICW_K2_TILE * tpw)) * a.n_streams < 512) tpw >>= 1;
+    a.tpw = tpw;
+    const int span = ICW_K2_TILE * tpw;
     dim3 grid((a.T + span - 1) / span, a.n_streams);
     const size_t lds = (size_t)a.n_regs * 4 * ICW_K2_TILE * sizeof(double);
     if (a.fes && !a.cw) hipLaunchKernelGGL((icw_output<N, K, true, true>), grid, dim3(ICW_K2_TILE), lds, st, a);
