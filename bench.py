@@ -52,7 +52,7 @@ sys.path.insert(0, str(ROOT))
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 FP64_PEAK_TFLOPS = 78.6        # MI355X FP64 vector (256 CU x 2.4 GHz x 128 flop/clk), MI355X_MICROARCH.md
 # effective engine clock under the C2 recurrence: SQ_BUSY_CYCLES / 32 shader engines / launch time
-# (profiles/r01_c2_sq_counters.json: 6.48 M cycles per 2.80 ms launch = 2.31 GHz)
+# of the K1 kernel in the newest committed SQ pass (profiles/r*_c2_sq.json; r01: 2.31 GHz)
 CLOCK_GHZ = 2.31
 # Issue floor of the recurrence: a lone wave issues one FP64 VALU instruction per
 # ~5.0 cycles, dependent or not (profiles/r01_fp64_bank_probe.txt).  icw_iir_state<19> issues 91
@@ -414,8 +414,16 @@ def measure_gpu(wname, streams, frames, steps, warmup, e2e_steps, dev, local_dev
     except Exception:
         traffic = None
     valu = K1_VALU_PER_SAMPLE.get(k1_kind)
+    clock_ghz, clock_src = CLOCK_GHZ, "r01_c2_sq_counters.json"
+    sq_file = _latest("r*_c2_sq.json")
+    try:
+        sq = json.loads(sq_file.read_text())["kernels"]
+        clock_ghz = next(v["effective_clock_ghz"] for k, v in sq.items() if k1_name in k)
+        clock_src = sq_file.name
+    except Exception:
+        pass
     samples_per_chain = frames_per_launch / S
-    floor_ms = (samples_per_chain * valu * CYC_PER_FP64_VALU / (CLOCK_GHZ * 1e6)) if valu else None
+    floor_ms = (samples_per_chain * valu * CYC_PER_FP64_VALU / (clock_ghz * 1e6)) if valu else None
     roof = {
         "bound": "fp64", "achieved": achieved_tf, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
         "frac": (achieved_tf / FP64_PEAK_TFLOPS) if achieved_tf else None, "traffic": traffic,
@@ -424,7 +432,8 @@ def measure_gpu(wname, streams, frames, steps, warmup, e2e_steps, dev, local_dev
         "hbm": {"achieved": hbm_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": (hbm_gbs / HBM_PEAK_GBS) if hbm_gbs else None,
                 "alg_bytes_per_frame": W["bytes"], "traffic_source": pmc_file.name if (traffic and pmc_file) else None},
-        "issue_bound": {"valu_per_sample": valu, "cycles_per_valu": CYC_PER_FP64_VALU, "clock_ghz": CLOCK_GHZ,
+        "issue_bound": {"valu_per_sample": valu, "cycles_per_valu": CYC_PER_FP64_VALU, "clock_ghz": clock_ghz,
+                        "clock_source": clock_src,
                         "floor_ms_per_launch": floor_ms,
                         "frac": (floor_ms / (k1_avg_s * 1e3)) if (k1_avg_s and floor_ms) else None},
         "note": f"serial IIR recurrence: {chains_per_stream * S} DF-II chains per GPU, each a dependent "

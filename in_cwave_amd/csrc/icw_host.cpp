@@ -14,7 +14,8 @@
 #include <string.h>
 
 #include <algorithm>
-#include <deque>
+#include <list>
+#include <map>
 #include <mutex>
 #include <new>
 #include <vector>
@@ -425,13 +426,24 @@ hipError_t quiesce(icw_ctx *c)
     return hipDeviceSynchronize();
 }
 
-/* The CU-masked stream sets live for the process, shared by every context of a device: measured,
- * a second context's own masked streams did not keep K1 off the other kernels' CUs (C3 K1 3.1 ->
- * 4.7 ms per launch in any context after the first of a process, C2 2.8 -> 4.1), while one set
- * created once and reused keeps the partition.  Sharing only adds ordering between contexts that
- * run on the same device at the same time. */
+/* The CU-masked stream sets are shared by the contexts of a device (created on first use, destroyed
+ * with the device's last context), so a process that opens many contexts does not multiply queues.
+ * Sharing only adds ordering between contexts that run on the same device at the same time. */
 std::mutex g_split_mu;
-std::deque<std::pair<int, CuSplit>> g_splits;    /* deque: entries never move */
+std::list<std::pair<int, CuSplit>> g_splits;     /* list: entries never move */
+std::map<int, int> g_live;                       /* device -> live contexts */
+
+void split_ref(int device, int delta)
+{
+    std::lock_guard<std::mutex> lk(g_split_mu);
+    if ((g_live[device] += delta) > 0) return;
+    for (auto it = g_splits.begin(); it != g_splits.end();) {
+        if (it->first != device) { ++it; continue; }
+        for (hipStream_t q : {it->second.k1, it->second.rest, it->second.dith, it->second.render})
+            if (q) hipStreamDestroy(q);
+        it = g_splits.erase(it);
+    }
+}
 
 const CuSplit *cu_split(icw_ctx *c, int k1_cus)
 {
@@ -644,6 +656,7 @@ int icw_create(const icw_config *cfg, const icw_node *nodes, int n_nodes, int n_
     }
     rc = icw_stream_init(c, 0, n_streams);
     if (rc) { free_all(c); delete c; return rc; }
+    split_ref(c->device, +1);
     *out = c;
     return ICW_OK;
 }
@@ -654,6 +667,7 @@ int icw_destroy(icw_ctx *c)
     set_dev(c);
     quiesce(c);
     free_all(c);
+    split_ref(c->device, -1);
     delete c;
     return ICW_OK;
 }
