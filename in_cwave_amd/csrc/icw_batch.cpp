@@ -210,17 +210,17 @@ int run_group(const icw_config &cfg0, const icw_node *nodes, int n_nodes, std::v
     hipStream_t cs = nullptr, ks = nullptr;
     hipEvent_t h2d[2] = {nullptr, nullptr}, comp[2] = {nullptr, nullptr}, d2h[2] = {nullptr, nullptr};
     auto cleanup = [&]() {
-        if (cs) hipStreamSynchronize(cs);
-        if (ks) hipStreamSynchronize(ks);
+        if (cs) (void)hipStreamSynchronize(cs);
+        if (ks) (void)hipStreamSynchronize(ks);
         for (int p = 0; p < 2; ++p) {
-            if (hin[p]) hipHostFree(hin[p]);
-            if (hout[p]) hipHostFree(hout[p]);
-            if (din[p]) hipFree(din[p]);
-            if (dout[p]) hipFree(dout[p]);
-            for (hipEvent_t e : {h2d[p], comp[p], d2h[p]}) if (e) hipEventDestroy(e);
+            if (hin[p]) (void)hipHostFree(hin[p]);
+            if (hout[p]) (void)hipHostFree(hout[p]);
+            if (din[p]) (void)hipFree(din[p]);
+            if (dout[p]) (void)hipFree(dout[p]);
+            for (hipEvent_t e : {h2d[p], comp[p], d2h[p]}) if (e) (void)hipEventDestroy(e);
         }
-        if (cs) hipStreamDestroy(cs);
-        if (ks) hipStreamDestroy(ks);
+        if (cs) (void)hipStreamDestroy(cs);
+        if (ks) (void)hipStreamDestroy(ks);
     };
     bool ok = true;
     for (int p = 0; p < 2 && ok; ++p) {

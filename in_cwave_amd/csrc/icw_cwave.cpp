@@ -136,7 +136,7 @@ int icw_crc32_batch(const void *base, const uint64_t *offsets, const uint64_t *l
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess) return ICW_EDEVICE;
     int n_cu = 256;
-    hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev);
+    if (hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) n_cu = 256;
     hipStream_t st = (hipStream_t)hip_stream;
     const bool devp = flags & ICW_F_DEVICE_PTRS;
 
@@ -163,7 +163,7 @@ int icw_crc32_batch(const void *base, const uint64_t *offsets, const uint64_t *l
         for (int i = 0; i < n; ++i)
             if (lengths[i] && hipMemcpyAsync(stage + start[i], (const unsigned char *)base + offsets[i], lengths[i],
                                              hipMemcpyHostToDevice, st) != hipSuccess) {
-                hipFree(stage);
+                (void)hipFree(stage);
                 return ICW_EDEVICE;
             }
         dbase = stage;
@@ -216,8 +216,8 @@ int icw_crc32_batch(const void *base, const uint64_t *offsets, const uint64_t *l
     if (rc == ICW_OK && (hipMemcpyAsync(raw.data(), blk + raw_off, raw_b, hipMemcpyDeviceToHost, st) != hipSuccess ||
                          hipStreamSynchronize(st) != hipSuccess))
         rc = ICW_EDEVICE;
-    if (blk) hipFree(blk);
-    if (stage) hipFree(stage);
+    if (blk) (void)hipFree(blk);
+    if (stage) (void)hipFree(stage);
     if (rc != ICW_OK) return rc;
     for (int i = 0; i < n; ++i) {
         const uint32_t c0 = crc_in ? crc_in[i] : 0u;

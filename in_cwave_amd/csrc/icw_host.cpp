@@ -404,7 +404,7 @@ void render_consts(const icw_render_cfg &cfg, int is24, IcwRenderK &k)
 int grow(void **p, size_t *cur, size_t need)
 {
     if (*cur >= need) return ICW_OK;
-    if (*p) hipFree(*p);
+    if (*p) (void)hipFree(*p);
     *p = nullptr;
     *cur = 0;
     if (hipMalloc(p, need) != hipSuccess) return ICW_ENOMEM;
@@ -440,7 +440,7 @@ void split_ref(int device, int delta)
     for (auto it = g_splits.begin(); it != g_splits.end();) {
         if (it->first != device) { ++it; continue; }
         for (hipStream_t q : {it->second.k1, it->second.rest, it->second.dith, it->second.render})
-            if (q) hipStreamDestroy(q);
+            if (q) (void)hipStreamDestroy(q);
         it = g_splits.erase(it);
     }
 }
@@ -462,7 +462,7 @@ const CuSplit *cu_split(icw_ctx *c, int k1_cus)
         hipExtStreamCreateWithCUMask(&x.dith, (uint32_t)words, mr.data()) != hipSuccess ||
         hipExtStreamCreateWithCUMask(&x.render, (uint32_t)words, mr.data()) != hipSuccess) {
         for (hipStream_t q : {x.k1, x.rest, x.dith, x.render})
-            if (q) hipStreamDestroy(q);
+            if (q) (void)hipStreamDestroy(q);
         return nullptr;
     }
     g_splits.emplace_back(c->device, x);
@@ -475,21 +475,21 @@ void free_all(icw_ctx *c)
     void *ptrs[] = {s.mt, s.mt_idx, s.rs, s.lr_equal, s.fes, s.err, s.hist, s.sncnt, s.hq_phase, s.pos, s.fade,
                     s.n_frame, s.bus, s.clips, s.peak_bits, c->d_prog, c->trig, c->d_in, c->d_out, c->d_pre};
     for (void *p : ptrs)
-        if (p) hipFree(p);
+        if (p) (void)hipFree(p);
     for (int p = 0; p < kSets; ++p) {
         for (void *q : {(void *)c->info_dup[p], (void *)c->w[p], (void *)c->xd[p], (void *)c->dith[p],
                         (void *)c->rpre[p], (void *)c->iq[p]})
-            if (q) hipFree(q);
+            if (q) (void)hipFree(q);
         for (hipEvent_t e : {c->ditdone[p], c->k1done[p], c->k2done[p], c->k0done[p], c->k3done[p]})
-            if (e) hipEventDestroy(e);
+            if (e) (void)hipEventDestroy(e);
     }
-    if (c->h_stage) hipHostFree(c->h_stage);
-    if (c->stream3) hipStreamDestroy(c->stream3);
-    if (c->stream4) hipStreamDestroy(c->stream4);
-    if (c->join) hipEventDestroy(c->join);
-    if (c->stream2) hipStreamDestroy(c->stream2);
-    for (auto e : c->ev) hipEventDestroy(e);
-    if (c->stream) hipStreamDestroy(c->stream);
+    if (c->h_stage) (void)hipHostFree(c->h_stage);
+    if (c->stream3) (void)hipStreamDestroy(c->stream3);
+    if (c->stream4) (void)hipStreamDestroy(c->stream4);
+    if (c->join) (void)hipEventDestroy(c->join);
+    if (c->stream2) (void)hipStreamDestroy(c->stream2);
+    for (auto e : c->ev) (void)hipEventDestroy(e);
+    if (c->stream) (void)hipStreamDestroy(c->stream);
 }
 
 }  // namespace
@@ -665,7 +665,7 @@ int icw_destroy(icw_ctx *c)
 {
     if (!c) return ICW_EINVAL;
     set_dev(c);
-    quiesce(c);
+    (void)quiesce(c);
     free_all(c);
     split_ref(c->device, -1);
     delete c;
@@ -834,7 +834,7 @@ int icw_process_streams(icw_ctx *c, int first, int count, const void *in, size_t
     const bool pinned = !dev && stage_in + stage_out + 16 <= kPinnedStage;
     if (pinned) {
         if (c->h_stage_bytes < stage_in + stage_out + 16) {
-            if (c->h_stage) hipHostFree(c->h_stage);
+            if (c->h_stage) (void)hipHostFree(c->h_stage);
             c->h_stage = nullptr;
             c->h_stage_bytes = 0;
             if (hipHostMalloc((void **)&c->h_stage, kPinnedStage, hipHostMallocDefault) != hipSuccess) return ICW_ENOMEM;
@@ -1028,20 +1028,20 @@ int icw_process_streams(icw_ctx *c, int first, int count, const void *in, size_t
             /* K0(b) done, and K2(b-2), the last reader of w[p] / info_dup[p] */
             if (sK != sA && hipStreamWaitEvent(sK, c->k0done[p], 0) != hipSuccess) return ICW_EDEVICE;
             if (b >= n_sets && sK != sA && hipStreamWaitEvent(sK, c->k2done[p], 0) != hipSuccess) return ICW_EDEVICE;
-            if (timing) hipEventRecord(c->ev[4 * b], sK);
+            if (timing && hipEventRecord(c->ev[4 * b], sK) != hipSuccess) return ICW_EDEVICE;
             const hipError_t e1 = k1_mode == ICW_K1_FC ? icw_launch_iir_fc(&a1, N, cfg.iir_kahan, cfg.iir_subnorm_reject, sK)
                                 : k1_mode == 3 ? icw_launch_iir_row(&a1, N, cfg.iir_kahan, cfg.iir_subnorm_reject, sK)
                                                : icw_launch_iir_state(&a1, N, cfg.iir_kahan, cfg.iir_subnorm_reject, sK);
             if (e1 != hipSuccess) return ICW_EDEVICE;
-            if (timing) hipEventRecord(c->ev[4 * b + 1], sK);
+            if (timing && hipEventRecord(c->ev[4 * b + 1], sK) != hipSuccess) return ICW_EDEVICE;
             if (hipEventRecord(c->k1done[p], sK) != hipSuccess) return ICW_EDEVICE;
             if (sK != sA && hipStreamWaitEvent(sA, c->k1done[p], 0) != hipSuccess) return ICW_EDEVICE;
             /* real input: K0(b + n_sets) reuses xd[p], which K1(b) read; queued before K2(b) it
              * runs beside K1(b+1) instead of between two recurrences */
             if (b + n_sets < n_blocks && (rc0 = launch_k0(b + n_sets)) != ICW_OK) return rc0;
         } else if (timing) {
-            hipEventRecord(c->ev[4 * b], sA);
-            hipEventRecord(c->ev[4 * b + 1], sA);
+            if (hipEventRecord(c->ev[4 * b], sA) != hipSuccess || hipEventRecord(c->ev[4 * b + 1], sA) != hipSuccess)
+                return ICW_EDEVICE;
         }
 
         /* the drain: K2 of the last block on the unmasked stream, after K1 of the block and K2 of
@@ -1113,7 +1113,7 @@ int icw_process_streams(icw_ctx *c, int first, int count, const void *in, size_t
         /* rpre[p] / iq[p] were last read by the serial render of block b - n_sets (on sR) */
         if (c->serial_render && b >= n_sets && sR != s2 && hipStreamWaitEvent(s2, c->k3done[p], 0) != hipSuccess)
             return ICW_EDEVICE;
-        if (timing) hipEventRecord(c->ev[4 * b + 2], s2);
+        if (timing && hipEventRecord(c->ev[4 * b + 2], s2) != hipSuccess) return ICW_EDEVICE;
         if (icw_launch_output(&a2, N, cfg.iir_kahan, s2) != hipSuccess) return ICW_EDEVICE;
         if (hipEventRecord(c->k2done[p], s2) != hipSuccess) return ICW_EDEVICE;
         /* the serial part (K4, K3b) on sR after K2(b): it then overlaps K2(b+1) instead of
@@ -1168,7 +1168,7 @@ int icw_process_streams(icw_ctx *c, int first, int count, const void *in, size_t
             if (icw_launch_render(&a3, sR) != hipSuccess) return ICW_EDEVICE;
             if (hipEventRecord(c->k3done[p], sR) != hipSuccess) return ICW_EDEVICE;
         }
-        if (timing) hipEventRecord(c->ev[4 * b + 3], c->serial_render ? sR : s2);
+        if (timing && hipEventRecord(c->ev[4 * b + 3], c->serial_render ? sR : s2) != hipSuccess) return ICW_EDEVICE;
         /* complex input: K0(b + n_sets) reuses xd[p], which K2(b) read */
         if (cw && b + n_sets < n_blocks && (rc0 = launch_k0(b + n_sets)) != ICW_OK) return rc0;
     }
@@ -1221,8 +1221,9 @@ int icw_process_streams(icw_ctx *c, int first, int count, const void *in, size_t
         double m1 = 0, m2 = 0;
         for (int b = 0; b < n_blocks; ++b) {
             float x = 0, y = 0;
-            hipEventElapsedTime(&x, c->ev[4 * b], c->ev[4 * b + 1]);
-            hipEventElapsedTime(&y, c->ev[4 * b + 2], c->ev[4 * b + 3]);
+            if (hipEventElapsedTime(&x, c->ev[4 * b], c->ev[4 * b + 1]) != hipSuccess ||
+                hipEventElapsedTime(&y, c->ev[4 * b + 2], c->ev[4 * b + 3]) != hipSuccess)
+                return ICW_EDEVICE;
             m1 += x;
             m2 += y;
         }

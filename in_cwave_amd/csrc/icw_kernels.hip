@@ -144,10 +144,11 @@ __global__ __launch_bounds__(256) void icw_unpack_frames(IcwK0Args a)
     const int nchw = a.dedup ? 1 : 2;          /* mono dedup: K1 reads the left rows only */
 #pragma unroll
     for (int ch = 0; ch < 2; ++ch) {
-        if (ch >= nchw) break;
-        const unsigned k = (a.hq_phase[s * 2 + ch] + (unsigned)(a.t0 + t)) & 3u;
-        xs[(size_t)(ch * 2 + 0) * a.x_pitch] = icw_filter_in(v[ch], k);
-        xs[(size_t)(ch * 2 + 1) * a.x_pitch] = icw_filter_in(v[ch], (k + 1u) & 3u);
+        if (ch < nchw) {
+            const unsigned k = (a.hq_phase[s * 2 + ch] + (unsigned)(a.t0 + t)) & 3u;
+            xs[(size_t)(ch * 2 + 0) * a.x_pitch] = icw_filter_in(v[ch], k);
+            xs[(size_t)(ch * 2 + 1) * a.x_pitch] = icw_filter_in(v[ch], (k + 1u) & 3u);
+        }
     }
 }
 
