@@ -58,7 +58,7 @@ CLOCK_GHZ = 2.31
 # ~5.0 cycles, dependent or not (profiles/r01_fp64_bank_probe.txt).  icw_iir_state<19> issues 91
 # FP64 VALU per sample (zero-input steps included), icw_iir_row<19> 75.5 (products lane-parallel,
 # the Kahan steps through v_fmac_f64_dpp row_newbcast).
-K1_VALU_PER_SAMPLE = {0: 91, 3: 75.5}          # by ICW_K1_* (icw_last_k1_kernel)
+K1_VALU_PER_SAMPLE = {0: 91.1, 3: 75.6}        # by ICW_K1_* (icw_last_k1_kernel); ISA: 3461 / 2874 VALU per 38-sample pair
 K1_KERNEL_NAME = {0: "icw_iir_state", 3: "icw_iir_row", 4: "icw_iir_state_fc"}
 CYC_PER_FP64_VALU = 5.0
 

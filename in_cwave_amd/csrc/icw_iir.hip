@@ -30,12 +30,33 @@ __device__ unsigned long long icw_stamps[8][1024];
 #endif
 
 /* ------------------------------------------------------------ IIR state kernel (K1) ----- */
+/* mn = min(mn, |s|) in one instruction: v_min_f64 with the abs modifier (the fmin builtin adds a
+ * NaN-quieting v_max_f64 per operand in IEEE mode).  A NaN s leaves mn unchanged, as it leaves the
+ * reference's `fabs(sum) < 1` false. */
+__device__ __forceinline__ double icw_minabs(double m, double s)
+{
+    double r;
+    asm("v_min_f64 %0, %1, |%2|" : "=v"(r) : "v"(m), "v"(s));
+    return r;
+}
+
+/* the same, volatile: K1r keeps it in program order among its volatile term chains (placed freely
+ * there, the scheduler's choices pushed the kernel past 256 VGPRs) -- and K1 must not use this one:
+ * memory operations do not move across a volatile asm, so the mins dragged K1's look-ahead loads
+ * to the end of each block, and block 2 waited on them (C4 K1 3.18 -> 3.29 ms per launch) */
+__device__ __forceinline__ double icw_minabs_v(double m, double s)
+{
+    double r;
+    asm volatile("v_min_f64 %0, %1, |%2|" : "=v"(r) : "v"(m), "v"(s));
+    return r;
+}
+
 /* One unrolled step of the loop-back sum for sample J of an N-block.  The delay line lives in
  * R[]: at step J the logical z_i (i = 0 most recent) is R[(J-1-i) mod N]; the new w is written
  * to R[J], overwriting the oldest value.  All indices are compile-time constants. */
-template <int N, bool KAHAN, bool SUBN, int J>
+template <int N, bool KAHAN, bool SUBN, int J, bool SPEC = false>
 __device__ __forceinline__ void icw_iir_step(double (&R)[N], double xin, const double (&pc)[20],
-                                             unsigned &cnt)
+                                             unsigned &cnt, double *mn = nullptr)
 {
     double S;
     if (KAHAN) {
@@ -55,7 +76,9 @@ __device__ __forceinline__ void icw_iir_step(double (&R)[N], double xin, const d
 #pragma unroll
         for (int i = 0; i < N; ++i) S += R[(J - 1 - i + 2 * N) % N] * pc[i];
     }
-    if (SUBN) {
+    if constexpr (SPEC) {
+        *mn = icw_minabs(*mn, S);                /* the reject speculated away ("Speculative blocks") */
+    } else if (SUBN) {
         /* fabs(sum) < is_subnorm_reject, a BOOL == 1 -> threshold 1.0 (hblpf.c:915, 1046) */
         const bool z = fabs(S) < 1.0;
         cnt += z ? 1u : 0u;
@@ -108,14 +131,22 @@ __device__ __forceinline__ void icw_block_steps(double (&R)[N], const double (&x
 
 /* full block of N steps; after step J consumes xv[J], refill it with the input N samples ahead
  * (rows are padded by >= N doubles, so the last block's look-ahead loads stay in bounds) */
-template <int N, int J0, bool KAHAN, bool SUBN>
+/* Before a loop over blocks: wait for every outstanding global access, once.  The loop's first
+ * iteration can be entered straight from a block whose last look-ahead loads were just issued; the
+ * waitcnt pass then sizes the in-loop waits for that path (vmcnt(0)-(2) a few steps in) and every
+ * iteration pays them, waiting on the previous block's stores -- in K1 those are 10 stores over
+ * 64 rows each (C4: K1 3.18 -> 3.29-3.40 ms per launch).  Drained here, the loop's waits follow
+ * the steady state (vmcnt(19) down to (10)). */
+#define ICW_DRAIN_VMEM() __builtin_amdgcn_s_waitcnt(0x0F70)   /* vmcnt(0), expcnt / lgkmcnt free */
+
+template <int N, int J0, bool KAHAN, bool SUBN, bool SPEC = false>
 __device__ __forceinline__ void icw_block_steps_pf(double (&R)[N], double (&xv)[N], const double *xnext,
-                                                   const double (&pc)[20], unsigned &cnt)
+                                                   const double (&pc)[20], unsigned &cnt, double *mn = nullptr)
 {
     if constexpr (J0 < N) {
-        icw_iir_step<N, KAHAN, SUBN, J0>(R, xv[J0], pc, cnt);
+        icw_iir_step<N, KAHAN, SUBN, J0, SPEC>(R, xv[J0], pc, cnt, mn);
         xv[J0] = xnext[J0];
-        icw_block_steps_pf<N, J0 + 1, KAHAN, SUBN>(R, xv, xnext, pc, cnt);
+        icw_block_steps_pf<N, J0 + 1, KAHAN, SUBN, SPEC>(R, xv, xnext, pc, cnt, mn);
     }
 }
 
@@ -127,8 +158,9 @@ __device__ __forceinline__ void icw_block_steps_pf(double (&R)[N], double (&xv)[
  * reference only in the sign of a zero (t0 = -0 gives T = +0); a zero's sign is absorbed by the
  * first nonzero term, and a sum that stays zero is rejected to +0.0 (|S| < 1, hblpf.c:1046), so
  * w is bit-identical.  (With the reject off the sign would survive: that mode takes icw_iir_step.) */
-template <int N, int J>
-__device__ __forceinline__ void icw_iir_step_z(double (&R)[N], const double (&pc)[20], unsigned &cnt)
+template <int N, int J, bool SPEC = false>
+__device__ __forceinline__ void icw_iir_step_z(double (&R)[N], const double (&pc)[20], unsigned &cnt,
+                                               double *mn = nullptr)
 {
     double S = R[(J - 1 + N) % N] * pc[0];
     double C, Y, T;
@@ -139,27 +171,31 @@ __device__ __forceinline__ void icw_iir_step_z(double (&R)[N], const double (&pc
         const double ti = R[(J - 1 - i + 2 * N) % N] * pc[i];
         Y = ti - C; T = S + Y; C = (T - S) - Y; S = T;
     }
-    const bool z = fabs(S) < 1.0;
-    cnt += z ? 1u : 0u;
-    S = z ? 0.0 : S;
+    if constexpr (SPEC) {
+        *mn = icw_minabs(*mn, S);
+    } else {
+        const bool z = fabs(S) < 1.0;
+        cnt += z ? 1u : 0u;
+        S = z ? 0.0 : S;
+    }
     R[J] = S;
 }
 
 /* A block of N steps whose input is zero at the steps J with (J & 1) == Z.  The next block's
  * zero steps are the other parity (N is odd), so the look-ahead refill of xv[J] is needed exactly
  * where this block's step J had a zero input. */
-template <int N, int J0, int Z, bool SUBN>
+template <int N, int J0, int Z, bool SUBN, bool SPEC = false>
 __device__ __forceinline__ void icw_block_steps_zpf(double (&R)[N], double (&xv)[N], const double *xnext,
-                                                    const double (&pc)[20], unsigned &cnt)
+                                                    const double (&pc)[20], unsigned &cnt, double *mn = nullptr)
 {
     if constexpr (J0 < N) {
         if constexpr ((J0 & 1) == Z) {
-            icw_iir_step_z<N, J0>(R, pc, cnt);
+            icw_iir_step_z<N, J0, SPEC>(R, pc, cnt, mn);
             xv[J0] = xnext[J0];
         } else {
-            icw_iir_step<N, true, SUBN, J0>(R, xv[J0], pc, cnt);
+            icw_iir_step<N, true, SUBN, J0, SPEC>(R, xv[J0], pc, cnt, mn);
         }
-        icw_block_steps_zpf<N, J0 + 1, Z, SUBN>(R, xv, xnext, pc, cnt);
+        icw_block_steps_zpf<N, J0 + 1, Z, SUBN, SPEC>(R, xv, xnext, pc, cnt, mn);
     }
 }
 
@@ -170,6 +206,23 @@ __device__ __forceinline__ void icw_load_x(double (&xv)[N], const double *xp)
     for (int j = 0; j < N; ++j) xv[j] = xp[j];
 }
 
+/* a block's w values to its row: after a full block R[j] is the block's sample j */
+template <int N>
+__device__ __forceinline__ void icw_store_block(const double (&R)[N], double *wo)
+{
+#pragma unroll
+    for (int j = 0; j < N; ++j) wo[j] = R[j];
+}
+
+/* Speculative blocks (icw_iir_state, icw_iir_row): the loop-back sums run without the
+ * reject's compare-and-select (hblpf.c:1046), i.e. w = S, which is exact unless some |S| < 1.  The
+ * smallest |S| is checked once per loop iteration (a pair of blocks for odd orders); if any chain
+ * of the wave fell below 1, the wave drops the iteration and runs the rest of the launch with the
+ * exact steps, starting from the iteration's start state: the ring is the N w values just before
+ * it, which the w row already holds, and the inputs are reloaded.  (Silence rejects every sample; a wave that meets it runs at the
+ * exact kernel's speed.)  Only the zero-input loops speculate.  The exact loops follow the
+ * speculative one instead of sharing a loop with it: one loop nest with both made the register
+ * allocator keep ~80 more VGPRs live and spill to AGPRs (accvgpr moves cost VALU slots). */
 /* Lane layout: a group of 128 lanes (two waves) covers 32 streams (64 with the mono dedup); wave
  * f of the group holds filter f (0: I, 1: Q) of every channel, lane l = stream (l >> 1), channel
  * (l & 1) -- or stream l, left channel, under the dedup.  A wave's chains then share the phase
@@ -216,36 +269,64 @@ __global__ __launch_bounds__(256) void icw_iir_state(IcwK1Args a)
          * with no register copies */
         double xv[N];
         icw_load_x<N>(xv, xp);
+        bool zfast = false;
+        unsigned phi0 = 0;
         if constexpr (KAHAN && SUBN && (N & 1)) {
             /* block-relative sample n has a zero input iff (phi + n) is odd (I: k = hq + t0 + n odd;
              * Q: k + 1 odd); the fast path needs one parity across the wave */
             const unsigned phi = (a.hq_phase[s * 2 + ch] + (unsigned)a.t0 + (unsigned)f) & 1u;
-            const unsigned phi0 = __builtin_amdgcn_readfirstlane(phi);
-            if (__all(phi == phi0) && T >= 3 * N) {
-                if (phi0) {   /* align: pairs start on a nonzero sample */
+            phi0 = __builtin_amdgcn_readfirstlane(phi);
+            zfast = __all(phi == phi0) && T >= 3 * N;
+        }
+        if constexpr (KAHAN && SUBN && (N & 1)) {
+            if (zfast) {
+                /* speculative pairs of blocks ("Speculative blocks") that start on a nonzero sample; a
+                 * failed block ends them and the exact loops below take over at its start */
+                if ((phi0 + (unsigned)t) & 1u) {
                     icw_block_steps_pf<N, 0, KAHAN, SUBN>(R, xv, xp + t + N, pc, cnt);
-                    double *wo = wrow + N + t;
-#pragma unroll
-                    for (int j = 0; j < N; ++j) wo[j] = R[j];
+                    icw_store_block<N>(R, wrow + N + t);
                     t += N;
                 }
-                for (; t + 2 * N <= T; t += 2 * N) {
-                    icw_block_steps_zpf<N, 0, 1, SUBN>(R, xv, xp + t + N, pc, cnt);
-                    double *wo = wrow + N + t;
-#pragma unroll
-                    for (int j = 0; j < N; ++j) wo[j] = R[j];
-                    icw_block_steps_zpf<N, 0, 0, SUBN>(R, xv, xp + t + 2 * N, pc, cnt);
-#pragma unroll
-                    for (int j = 0; j < N; ++j) wo[N + j] = R[j];
+                double mn = __builtin_inf();       /* smallest |sum| of the speculative block */
+                bool fail = false;
+                ICW_DRAIN_VMEM();
+                while (!fail && t + 2 * N <= T) {
+                    /* a failed pair's stores land past [t, t + N), the restart state, and the
+                     * exact re-run overwrites them */
+                    icw_block_steps_zpf<N, 0, 1, SUBN, true>(R, xv, xp + t + N, pc, cnt, &mn);
+                    icw_store_block<N>(R, wrow + N + t);
+                    icw_block_steps_zpf<N, 0, 0, SUBN, true>(R, xv, xp + t + 2 * N, pc, cnt, &mn);
+                    icw_store_block<N>(R, wrow + 2 * N + t);
+                    fail = __any(mn < 1.0);
+                    if (!fail) t += 2 * N;
                 }
-                icw_load_x<N>(xv, xp + t);   /* the zero steps left half of xv unloaded */
+                if (fail) {
+                    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+#pragma unroll
+                    for (int j = 0; j < N; ++j) R[j] = wrow[t + j];
+                }
+                icw_load_x<N>(xv, xp + t);   /* the block's inputs (the zero steps left slots unloaded) */
+                if (fail) {
+                    /* exact from here: the same zero-input pairs with the reject */
+                    ICW_DRAIN_VMEM();
+                    if (((phi0 + (unsigned)t) & 1u) && t + N <= T) {
+                        icw_block_steps_pf<N, 0, KAHAN, SUBN>(R, xv, xp + t + N, pc, cnt);
+                        icw_store_block<N>(R, wrow + N + t);
+                        t += N;
+                    }
+                    for (; t + 2 * N <= T; t += 2 * N) {
+                        icw_block_steps_zpf<N, 0, 1, SUBN>(R, xv, xp + t + N, pc, cnt);
+                        icw_store_block<N>(R, wrow + N + t);
+                        icw_block_steps_zpf<N, 0, 0, SUBN>(R, xv, xp + t + 2 * N, pc, cnt);
+                        icw_store_block<N>(R, wrow + 2 * N + t);
+                    }
+                    icw_load_x<N>(xv, xp + t);
+                }
             }
         }
         for (; t + N <= T; t += N) {
             icw_block_steps_pf<N, 0, KAHAN, SUBN>(R, xv, xp + t + N, pc, cnt);
-            double *wo = wrow + N + t;
-#pragma unroll
-            for (int j = 0; j < N; ++j) wo[j] = R[j];
+            icw_store_block<N>(R, wrow + N + t);
         }
     }
     const int rem = T - t;
@@ -385,11 +466,14 @@ struct IcwRowC {
     double one;         /* 1.0 in a VGPR (VOP2 src1) */
 };
 
+
 /* one sample at unroll step J; zero-input step when Z != 2 and (J & 1) == Z.  Logical z_i =
- * W[(J-1-i) mod N] (row-uniform); the new w goes to W[J] and its products to P[J] / P2[J]. */
-template <int N, int J, int Z>
+ * W[(J-1-i) mod N] (row-uniform); the new w goes to W[J] and its products to P[J] / P2[J].
+ * SPEC: the reject (hblpf.c:1046) is speculated away -- w = S unconditionally, and mn tracks the
+ * smallest |S| so the block can be re-run exactly if any sum fell below 1 ("Speculative blocks"). */
+template <int N, int J, int Z, bool SPEC>
 __device__ __forceinline__ void icw_row_step(double (&W)[N], double (&P)[N], double (&P2)[N], double xin,
-                                             const IcwRowC &c)
+                                             const IcwRowC &c, double &mn)
 {
     constexpr bool ZS = Z != 2 && (J & 1) == Z;
     double S, Y;
@@ -405,7 +489,8 @@ __device__ __forceinline__ void icw_row_step(double (&W)[N], double (&P)[N], dou
     double NC = Y - (T - S);
     /* terms I0..N-1: Y = t_i - C with t_i = lane i-1 of P (i-17 of P2), one asm block */
     S = icw_row_chain<N, ZS ? 2 : 1, J>(T, NC, c.one, P, P2);
-    S = fabs(S) < 1.0 ? 0.0 : S;               /* hblpf.c:1046 */
+    if constexpr (SPEC) mn = icw_minabs_v(mn, S);
+    else S = fabs(S) < 1.0 ? 0.0 : S;          /* hblpf.c:1046 */
     W[J] = S;
     P[J] = icw_vmul(c.pl, S);
     if constexpr (N > 17) P2[J] = icw_vmul(c.pl2, S);
@@ -413,14 +498,14 @@ __device__ __forceinline__ void icw_row_step(double (&W)[N], double (&P)[N], dou
 
 /* a block of N samples; xv[J] is refilled with the input N samples ahead right after step J when
  * the next block's step J (zero parity ZN) consumes an input */
-template <int N, int J, int Z, int ZN>
+template <int N, int J, int Z, int ZN, bool SPEC>
 __device__ __forceinline__ void icw_row_block(double (&W)[N], double (&P)[N], double (&P2)[N], double (&xv)[N],
-                                              const double *xnext, const IcwRowC &c)
+                                              const double *xnext, const IcwRowC &c, double &mn)
 {
     if constexpr (J < N) {
-        icw_row_step<N, J, Z>(W, P, P2, xv[J], c);
+        icw_row_step<N, J, Z, SPEC>(W, P, P2, xv[J], c, mn);
         if constexpr (!(ZN != 2 && (J & 1) == ZN)) xv[J] = xnext[J];
-        icw_row_block<N, J + 1, Z, ZN>(W, P, P2, xv, xnext, c);
+        icw_row_block<N, J + 1, Z, ZN, SPEC>(W, P, P2, xv, xnext, c, mn);
     }
 }
 
@@ -430,7 +515,8 @@ __device__ __forceinline__ void icw_row_block_lim(double (&W)[N], double (&P)[N]
 {
     if constexpr (J < N) {
         if (J < lim) {
-            icw_row_step<N, J, 2>(W, P, P2, xv[J], c);
+            double mn;
+            icw_row_step<N, J, 2, false>(W, P, P2, xv[J], c, mn);
             icw_row_block_lim<N, J + 1>(W, P, P2, xv, c, lim);
         }
     }
@@ -443,6 +529,33 @@ __device__ __forceinline__ void icw_row_store(const double (&W)[N], double *wo, 
 #pragma unroll
         for (int j = 0; j < N; ++j) wo[j] = W[j];
     }
+}
+
+/* the lane-parallel products of the whole ring: P[k] = c[l+1] * W[k], P2[k] = c[l+17] * W[k] */
+template <int N>
+__device__ __forceinline__ void icw_row_products(const double (&W)[N], double (&P)[N], double (&P2)[N],
+                                                 const IcwRowC &c)
+{
+    if constexpr (N > 17) {
+#pragma unroll
+        for (int k = 0; k < N; ++k) P2[k] = icw_vmul(c.pl2, W[k]);
+    }
+#pragma unroll
+    for (int k = 0; k < N; ++k) P[k] = icw_vmul(c.pl, W[k]);
+    asm volatile("s_nop 1");   /* VALU write -> DPP read of P / P2 */
+}
+
+/* after a failed speculative block at t: the ring from the w row, its products, the block's inputs */
+template <int N>
+__device__ __forceinline__ void icw_row_restart(double (&W)[N], double (&P)[N], double (&P2)[N], double (&xv)[N],
+                                                const double *xp, const double *wrow, int t, const IcwRowC &c)
+{
+    /* the writer lane stored the row [t, t + N): block start or the previous block */
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+#pragma unroll
+    for (int j = 0; j < N; ++j) W[j] = wrow[t + j];
+    icw_row_products<N>(W, P, P2, c);
+    icw_load_x<N>(xv, xp + t);
 }
 
 /* Row layout: wave v holds filter f = v & 1 of the four chain slots 4 (v >> 1) + r, r = row;
@@ -472,13 +585,7 @@ __global__ __launch_bounds__(256) void icw_iir_row(IcwK1Args a)
     double W[N], P[N], P2[N];
 #pragma unroll
     for (int i = 0; i < N; ++i) W[N - 1 - i] = a.hist[(size_t)g * ICW_HIST_PITCH + i];
-    if constexpr (N > 17) {
-#pragma unroll
-        for (int k = 0; k < N; ++k) P2[k] = icw_vmul(c.pl2, W[k]);
-    }
-#pragma unroll
-    for (int k = 0; k < N; ++k) P[k] = icw_vmul(c.pl, W[k]);
-    asm volatile("s_nop 1");
+    icw_row_products<N>(W, P, P2, c);
 
     if (writer && ch == 0) a.info_dup[s * 2 + f] = a.lr_equal[s * 2 + f];
     const double *xp = a.xd + (size_t)g * a.x_pitch;
@@ -493,36 +600,77 @@ __global__ __launch_bounds__(256) void icw_iir_row(IcwK1Args a)
         /* block-relative sample n has a zero input iff (phi + n) is odd (see icw_iir_state) */
         const unsigned phi = (a.hq_phase[s * 2 + ch] + (unsigned)a.t0 + (unsigned)f) & 1u;
         const unsigned phi0 = __builtin_amdgcn_readfirstlane(phi);
-        if (__all(phi == phi0) && T >= 3 * N) {
+        const bool zfast = __all(phi == phi0) && T >= 3 * N;
+        double mn = __builtin_inf();               /* smallest |sum| of the speculative block */
+        bool fail = false;
+        ICW_DRAIN_VMEM();
+        if (zfast) {
+            /* speculative zero-input blocks ("Speculative blocks" above); a failed block ends them
+             * and the exact loops below take over at its start */
             if constexpr (N & 1) {
-                /* odd order: the zero parity alternates block to block */
-                if (phi0) {
-                    icw_row_block<N, 0, 0, 1>(W, P, P2, xv, xp + t + N, c);
+                /* odd order: the zero parity alternates block to block; pairs start on a nonzero
+                 * sample */
+                if ((phi0 + (unsigned)t) & 1u) {
+                    icw_row_block<N, 0, 0, 1, false>(W, P, P2, xv, xp + t + N, c, mn);
                     icw_row_store<N>(W, wrow + N + t, writer);
                     t += N;
                 }
                 for (; t + 2 * N <= T; t += 2 * N) {
-                    icw_row_block<N, 0, 1, 0>(W, P, P2, xv, xp + t + N, c);
+                    /* a failed pair's stores land past [t, t + N), the restart state, and the
+                     * exact re-run overwrites them */
+                    icw_row_block<N, 0, 1, 0, true>(W, P, P2, xv, xp + t + N, c, mn);
                     icw_row_store<N>(W, wrow + N + t, writer);
-                    icw_row_block<N, 0, 0, 1>(W, P, P2, xv, xp + t + 2 * N, c);
+                    icw_row_block<N, 0, 0, 1, true>(W, P, P2, xv, xp + t + 2 * N, c, mn);
                     icw_row_store<N>(W, wrow + 2 * N + t, writer);
+                    if (__any(mn < 1.0)) { fail = true; break; }
                 }
             } else if (phi0) {
                 /* even order: the same zero steps in every block */
                 for (; t + N <= T; t += N) {
-                    icw_row_block<N, 0, 0, 0>(W, P, P2, xv, xp + t + N, c);
+                    icw_row_block<N, 0, 0, 0, true>(W, P, P2, xv, xp + t + N, c, mn);
+                    icw_row_store<N>(W, wrow + N + t, writer);
+                    if (__any(mn < 1.0)) { fail = true; break; }
+                }
+            } else {
+                for (; t + N <= T; t += N) {
+                    icw_row_block<N, 0, 1, 1, true>(W, P, P2, xv, xp + t + N, c, mn);
+                    icw_row_store<N>(W, wrow + N + t, writer);
+                    if (__any(mn < 1.0)) { fail = true; break; }
+                }
+            }
+            if (fail) icw_row_restart<N>(W, P, P2, xv, xp, wrow, t, c);
+            else icw_load_x<N>(xv, xp + t);   /* the zero steps left part of xv unloaded */
+        }
+        if (fail) {
+            /* exact from here: the same zero-input blocks with the reject */
+            ICW_DRAIN_VMEM();
+            if constexpr (N & 1) {
+                if (((phi0 + (unsigned)t) & 1u) && t + N <= T) {
+                    icw_row_block<N, 0, 0, 1, false>(W, P, P2, xv, xp + t + N, c, mn);
+                    icw_row_store<N>(W, wrow + N + t, writer);
+                    t += N;
+                }
+                for (; t + 2 * N <= T; t += 2 * N) {
+                    icw_row_block<N, 0, 1, 0, false>(W, P, P2, xv, xp + t + N, c, mn);
+                    icw_row_store<N>(W, wrow + N + t, writer);
+                    icw_row_block<N, 0, 0, 1, false>(W, P, P2, xv, xp + t + 2 * N, c, mn);
+                    icw_row_store<N>(W, wrow + 2 * N + t, writer);
+                }
+            } else if (phi0) {
+                for (; t + N <= T; t += N) {
+                    icw_row_block<N, 0, 0, 0, false>(W, P, P2, xv, xp + t + N, c, mn);
                     icw_row_store<N>(W, wrow + N + t, writer);
                 }
             } else {
                 for (; t + N <= T; t += N) {
-                    icw_row_block<N, 0, 1, 1>(W, P, P2, xv, xp + t + N, c);
+                    icw_row_block<N, 0, 1, 1, false>(W, P, P2, xv, xp + t + N, c, mn);
                     icw_row_store<N>(W, wrow + N + t, writer);
                 }
             }
-            icw_load_x<N>(xv, xp + t);   /* the zero steps left part of xv unloaded */
+            icw_load_x<N>(xv, xp + t);
         }
         for (; t + N <= T; t += N) {
-            icw_row_block<N, 0, 2, 2>(W, P, P2, xv, xp + t + N, c);
+            icw_row_block<N, 0, 2, 2, false>(W, P, P2, xv, xp + t + N, c, mn);
             icw_row_store<N>(W, wrow + N + t, writer);
         }
     }

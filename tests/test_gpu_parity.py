@@ -85,6 +85,31 @@ def test_all_filters_modes(oracle, icw, htype, kahan, subn):
     assert_parity(out, pre, ro, rp, 2, exact_pre=True)
 
 
+@pytest.mark.parametrize("htype", [1, 2])
+def test_speculative_reject_fallback(oracle, icw, htype):
+    """The zero-input loops of K1 / K1r run without the reject's select and fall back to exact
+    blocks from a failed block's start when some |sum| < 1 (icw_iir.hip, "Speculative blocks").
+    Stream 0 falls silent after 2000 frames: its decaying states dip below 1 now and then from
+    ~50 000 frames on, so speculation fails in the middle of a launch; stream 1 starts silent
+    (every sum rejected) and fails at a launch's first block; streams 2-5 stay speculative in the
+    same waves.  Orders 19 (pairs of blocks) and 18 (one zero parity per block)."""
+    cfg = graph.default_config(48000, hilbert_type=htype)
+    T = 64000
+    raw = synth.batch_pcm(6, T, 48000)
+    x = raw.view(np.int16).reshape(6, T, 2)
+    x[0, 2000:] = 0
+    x[1, :3000] = 0
+    x[4, 30000:30500] = 0
+    ctx, out, pre, ro, rp = run_both(oracle, icw, cfg, graph.graph_master_only(), raw, T)
+    assert_parity(out, pre, ro, rp)
+    sts = [oracle.Stream(cfg, graph.graph_master_only()) for _ in range(2)]
+    for s in range(2):
+        sts[s].process(raw[s], T, want_pre=False)
+        r = sts[s].meters()
+        assert r["desubnorm"] > (2 if s == 0 else 3000)      # the fallback did run
+        assert ctx.meters(s)["desubnorm"] == r["desubnorm"], s
+
+
 @pytest.mark.parametrize("htype", [0, 1, 2, 4])
 def test_block_split_invariance(oracle, icw, htype):
     """state carried across blocks of odd sizes == one pass (and == oracle); orders 15 / 19 / 18 /
