@@ -117,6 +117,15 @@ struct icw_ctx {
     int max_block = kDefBlockFrames;      /* ICW_BLOCK: frames per launch block */
     bool dedup_ok = true;                 /* ICW_DEDUP=0 disables the mono K1 dedup (A/B) */
     int max_sets = 2;                     /* ICW_SETS: block scratch sets (2..kSets) */
+    /* block schedule of long calls (plan_blocks): a short first block (the pipeline fill is K0 of
+     * block 0 alone: C3 +2.5 %, C4 +1.4 %) and an optional geometric tail (the drain is K2 / K3 of
+     * the last block alone).  The tail is off by default: it pays only if K0 + K2 of a block fit
+     * beside K1 of a block r times shorter, and in C3 / C4 they take 0.87 / 0.94 of K1's time per
+     * frame -- r = 0.85 measured C3 -4 %, C4 -8 %, and r >= 0.9 leaves no room for a tail in a
+     * 2^18-frame call.  C5's drain is the serial render's, which a tail does not shorten. */
+    int first_block = 4096;               /* ICW_FIRST_BLOCK (0: uniform blocks) */
+    double taper = 0.0;                   /* ICW_TAPER: tail block ratio (0: no tail) */
+    int taper_min = 1024;                 /* ICW_TAPER_MIN: smallest tail block */
     /* dither generation (K3a) runs on its own stream, double-buffered like the block scratch */
     hipStream_t stream3 = nullptr;
     hipEvent_t ditdone[kSets] = {};
@@ -420,6 +429,44 @@ int grow(void **p, size_t *cur, size_t need)
  * name CUs in every XCD: the K1 mask is bits [0, k1_cus), the rest its complement. */
 /* wait for every kernel and copy of the context (they run on several streams, the caller's among
  * them); host-side state changes and reads happen only between calls */
+/* Launch blocks of one call: (offset, frames) pairs of at most Tb frames.  A block pipeline fills
+ * with K0 of the first block alone and drains with K2 (and the serial render) of the last block
+ * alone, each on the whole chip (sF).  For calls of many blocks both ends are made short:
+ *   - the first block is `first` frames, long enough that K1 of it covers K0 of the next full one;
+ *   - the tail shrinks geometrically (ratio r) down to `tmin`, so that K2 of every tail block, which
+ *     runs beside K1 of the next one, stays no longer than that K1 (C4: K2 ~0.8 K1 per frame).
+ * Block sizes stay multiples of 64 frames; short calls keep uniform blocks. */
+std::vector<std::pair<int, int>> plan_blocks(int n_frames, int Tb, int first, double r, int tmin)
+{
+    std::vector<std::pair<int, int>> bl;
+    std::vector<int> tail;
+    const bool shape = n_frames >= 4 * Tb;
+    if (shape && r > 0.0) {
+        for (double x = Tb * r; x >= tmin; x *= r) tail.push_back(((int)x) & ~63);
+        long sum = 0;
+        for (int v : tail) sum += v;
+        if (sum > n_frames / 2) tail.clear();
+    }
+    int t = 0;
+    if (shape && first >= 64 && first < Tb) {
+        bl.emplace_back(0, first);
+        t = first;
+    }
+    long tail_sum = 0;
+    for (int v : tail) tail_sum += v;
+    const int body_end = n_frames - (int)tail_sum;
+    while (t < body_end) {
+        const int T = std::min(Tb, body_end - t);
+        bl.emplace_back(t, T);
+        t += T;
+    }
+    for (int v : tail) {
+        bl.emplace_back(t, v);
+        t += v;
+    }
+    return bl;
+}
+
 hipError_t quiesce(icw_ctx *c)
 {
     (void)c;
@@ -636,6 +683,12 @@ int icw_create(const icw_config *cfg, const icw_node *nodes, int n_nodes, int n_
         if (bl && atoi(bl) >= 256 && atoi(bl) <= kMaxBlockFrames) c->max_block = atoi(bl);
         const char *ns = getenv("ICW_SETS");
         if (ns && atoi(ns) >= 2 && atoi(ns) <= kSets) c->max_sets = atoi(ns);
+        const char *fb = getenv("ICW_FIRST_BLOCK");
+        if (fb && atoi(fb) >= 0) c->first_block = atoi(fb);
+        const char *tp = getenv("ICW_TAPER");
+        if (tp && atof(tp) >= 0.0 && atof(tp) < 1.0) c->taper = atof(tp);
+        const char *tm = getenv("ICW_TAPER_MIN");
+        if (tm && atoi(tm) >= 64) c->taper_min = atoi(tm);
         const char *dd = getenv("ICW_DEDUP");
         if (dd && !strcmp(dd, "0")) c->dedup_ok = false;
         const char *fd = getenv("ICW_FILL_DRAIN");
@@ -876,7 +929,8 @@ int icw_process_streams(icw_ctx *c, int first, int count, const void *in, size_t
     const int Tb = std::min(n_frames, c->max_block);
     const size_t w_pitch = (size_t)Tb + N + 1;
     const size_t x_pitch = ((size_t)Tb + ICW_MAX_IIR_ORDER + 2) & ~(size_t)1;   /* look-ahead pad */
-    const int n_blocks = (n_frames + Tb - 1) / Tb;
+    const std::vector<std::pair<int, int>> blocks = plan_blocks(n_frames, Tb, c->first_block, c->taper, c->taper_min);
+    const int n_blocks = (int)blocks.size();
     const int n_sets = std::min(n_blocks, c->max_sets);
     for (int p = 0; p < n_sets; ++p) {
         if (grow((void **)&c->w[p], &c->w_bytes[p], S * 4 * w_pitch * sizeof(double))) return ICW_ENOMEM;
@@ -964,7 +1018,7 @@ int icw_process_streams(icw_ctx *c, int first, int count, const void *in, size_t
     /* K0 of block b on sA: xd[p] was last read by K1 of block b-2 (and, complex input, by K2 of
      * block b-2, which precedes it on sA) */
     auto launch_k0 = [&](int b) -> int {
-        const int t0 = b * Tb, T = std::min(Tb, n_frames - t0), p = b % n_sets;
+        const int t0 = blocks[b].first, T = blocks[b].second, p = b % n_sets;
         IcwK0Args a0;
         memset(&a0, 0, sizeof(a0));
         a0.lds_guard = c->k1_lds ? 256u : 0u;
@@ -998,8 +1052,8 @@ int icw_process_streams(icw_ctx *c, int first, int count, const void *in, size_t
     for (int b = 0; b < n_sets; ++b)
         if ((rc0 = launch_k0(b)) != ICW_OK) return rc0;
     for (int b = 0; b < n_blocks; ++b) {
-        const int t0 = b * Tb;
-        const int T = std::min(Tb, n_frames - t0);
+        const int t0 = blocks[b].first;
+        const int T = blocks[b].second;
         const int p = b % n_sets;
 
         if (!cw) {

@@ -132,6 +132,22 @@ def test_launch_blocks_inside_one_call(oracle, icw, htype, monkeypatch):
     assert_parity(out, pre, ro, rp, 2, exact_pre=True)
 
 
+@pytest.mark.parametrize("graph_name", ["shift_master", "pm_shift_mix"])
+def test_block_schedule_first_and_tail(oracle, icw, graph_name, monkeypatch):
+    """a long call's launch blocks: a short first block, full blocks, then a geometric tail of
+    shrinking blocks (plan_blocks in icw_host.cpp), here 640 | 2048 x k | 1728, 1408, ..., 128 --
+    every block offset and size reaches K0 / K1 / K2 / the rotation table like a uniform block"""
+    monkeypatch.setenv("ICW_BLOCK", "2048")
+    monkeypatch.setenv("ICW_FIRST_BLOCK", "640")
+    monkeypatch.setenv("ICW_TAPER", "0.85")
+    monkeypatch.setenv("ICW_TAPER_MIN", "128")
+    cfg = graph.default_config(48000)
+    nodes = getattr(graph, "graph_" + graph_name)()
+    raw = synth.batch_pcm(6, 20011, 48000)
+    _, out, pre, ro, rp = run_both(oracle, icw, cfg, nodes, raw, 20011)
+    assert_parity(out, pre, ro, rp)
+
+
 @pytest.mark.parametrize("fmt", [abi.FMT_U8, abi.FMT_I16, abi.FMT_I24, abi.FMT_I32, abi.FMT_F32])
 @pytest.mark.parametrize("ch", [1, 2])
 def test_input_formats(oracle, icw, fmt, ch):
