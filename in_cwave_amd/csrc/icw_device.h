@@ -157,6 +157,7 @@ struct IcwK3Args {
     double *dith;                  /* [T][dith_pitch] rnd * dth_mul per sample, time-major (K3a -> K3b); null: ROUND */
     size_t dith_pitch;
     uint32_t *fes;                 /* FP_CHECK census, as in IcwK1Args; null: no FC() */
+    int32_t row;                   /* render kernel: 1 row broadcast (K3r, small batches), 0 lane per channel */
 };
 
 /* Arguments of the output kernel (frame-parallel: Kahan output sums, unmix, graph, render). */

@@ -51,6 +51,7 @@ double u2d(unsigned long long u)
 constexpr int kMaxBlockFrames = 1 << 16;
 constexpr int kDefBlockFrames = 1 << 14;   /* launch block: shorter pipeline fill / drain */
 constexpr int kSets = 3;                    /* most block scratch sets (ICW_SETS); default 2 */
+constexpr int kRowRenderMax = 2048;          /* channels up to which the render runs a row per channel */
 constexpr size_t kPinnedStage = 1u << 20;   /* host-pointer calls up to this size stage through pinned memory */
 
 struct DevState {
@@ -161,6 +162,8 @@ struct icw_ctx {
     int k1_mode = -1;         /* K1 variant: -1 auto (row / plain), 0 plain lanes, 3 row broadcast
                                  (ICW_K1_MODE=plain|row, A/B runs) */
     bool dither_lane = false; /* ICW_DITHER=lane: lane-per-channel dither generator (A/B only) */
+    int render_row = -1;      /* serial render kernel: -1 auto (row broadcast for <= kRowRenderMax
+                                 channels), 0 lane per channel, 1 row (ICW_RENDER=serial|row) */
     bool serialize = false;   /* ICW_SERIALIZE=1: every kernel on the caller's stream (profiling) */
     double last_ms[2]{};
     int last_launches[2]{};
@@ -671,6 +674,9 @@ int icw_create(const icw_config *cfg, const icw_node *nodes, int n_nodes, int n_
         const char *m = getenv("ICW_K1_MODE");
         if (m && !strcmp(m, "plain")) c->k1_mode = 0;
         if (m && !strcmp(m, "row")) c->k1_mode = 3;
+        const char *rr = getenv("ICW_RENDER");
+        if (rr && !strcmp(rr, "serial")) c->render_row = 0;
+        if (rr && !strcmp(rr, "row")) c->render_row = 1;
         const char *d = getenv("ICW_DITHER");
         c->dither_lane = d && !strcmp(d, "lane");
         const char *z = getenv("ICW_SERIALIZE");
@@ -1209,6 +1215,9 @@ int icw_process_streams(icw_ctx *c, int first, int count, const void *in, size_t
             a3.mt_pitch = c->n_streams * 2;
             a3.rk = c->rk;
             a3.fes = fcm ? ds.fes + f0 * 4 * ICW_FES_PITCH : nullptr;
+            /* the row-broadcast render (16 lanes per channel) while its waves stay few; FP_CHECK
+             * keeps the compact lane-per-channel form */
+            a3.row = !fcm && (c->render_row == 1 || (c->render_row < 0 && a3.n_gen <= kRowRenderMax)) ? 1 : 0;
             if (dither) {
                 /* K3a for this block on its own stream: dith[p] was last read by K3b of block b-2 */
                 a3.dith = c->dith[p];

@@ -1281,6 +1281,255 @@ __global__ __launch_bounds__(64) void icw_render_serial(IcwK3Args a)
     if (pk > 0.0) atomicMax(&a.peak_bits[g], (unsigned long long)__double_as_longlong(pk));
 }
 
+/* ------------------------------------------------------- render, row broadcast (K3r) ------- */
+/* The serial render of K3b with one 16-lane DPP row per channel instead of one lane, built like the
+ * IIR kernel K1r (icw_iir.hip): every lane of a row runs the channel's chain redundantly, so each
+ * value is row-uniform, and what is not on the chain leaves the per-sample instruction stream --
+ * K3b spends ~51 instructions per sample for a ~22-instruction dependent chain:
+ *   - the shaper terms: right after the error ev of sample n is known, ONE lane-parallel multiply
+ *     makes lane l hold cf[l+1] * ev (P2: cf[l+17]), term l+1 of sample n+l+1; the sum adds it
+ *     from that lane with `v_fmac_f64_dpp ... row_newbcast` (icw_render_asm.inc).  The IIR shaper's
+ *     term cf[i]*E - cf[i+NN]*O is formed the same way, three lane-parallel ops per sample;
+ *   - clips and peak: each lane stages q in its own LDS slot; at the end of a 20-sample block lane
+ *     l counts samples l and l+16 (every row holds all of them) -- ~0.5 instead of ~6 per sample;
+ *   - the frames: the shifted values are staged alike and a block's frames are written by 40
+ *     lanes at once.
+ * Sums keep the reference's order (res = 0.0; res += t_0; res += t_1 ...), products are rounded
+ * before they are added, so every value is the reference's (sound_render.c:754-809, ns_fir
+ * :403-438, ns_iir :442-489).  Small batches (the host's choice): 4 channels per wave. */
+__device__ __forceinline__ double icw_rmul(double a, double b)
+{
+    double r;
+    asm volatile("v_mul_f64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+
+__device__ __forceinline__ double icw_rsub(double a, double b)
+{
+    double r;
+    asm volatile("v_add_f64 %0, %1, -%2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+
+#include "icw_render_asm.inc"
+
+struct IcwRowNs {
+    double c0, cN;      /* row-uniform: cf[0]; IIR: cf[NN] (the O term of t_0) */
+    double pl, pl2;     /* per lane: FIR cf[l+1], cf[l+17]; IIR cf[l+1], cf[l+1+NN] (0 past the taps) */
+    double one;
+};
+
+/* one sample at unroll step J (0..ICW_MAX_NS_TAPS-1); rings of R slots, the newest at J mod R */
+template <int KIND, int NN, int R, int J>
+__device__ __forceinline__ void icw_rrow_step(double x, double d, double &prev_err, double (&E)[R], double (&O)[R],
+                                              double (&P)[R], double (&P2)[R], const IcwRowNs &c,
+                                              const IcwRenderK &k, double *qst, int *vst)
+{
+    constexpr int S = J % R;
+    const double input = (x * k.norm_mul) - prev_err;
+    double q = input + d;
+    int delta;
+    q = icw_round_q(q, k.round_offset, k.sign_delta, delta);
+    /* the clip stage as it reaches the integer (icw_clamp_int); clips and peak from the staged q */
+    const int vc = (int)fmax(fmin(q, k.hi - 1.0), k.lo + 1.0);
+    const int val = (isnan(q) ? (int)0x80000000 : vc) + delta;
+    qst[J * 16] = q;
+    vst[J * 16] = val;                                 /* shifted by norm_shift when written out */
+    const double ev = (double)val - input;
+    double res = 0.0;
+    /* the new products go out before this sample's sum, whose volatile fmac block then separates
+     * them from their first DPP read in the next sample (a VALU write -> DPP read needs two
+     * instructions in between, and the compiler does not look into the asm) */
+    if constexpr (KIND == 1) {
+        E[S] = ev;
+        P[S] = icw_rmul(c.pl, ev);
+        if constexpr (NN > 17) P2[S] = icw_rmul(c.pl2, ev);
+        res = 0.0 + c.c0 * ev;
+        res = icw_ns_row_sum<NN, R, S>(res, c.one, P, P2);
+    } else if constexpr (KIND == 2) {
+        E[S] = ev;
+        const double op = O[(S + R - 1) % R];
+        P[S] = icw_rsub(icw_rmul(c.pl, ev), icw_rmul(c.pl2, op));
+        res = 0.0 + (c.c0 * ev - c.cN * op);
+        res = icw_ns_row_sum<NN, R, S>(res, c.one, P, P2);
+        O[S] = res;
+    }
+    prev_err = res;
+}
+
+/* look-ahead loads: pn is the lane's pre-render row at the next block; the dither rows are
+ * time-major, so their address is a wave-uniform base dn plus the row's channel offset dl -- the
+ * per-sample step is scalar arithmetic.  Without dither dn is icw_zero4 with pitch 0 (a branch per
+ * load made the compiler copy the prefetch registers around every sample). */
+__device__ double icw_zero4[4];
+template <int KIND, int NN, int R, int J>
+__device__ __forceinline__ void icw_rrow_block(double (&xin)[ICW_MAX_NS_TAPS], double (&dv)[ICW_MAX_NS_TAPS],
+                                               double &prev_err, double (&E)[R], double (&O)[R], double (&P)[R],
+                                               double (&P2)[R], const IcwRowNs &c, const IcwRenderK &k, double *qst,
+                                               int *vst, const double *pn, const double *dn, size_t dpitch, int dl)
+{
+    if constexpr (J < ICW_MAX_NS_TAPS) {
+        icw_rrow_step<KIND, NN, R, J>(xin[J], dv[J], prev_err, E, O, P, P2, c, k, qst, vst);
+        xin[J] = pn[(size_t)J * 2];
+        dv[J] = dn[(size_t)J * dpitch + dl];
+        icw_rrow_block<KIND, NN, R, J + 1>(xin, dv, prev_err, E, O, P, P2, c, k, qst, vst, pn, dn, dpitch, dl);
+    }
+}
+
+template <int KIND, int NN, int R, int J>
+__device__ __forceinline__ void icw_rrow_block_lim(const double (&xin)[ICW_MAX_NS_TAPS], const double (&dv)[ICW_MAX_NS_TAPS],
+                                                   double &prev_err, double (&E)[R], double (&O)[R], double (&P)[R],
+                                                   double (&P2)[R], const IcwRowNs &c, const IcwRenderK &k, double *qst,
+                                                   int *vst, int lim)
+{
+    if constexpr (J < ICW_MAX_NS_TAPS) {
+        if (J < lim) {
+            icw_rrow_step<KIND, NN, R, J>(xin[J], dv[J], prev_err, E, O, P, P2, c, k, qst, vst);
+            icw_rrow_block_lim<KIND, NN, R, J + 1>(xin, dv, prev_err, E, O, P, P2, c, k, qst, vst, lim);
+        }
+    }
+}
+
+/* End of a block of nf samples: clips and peak of the staged q (lane l: samples l, l + 16 of its
+ * row), then the block's frames -- lanes 0-31 write stream A's (rows 0, 1), 32-63 stream B's. */
+__device__ __forceinline__ void icw_rrow_flush(const double (*qs)[ICW_MAX_NS_TAPS][16],
+                                               const int (*vs)[ICW_MAX_NS_TAPS][16], int r, int lr, int lane,
+                                               int nf, const IcwRenderK &k, unsigned &clips, double &pk,
+                                               unsigned char *o0, unsigned char *o1, int osz)
+{
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        const int j = lr + 16 * h;
+        if (j < nf) {
+            const double q = qs[r][j][lr];
+            clips += (q >= k.hi ? 1u : 0u) + (q <= k.lo ? 1u : 0u);
+            pk = fmax(pk, fabs(q));
+        }
+    }
+    const int sb = lane >> 5, f = lane & 31;
+    unsigned char *o = sb ? o1 : o0;
+    if (o && f < nf) {
+        const uint32_t l = (uint32_t)(vs[2 * sb][f][0] << k.norm_shift);
+        const uint32_t rr = (uint32_t)(vs[2 * sb + 1][f][0] << k.norm_shift);
+        if (osz == 2) {
+            *(uint32_t *)(o + (size_t)f * 4) = (l & 0xffffu) | (rr << 16);
+        } else {
+            uint16_t *p = (uint16_t *)(o + (size_t)f * 6);
+            p[0] = (uint16_t)(l & 0xffffu);
+            p[1] = (uint16_t)(((l >> 16) & 0xffu) | ((rr & 0xffu) << 8));
+            p[2] = (uint16_t)((rr >> 8) & 0xffffu);
+        }
+    }
+    __builtin_amdgcn_wave_barrier();
+}
+
+template <int KIND, int NN>
+__global__ __launch_bounds__(64) void icw_render_row(IcwK3Args a)
+{
+    constexpr int U = ICW_MAX_NS_TAPS;                 /* samples per unrolled block */
+    constexpr int R = KIND == 1 ? U : (KIND == 2 ? 4 : 1);
+    static_assert(U % R == 0, "ring period must divide the unroll");
+    __shared__ double qs[4][U][16];                    /* q of each sample, every lane its own slot */
+    __shared__ int vs[4][U][16];                       /* the output values before the shift */
+    const int lane = threadIdx.x, r = lane >> 4, lr = lane & 15;
+    const int g0 = blockIdx.x * 4 + r;
+    const bool valid = g0 < a.n_gen;
+    const int g = valid ? g0 : a.n_gen - 1;            /* spare rows run a copy, store nothing */
+    const int s = g >> 1, ch = g & 1;
+    const IcwRenderK &k = a.rk;
+    double *rs = a.rs + (size_t)g * ICW_RSTATE;
+    double prev_err = rs[1];
+    double E[R], O[R], P[R], P2[R];
+    IcwRowNs c;
+    c.one = 1.0;
+    c.c0 = k.ns_c[0];
+    c.cN = KIND == 2 ? k.ns_c[NN] : 0.0;
+    if constexpr (KIND == 2) {
+        c.pl = lr + 1 < NN ? k.ns_c[lr + 1] : 0.0;
+        c.pl2 = lr + 1 < NN ? k.ns_c[lr + 1 + NN] : 0.0;
+    } else {
+        c.pl = lr + 1 < NN ? k.ns_c[lr + 1] : 0.0;
+        c.pl2 = lr + 17 < NN ? k.ns_c[lr + 17] : 0.0;
+    }
+    /* block start: age i sits in slot (-1 - i) mod R; the products of those ages */
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+        E[(R - 1 - i) % R] = rs[2 + i];
+        O[(R - 1 - i) % R] = rs[2 + U + i];
+    }
+    if constexpr (KIND == 1) {
+#pragma unroll
+        for (int m = 0; m < R; ++m) {
+            P[m] = icw_rmul(c.pl, E[m]);
+            if constexpr (NN > 17) P2[m] = icw_rmul(c.pl2, E[m]);
+        }
+    } else if constexpr (KIND == 2) {
+#pragma unroll
+        for (int m = 0; m < R; ++m) P[m] = icw_rsub(icw_rmul(c.pl, E[m]), icw_rmul(c.pl2, O[(m + R - 1) % R]));
+    }
+    asm volatile("s_nop 1");                           /* VALU write -> DPP read of P / P2 */
+    const int osz = k.is24 ? 3 : 2;
+    const double *pp = a.pre + (size_t)s * a.pre_stride + ch;
+    /* dither rows, time-major [t][dith_pitch]; ROUND: rnd * dth_mul == 0.0 * dth_mul, all zeros */
+    const double *dp = a.dith ? a.dith + blockIdx.x * 4 : icw_zero4;
+    const int dl = g - blockIdx.x * 4;                 /* this row's channel in the wave's four */
+    const size_t dpitch = a.dith ? a.dith_pitch : 0;
+    /* the wave's two streams (channels 4b..4b+3); a stream past the batch writes nothing */
+    const int sA = blockIdx.x * 2, sB = sA + 1;
+    unsigned char *oA = 2 * sA < a.n_gen ? a.out + (size_t)sA * a.out_stride : nullptr;
+    unsigned char *oB = 2 * sB < a.n_gen ? a.out + (size_t)sB * a.out_stride : nullptr;
+    double *qst = &qs[r][0][lr];
+    int *vst = &vs[r][0][lr];
+    unsigned clips = 0;
+    double pk = 0.0;
+    const int T = a.T;
+    int t = 0;
+    double xin[U], dv[U];
+    if (T >= U) {
+#pragma unroll
+        for (int j = 0; j < U; ++j) {
+            xin[j] = pp[(size_t)j * 2];
+            dv[j] = dp[(size_t)j * dpitch + dl];
+        }
+        for (; t + U <= T; t += U) {
+            /* look-ahead loads of the next block; the last full block re-reads a valid window */
+            const int tn = t + 2 * U <= T ? t + U : T - U;
+            icw_rrow_block<KIND, NN, R, 0>(xin, dv, prev_err, E, O, P, P2, c, k, qst, vst, pp + (size_t)tn * 2,
+                                           dp + (size_t)tn * dpitch, dpitch, dl);
+            icw_rrow_flush(qs, vs, r, lr, lane, U, k, clips, pk, oA ? oA + (size_t)t * 2 * osz : nullptr,
+                           oB ? oB + (size_t)t * 2 * osz : nullptr, osz);
+        }
+    }
+    const int rem = T - t;
+    if (rem > 0) {
+#pragma unroll
+        for (int j = 0; j < U; ++j) {
+            xin[j] = j < rem ? pp[(size_t)(t + j) * 2] : 0.0;
+            dv[j] = j < rem ? dp[(size_t)(t + j) * dpitch + dl] : 0.0;
+        }
+        icw_rrow_block_lim<KIND, NN, R, 0>(xin, dv, prev_err, E, O, P, P2, c, k, qst, vst, rem);
+        icw_rrow_flush(qs, vs, r, lr, lane, rem, k, clips, pk, oA ? oA + (size_t)t * 2 * osz : nullptr,
+                       oB ? oB + (size_t)t * 2 * osz : nullptr, osz);
+        /* back to the block-start mapping: rotate left by rem mod R */
+#pragma unroll
+        for (int q = 1; q < U; ++q)
+            if (q <= rem) { icw_ring_rotate1<R>(E); icw_ring_rotate1<R>(O); }
+    }
+    /* meters: the row's lanes hold disjoint samples */
+#pragma unroll
+    for (int off = 1; off < 16; off <<= 1) {
+        clips += __shfl_xor(clips, off);
+        pk = fmax(pk, __shfl_xor(pk, off));
+    }
+    if (!valid || lr != 0) return;
+    rs[1] = prev_err;
+#pragma unroll
+    for (int i = 0; i < R; ++i) { rs[2 + i] = E[(R - 1 - i) % R]; rs[2 + U + i] = O[(R - 1 - i) % R]; }
+    if (clips) atomicAdd(&a.clips[g], clips);
+    if (pk > 0.0) atomicMax(&a.peak_bits[g], (unsigned long long)__double_as_longlong(pk));
+}
+
 /* Render with FP_CHECK (K3f): sound_render_value's WITH FC CHECKS arithmetic (sound_render.c:
  * 857-903) and ns_fir / ns_iir's (428-433, 474-486), counting into the render census.  One lane per
  * channel like K3b, but compact (run-time loops, the reference's own decrementing ring in private
@@ -1419,6 +1668,25 @@ extern "C" hipError_t icw_launch_render(const IcwK3Args *a, hipStream_t st)
     }
     /* the tap counts of the canned shapers (sound_render.c:75-235): FIR 5, 9, 15, 16, 20; IIR 4 */
     const int nn = a->rk.ns_n;
+    if (a->row) {
+        const int rb = (a->n_gen + 3) / 4;          /* four channels (two streams) per wave */
+        if (a->rk.ns_kind == 0) {
+            hipLaunchKernelGGL((icw_render_row<0, 0>), dim3(rb), dim3(64), 0, st, *a);
+        } else if (a->rk.ns_kind == 1) {
+            switch (nn) {
+            case 5: hipLaunchKernelGGL((icw_render_row<1, 5>), dim3(rb), dim3(64), 0, st, *a); break;
+            case 9: hipLaunchKernelGGL((icw_render_row<1, 9>), dim3(rb), dim3(64), 0, st, *a); break;
+            case 15: hipLaunchKernelGGL((icw_render_row<1, 15>), dim3(rb), dim3(64), 0, st, *a); break;
+            case 16: hipLaunchKernelGGL((icw_render_row<1, 16>), dim3(rb), dim3(64), 0, st, *a); break;
+            case 20: hipLaunchKernelGGL((icw_render_row<1, 20>), dim3(rb), dim3(64), 0, st, *a); break;
+            default: return hipErrorInvalidValue;
+            }
+        } else {
+            if (nn != 4) return hipErrorInvalidValue;
+            hipLaunchKernelGGL((icw_render_row<2, 4>), dim3(rb), dim3(64), 0, st, *a);
+        }
+        return hipGetLastError();
+    }
     if (a->rk.ns_kind == 0) {
         hipLaunchKernelGGL((icw_render_serial<0, 1, 0>), dim3(blocks), dim3(64), 0, st, *a);
     } else if (a->rk.ns_kind == 1) {

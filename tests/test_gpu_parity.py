@@ -14,10 +14,11 @@ pytestmark = pytest.mark.gpu
 
 @pytest.fixture(autouse=True, params=["plain", "row"])
 def k1_mode(request, monkeypatch):
-    """run every case through both shipped IIR-state kernels: the lane-per-chain kernel (large
-    batches) and the row-broadcast kernel (small batches; Kahan + reject only, other modes fall
-    back to the lane-per-chain kernel)"""
+    """run every case through both shipped forms of the two serial kernels: lane per chain / per
+    render channel (large batches: K1, K3b) and the 16-lane row broadcast (small batches: K1r, K3r;
+    K1r takes Kahan + reject only, other modes fall back to the lane-per-chain kernel)"""
     monkeypatch.setenv("ICW_K1_MODE", request.param)
+    monkeypatch.setenv("ICW_RENDER", "serial" if request.param == "plain" else "row")
     return request.param
 
 
