@@ -15,7 +15,7 @@ import json
 from pathlib import Path
 
 KERNELS = ("icw_unpack_frames", "icw_iir_state", "icw_iir_row", "icw_output", "icw_trig_table", "icw_dither_coop",
-           "icw_render_serial")
+           "icw_render_serial", "icw_render_row")
 
 
 def per_dispatch(d, counter):
