@@ -110,7 +110,8 @@ struct IcwOp {
     double f[2];                   /* effective (scaled) frequency */
     double pp[2], lp[2], fa[2];    /* PM: fphase*PI, flevel*PI, fangle */
     int32_t tslot[2];              /* Shift / PM channel: column of the per-frame rotation table */
-    int32_t pad_;
+    int32_t wb_slot;               /* register form: the slot whose final value this op writes (its
+                                      output goes to the persistent bus at a block's last frame), -1 */
 };
 
 /* A compiled DSP list.  Register form (frame-parallel output kernel): every slot read resolves at
@@ -126,8 +127,6 @@ struct IcwProg {
     int32_t n_trig;                /* active Shift / PM channels = columns of the rotation table */
     int32_t n_persist;             /* slots read before any write in the frame and never written */
     int32_t persist_reg[ICW_MAX_REGS], persist_slot[ICW_MAX_REGS];
-    int32_t n_wb;                  /* slots written in the frame: final value -> persistent bus */
-    int32_t wb_reg[ICW_MAX_REGS + ICW_MAX_REG_OPS], wb_slot[ICW_MAX_REGS + ICW_MAX_REG_OPS];
     IcwOp ops[ICW_MAX_OPS];
 };
 

@@ -252,6 +252,7 @@ double scaled_fr(double f) { return (double)((unsigned)(f * ((double)ICW_HZ_SCAL
 void op_params(const icw_node &n, IcwOp &op)
 {
     op.mode = n.mode;
+    op.wb_slot = -1;
     op.xch = n.xch_mode;
     op.iqinv[0] = n.iq_invert[0];
     op.iqinv[1] = n.iq_invert[1];
@@ -320,7 +321,15 @@ int compile_bus(const std::vector<icw_node> &nodes, int bypass, IcwProg &P)
 
 /* Register form for the frame-parallel output kernel; ICW_EUNSUPPORTED when a slot is read
  * before it is written in the frame (one-frame delay) or the list exceeds the register budget --
- * the caller then compiles the bus form. */
+ * the caller then compiles the bus form.
+ *
+ * Value registers live in K2's LDS (8 KB each per 256-frame workgroup), so they are allocated by
+ * liveness: `in` is register 0 for the frame; a node's output takes the lowest register whose value
+ * has had its last reader (an op may write over its own inputs: it reads them all first); a slot
+ * read but never written in the frame is loaded once per workgroup and keeps its register.  A
+ * written slot's final value goes to the persistent bus from the op that writes it (wb_slot), at
+ * the block's last frame, so it need not stay live to the end.  PM -> Shift -> Mix -> Master
+ * (C4) takes 2 registers instead of 4, which lets K2 keep 4 waves per SIMD. */
 int compile_graph(const std::vector<icw_node> &nodes, int bypass, IcwProg &P)
 {
     memset(&P, 0, sizeof(P));
@@ -329,6 +338,7 @@ int compile_graph(const std::vector<icw_node> &nodes, int bypass, IcwProg &P)
     if (bypass) order.push_back(0);
     else for (int i = (int)nodes.size() - 1; i >= 0; --i) order.push_back(i);
     if ((int)order.size() > ICW_MAX_REG_OPS) return ICW_EUNSUPPORTED;
+    const int n_ops = (int)order.size();
 
     bool written_any[ICW_N_INPUTS] = {false};
     for (int i : order)
@@ -337,46 +347,90 @@ int compile_graph(const std::vector<icw_node> &nodes, int bypass, IcwProg &P)
             if (o < 0 || o >= ICW_N_INPUTS) return ICW_EGRAPH;
             written_any[o] = true;
         }
+    /* values: 0 = `in`, then persistent slots and op outputs in order of appearance */
+    std::vector<int> last_use(1, -1), def_op(1, -1);
+    std::vector<char> pinned(1, 0);
+    std::vector<std::vector<int>> reads(n_ops);
+    std::vector<int> out_val(n_ops, -1);
     int cur[ICW_N_INPUTS];
     for (int k = 0; k < ICW_N_INPUTS; ++k) cur[k] = -1;
     cur[0] = 0;
-    int n_regs = 1;
-    for (size_t oi = 0; oi < order.size(); ++oi) {
+    std::vector<int> persist_val, persist_slot;
+    for (int oi = 0; oi < n_ops; ++oi) {
         const icw_node &n = nodes[order[oi]];
-        IcwOp &op = P.ops[oi];
-        op.mode = n.mode;
         if (!bypass) {
             for (int k = 0; k < ICW_N_INPUTS; ++k) {
                 if (!n.inputs[k]) continue;
-                int r = cur[k];
-                if (r < 0) {
+                int v = cur[k];
+                if (v < 0) {
                     if (written_any[k]) return ICW_EUNSUPPORTED;   /* delayed (feedback) read */
-                    if (n_regs >= ICW_MAX_REGS) return ICW_EUNSUPPORTED;
-                    r = n_regs++;
-                    P.persist_reg[P.n_persist] = r;
-                    P.persist_slot[P.n_persist] = k;
-                    ++P.n_persist;
-                    cur[k] = r;
+                    v = (int)last_use.size();
+                    last_use.push_back(-1);
+                    def_op.push_back(-1);
+                    pinned.push_back(1);
+                    persist_val.push_back(v);
+                    persist_slot.push_back(k);
+                    cur[k] = v;
                 }
-                op.in_reg[op.n_in++] = r;
+                reads[oi].push_back(v);
+                last_use[v] = oi;
             }
         }
-        op_params(n, op);
         if (n.mode != ICW_MODE_MASTER) {
-            if (n_regs >= ICW_MAX_REGS) return ICW_EUNSUPPORTED;
-            op.out_reg = n_regs++;
-            cur[n.n_out] = op.out_reg;
+            const int v = (int)last_use.size();
+            last_use.push_back(-1);
+            def_op.push_back(oi);
+            pinned.push_back(0);
+            out_val[oi] = v;
+            cur[n.n_out] = v;
         }
     }
-    P.n_ops = (int)order.size();
-    P.n_regs = n_regs;
-    set_needs_omega(P);
+    /* the op that leaves each written slot its final value */
+    std::vector<int> wb(n_ops, -1);
     for (int k = 0; k < ICW_N_INPUTS; ++k)
-        if (written_any[k] && cur[k] >= 0) {
-            P.wb_reg[P.n_wb] = cur[k];
-            P.wb_slot[P.n_wb] = k;
-            ++P.n_wb;
+        if (written_any[k] && cur[k] >= 0) wb[def_op[cur[k]]] = k;
+    /* physical registers */
+    std::vector<int> phys(last_use.size(), -1), holder(ICW_MAX_REGS, -1);
+    phys[0] = 0;
+    holder[0] = 0;
+    for (size_t q = 0; q < persist_val.size(); ++q) {
+        int r = 1;
+        while (r < ICW_MAX_REGS && holder[r] >= 0) ++r;
+        if (r >= ICW_MAX_REGS) return ICW_EUNSUPPORTED;
+        phys[persist_val[q]] = r;
+        holder[r] = persist_val[q];
+    }
+    int n_regs = 1 + (int)persist_val.size();
+    for (int oi = 0; oi < n_ops; ++oi) {
+        IcwOp &op = P.ops[oi];
+        const icw_node &n = nodes[order[oi]];
+        op.mode = n.mode;
+        for (int v : reads[oi]) op.in_reg[op.n_in++] = phys[v];
+        op_params(n, op);
+        op.wb_slot = wb[oi];
+        /* free the registers whose values were read for the last time by this op */
+        for (int r = 0; r < ICW_MAX_REGS; ++r) {
+            const int v = holder[r];
+            if (v >= 0 && !pinned[v] && last_use[v] <= oi) holder[r] = -1;
         }
+        if (out_val[oi] >= 0) {
+            int r = 0;
+            while (r < ICW_MAX_REGS && holder[r] >= 0) ++r;
+            if (r >= ICW_MAX_REGS) return ICW_EUNSUPPORTED;
+            phys[out_val[oi]] = r;
+            holder[r] = out_val[oi];
+            op.out_reg = r;
+            n_regs = std::max(n_regs, r + 1);
+        }
+    }
+    P.n_ops = n_ops;
+    P.n_regs = n_regs;
+    for (size_t q = 0; q < persist_val.size(); ++q) {
+        P.persist_reg[q] = phys[persist_val[q]];
+        P.persist_slot[q] = persist_slot[q];
+    }
+    P.n_persist = (int)persist_val.size();
+    set_needs_omega(P);
     return ICW_OK;
 }
 

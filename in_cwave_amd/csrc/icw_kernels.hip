@@ -377,6 +377,16 @@ __device__ __forceinline__ void icw_trig(const IcwOp &op, int c, double omega, d
     }
 }
 
+/* icw_trig out of line, for the per-stream fallback of K2 / K4 (a stream whose frame counter is
+ * not stream 0's): inlined, glibc's sincos path added ~45 VGPRs to K2 and cost it a wave per SIMD
+ * (141 -> 3 waves) although the per-frame rotation table serves every stream in step. */
+__device__ __noinline__ double2 icw_trig_call(const IcwOp &op, int c, double omega)
+{
+    double cs, sn;
+    icw_trig(op, c, omega, cs, sn);
+    return make_double2(cs, sn);
+}
+
 /* One DSP node on its mixed input d (adv_modulator.c:669-751): channel exchange, I/Q swap,
  * gains, then Master (-> lOut/rOut) or Shift / PM / Mix (-> o, returns true).  trow: this frame's
  * row of the rotation table (nullable: compute the factors inline). */
@@ -413,12 +423,12 @@ __device__ __forceinline__ bool icw_exec_op(const IcwOp &op, IcwLR d, double ome
         double cs, sn;
         if (op.act[0]) {
             if (trow) { cs = trow[op.tslot[0] * 2]; sn = trow[op.tslot[0] * 2 + 1]; }
-            else icw_trig(op, 0, omega, cs, sn);
+            else { const double2 f = icw_trig_call(op, 0, omega); cs = f.x; sn = f.y; }
             icw_rot(d.lre, d.lim, cs, sn, o.lre, o.lim);
         } else { o.lre = d.lre; o.lim = d.lim; }
         if (op.act[1]) {
             if (trow) { cs = trow[op.tslot[1] * 2]; sn = trow[op.tslot[1] * 2 + 1]; }
-            else icw_trig(op, 1, omega, cs, sn);
+            else { const double2 f = icw_trig_call(op, 1, omega); cs = f.x; sn = f.y; }
             icw_rot(d.rre, d.rim, cs, sn, o.rre, o.rim);
         } else { o.rre = d.rre; o.rim = d.rim; }
         return true;
@@ -570,6 +580,11 @@ __global__ __launch_bounds__(ICW_K2_TILE, ICW_K2_MINWG) void icw_output(IcwK2Arg
                                                         : 0.0;
                 /* DSP list (adv_modulator.c:637-751) */
                 R.set(0, in);
+                /* persistent bus at the block's last frame: slot 0 = in, then each written slot's
+                 * final value from the op that writes it (compile_graph: op.wb_slot) */
+                const bool last = t == T - 1;
+                double *bus_s = a.bus + (size_t)s * ICW_N_INPUTS * 4;
+                if (last) { bus_s[0] = in.lre; bus_s[1] = in.lim; bus_s[2] = in.rre; bus_s[3] = in.rim; }
                 double lOut = 0.0, rOut = 0.0;
                 for (int oi = 0; oi < P->n_ops; ++oi) {
                     const IcwOp &op = P->ops[oi];
@@ -585,7 +600,13 @@ __global__ __launch_bounds__(ICW_K2_TILE, ICW_K2_MINWG) void icw_output(IcwK2Arg
                         }
                     }
                     IcwLR o;
-                    if (icw_exec_op<TRIG>(op, d, omega, o, lOut, rOut, trow)) R.set(op.out_reg, o);
+                    if (icw_exec_op<TRIG>(op, d, omega, o, lOut, rOut, trow)) {
+                        R.set(op.out_reg, o);
+                        if (last && op.wb_slot >= 0) {
+                            double *b = bus_s + op.wb_slot * 4;
+                            b[0] = o.lre; b[1] = o.lim; b[2] = o.rre; b[3] = o.rim;
+                        }
+                    }
                 }
 
                 if (a.pre) {
@@ -603,17 +624,6 @@ __global__ __launch_bounds__(ICW_K2_TILE, ICW_K2_MINWG) void icw_output(IcwK2Arg
                     } else {
                         const unsigned pk = ((unsigned)vl & 0xffffu) | ((unsigned)vr << 16);
                         *(unsigned *)(o + (size_t)t * 4) = pk;
-                    }
-                }
-                /* persistent bus write-back from the block's last frame */
-                if (t == T - 1) {
-                    double *b0 = a.bus + (size_t)s * ICW_N_INPUTS * 4;
-                    b0[0] = in.lre; b0[1] = in.lim; b0[2] = in.rre; b0[3] = in.rim;
-                    for (int q = 0; q < P->n_wb; ++q) {
-                        IcwLR v;
-                        R.get(P->wb_reg[q], v);
-                        double *b = b0 + P->wb_slot[q] * 4;
-                        b[0] = v.lre; b[1] = v.lim; b[2] = v.rre; b[3] = v.rim;
                     }
                 }
             }
