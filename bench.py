@@ -376,18 +376,23 @@ def measure_gpu(wname, streams, frames, steps, warmup, e2e_steps, dev, local_dev
     # ---- end to end from host memory (H2D + D2H in the loop), one rank's view, not `value`
     e2e = None
     if e2e_steps > 0 and rank == 0:
-        h_in = np.ascontiguousarray(np.tile(gen, ((S + n_gen - 1) // n_gen, 1))[:S])
-        h_out = np.empty((S, T * osz), dtype=np.uint8)
+        # pinned host buffers (icw_host_alloc): the call copies each launch block's slices in and
+        # out on a copy stream beside the other blocks' kernels
+        h_in = L.host_array((S, gen.shape[1]))
+        for s0 in range(0, S, n_gen):
+            h_in[s0:s0 + n_gen] = gen[:min(n_gen, S - s0)]
+        h_out = L.host_array((S, T * osz))
         ctx.process(h_in, T, out=h_out)                       # warm the staging buffers
         te = time.perf_counter()
         for _ in range(e2e_steps):
             ctx.process(h_in, T, out=h_out)
         te = time.perf_counter() - te
-        del h_out
+        del h_out, h_in
         e2e = {"value": 2.0 * S * T * e2e_steps / te / 1e6, "unit": "Msamples/s",
                "ms_per_step": te * 1e3 / e2e_steps, "steps": e2e_steps,
-               "note": "host (pageable numpy) input and output: the call stages them through the "
-                       "context's pinned buffers, H2D + kernels + D2H, one GPU"}
+               "note": "host input and output in pinned memory (icw_host_alloc): H2D of each launch "
+                       "block's input, the kernels and D2H of its output, the copies on a copy stream "
+                       "beside the other blocks' kernels; one GPU"}
 
     # ---- roofline of the dominant kernel K1 (the serial recurrence), per launch, from HIP events
     # recorded on the stream K1 runs on (icw_last_timing)

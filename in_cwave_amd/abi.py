@@ -142,6 +142,8 @@ SIGNATURES = {
     "icw_process_batch": (_i, [_vp, _vp, _sz, _vp, _sz, _i, _u, _vp, _vp]),
     "icw_process_streams": (_i, [_vp, _i, _i, _vp, _sz, _vp, _sz, _i, _u, _vp, _vp]),
     "icw_synchronize": (_i, [_vp]),
+    "icw_host_alloc": (_i, [C.c_size_t, C.POINTER(_vp)]),
+    "icw_host_free": (_i, [_vp]),
     "icw_get_meters": (_i, [_vp, _i, _i, C.POINTER(Meters)]),
     "icw_render_size": (_i, [_vp]),
     "icw_n_frame": (_i, [_vp, _i, C.POINTER(C.c_uint64)]),

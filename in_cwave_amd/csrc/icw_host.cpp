@@ -143,6 +143,9 @@ struct icw_ctx {
     /* the serial render (K4 bus-form graph + K3b) runs on a fourth stream, one block behind K2:
      * its inputs are double-buffered like the block scratch */
     hipStream_t stream4 = nullptr;
+    /* copy stream of the block-pipelined host I/O (pinned host buffers): per-block H2D / D2H */
+    hipStream_t stream_io = nullptr;
+    std::vector<hipEvent_t> ev_io;        /* H2D of launch block b done */
     hipEvent_t k3done[kSets] = {};
     double *rpre[kSets] = {};             /* per-block pre-render buffer for the serial render */
     size_t rpre_bytes[kSets] = {};
@@ -524,6 +527,19 @@ std::vector<std::pair<int, int>> plan_blocks(int n_frames, int Tb, int first, do
     return bl;
 }
 
+/* page-locked host memory (hipHostMalloc / hipHostRegister): the DMA engines read it directly, so
+ * an asynchronous copy does not block the host thread.  A pageable pointer makes the query fail;
+ * the error is cleared so that it does not surface as the call's own. */
+bool host_pinned(const void *p)
+{
+    hipPointerAttribute_t a;
+    if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    return a.type == hipMemoryTypeHost;
+}
+
 hipError_t quiesce(icw_ctx *c)
 {
     (void)c;
@@ -590,6 +606,8 @@ void free_all(icw_ctx *c)
     if (c->h_stage) (void)hipHostFree(c->h_stage);
     if (c->stream3) (void)hipStreamDestroy(c->stream3);
     if (c->stream4) (void)hipStreamDestroy(c->stream4);
+    if (c->stream_io) (void)hipStreamDestroy(c->stream_io);
+    for (auto e : c->ev_io) (void)hipEventDestroy(e);
     if (c->join) (void)hipEventDestroy(c->join);
     if (c->stream2) (void)hipStreamDestroy(c->stream2);
     for (auto e : c->ev) (void)hipEventDestroy(e);
@@ -706,6 +724,7 @@ int icw_create(const icw_config *cfg, const icw_node *nodes, int n_nodes, int n_
     if (rc == ICW_OK && hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking) != hipSuccess) rc = ICW_EDEVICE;
     if (rc == ICW_OK && hipStreamCreateWithFlags(&c->stream3, hipStreamNonBlocking) != hipSuccess) rc = ICW_EDEVICE;
     if (rc == ICW_OK && hipStreamCreateWithFlags(&c->stream4, hipStreamNonBlocking) != hipSuccess) rc = ICW_EDEVICE;
+    if (rc == ICW_OK && hipStreamCreateWithFlags(&c->stream_io, hipStreamNonBlocking) != hipSuccess) rc = ICW_EDEVICE;
     for (int p = 0; p < kSets && rc == ICW_OK; ++p)
         if (hipEventCreateWithFlags(&c->k1done[p], hipEventDisableTiming) != hipSuccess ||
             hipEventCreateWithFlags(&c->k2done[p], hipEventDisableTiming) != hipSuccess ||
@@ -939,12 +958,19 @@ int icw_process_streams(icw_ctx *c, int first, int count, const void *in, size_t
     const size_t S = (size_t)count;
     if (!dev && (in_stride < (size_t)n_frames * fsz || out_stride < (size_t)n_frames * osz)) return ICW_EINVAL;
 
+    const int Tb = std::min(n_frames, c->max_block);
+    const std::vector<std::pair<int, int>> blocks = plan_blocks(n_frames, Tb, c->first_block, c->taper, c->taper_min);
+    const int n_blocks = (int)blocks.size();
+
     const unsigned char *d_in;
     unsigned char *d_out;
     size_t dis, dos;
     /* a small host-pointer call stages through pinned memory (asynchronous copies, one wait) */
     const size_t stage_in = (size_t)n_frames * fsz * S, stage_out = (size_t)n_frames * osz * S;
     const bool pinned = !dev && stage_in + stage_out + 16 <= kPinnedStage;
+    /* pinned host buffers on a call of several launch blocks: each block's input slice goes in and
+     * its output slice comes out on the copy stream, beside the other blocks' kernels */
+    const bool pipe_io = !dev && !pinned && n_blocks > 1 && !c->serialize && host_pinned(in) && host_pinned(out);
     if (pinned) {
         if (c->h_stage_bytes < stage_in + stage_out + 16) {
             if (c->h_stage) (void)hipHostFree(c->h_stage);
@@ -969,7 +995,8 @@ int icw_process_streams(icw_ctx *c, int first, int count, const void *in, size_t
                 memcpy(c->h_stage + i * dis, (const unsigned char *)in + i * in_stride, dis);
             if (hipMemcpyAsync(c->d_in, c->h_stage, dis * S, hipMemcpyHostToDevice, st) != hipSuccess)
                 return ICW_EDEVICE;
-        } else if (hipMemcpy2DAsync(c->d_in, dis, in, in_stride, dis, S, hipMemcpyHostToDevice, st) != hipSuccess) {
+        } else if (!pipe_io &&
+                   hipMemcpy2DAsync(c->d_in, dis, in, in_stride, dis, S, hipMemcpyHostToDevice, st) != hipSuccess) {
             return ICW_EDEVICE;
         }
         d_in = c->d_in;
@@ -986,11 +1013,8 @@ int icw_process_streams(icw_ctx *c, int first, int count, const void *in, size_t
     }
 
     const int N = c->nord;
-    const int Tb = std::min(n_frames, c->max_block);
     const size_t w_pitch = (size_t)Tb + N + 1;
     const size_t x_pitch = ((size_t)Tb + ICW_MAX_IIR_ORDER + 2) & ~(size_t)1;   /* look-ahead pad */
-    const std::vector<std::pair<int, int>> blocks = plan_blocks(n_frames, Tb, c->first_block, c->taper, c->taper_min);
-    const int n_blocks = (int)blocks.size();
     const int n_sets = std::min(n_blocks, c->max_sets);
     for (int p = 0; p < n_sets; ++p) {
         if (grow((void **)&c->w[p], &c->w_bytes[p], S * 4 * w_pitch * sizeof(double))) return ICW_ENOMEM;
@@ -1058,10 +1082,18 @@ int icw_process_streams(icw_ctx *c, int first, int count, const void *in, size_t
             if (c->fill_drain) sF = c->stream2;
         }
     }
+    hipStream_t sC = pipe_io ? c->stream_io : nullptr;
+    if (pipe_io && (int)c->ev_io.size() < n_blocks) {
+        while ((int)c->ev_io.size() < n_blocks) {
+            hipEvent_t e;
+            if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return ICW_EDEVICE;
+            c->ev_io.push_back(e);
+        }
+    }
     /* every stream starts after everything already queued on st (inputs, previous calls) */
     if (hipEventRecord(c->join, st) != hipSuccess)
         return ICW_EDEVICE;
-    for (hipStream_t x : {sK, sA, sD, sR, sF})
+    for (hipStream_t x : {sK, sA, sD, sR, sF, sC})
         if (x && x != st && hipStreamWaitEvent(x, c->join, 0) != hipSuccess) return ICW_EDEVICE;
 
     DevState &ds = c->st;
@@ -1099,6 +1131,13 @@ int icw_process_streams(icw_ctx *c, int first, int count, const void *in, size_t
         a0.dedup = dedup ? 1 : 0;
         if (b >= n_sets && !cw && sK != sA && hipStreamWaitEvent(sA, c->k1done[p], 0) != hipSuccess) return ICW_EDEVICE;
         hipStream_t s0 = (b == 0 && sF) ? sF : sA;         /* the fill: nothing else runs yet */
+        if (pipe_io) {
+            /* this block's input slice of every stream, on the copy stream */
+            if (hipMemcpy2DAsync(c->d_in + (size_t)t0 * fsz, dis, (const unsigned char *)in + (size_t)t0 * fsz, in_stride,
+                                 (size_t)T * fsz, S, hipMemcpyHostToDevice, sC) != hipSuccess ||
+                hipEventRecord(c->ev_io[b], sC) != hipSuccess || hipStreamWaitEvent(s0, c->ev_io[b], 0) != hipSuccess)
+                return ICW_EDEVICE;
+        }
         if (icw_launch_unpack(&a0, s0) != hipSuccess) return ICW_EDEVICE;
         if (hipEventRecord(c->k0done[p], s0) != hipSuccess) return ICW_EDEVICE;
         return ICW_OK;
@@ -1286,6 +1325,13 @@ int icw_process_streams(icw_ctx *c, int first, int count, const void *in, size_t
             if (hipEventRecord(c->k3done[p], sR) != hipSuccess) return ICW_EDEVICE;
         }
         if (timing && hipEventRecord(c->ev[4 * b + 3], c->serial_render ? sR : s2) != hipSuccess) return ICW_EDEVICE;
+        if (pipe_io) {
+            /* this block's output slice, once its last writer (K2, or the serial render) is done */
+            if (hipStreamWaitEvent(sC, c->serial_render ? c->k3done[p] : c->k2done[p], 0) != hipSuccess ||
+                hipMemcpy2DAsync((unsigned char *)out + (size_t)t0 * osz, out_stride, d_out + (size_t)t0 * osz, dos,
+                                 (size_t)T * osz, S, hipMemcpyDeviceToHost, sC) != hipSuccess)
+                return ICW_EDEVICE;
+        }
         /* complex input: K0(b + n_sets) reuses xd[p], which K2(b) read */
         if (cw && b + n_sets < n_blocks && (rc0 = launch_k0(b + n_sets)) != ICW_OK) return rc0;
     }
@@ -1293,7 +1339,7 @@ int icw_process_streams(icw_ctx *c, int first, int count, const void *in, size_t
         for (int i = 0; i < count; ++i) c->lr_known[first + i] = 0;   /* stereo: the halves diverge */
     /* join: the caller's stream continues after every kernel of the call, then the call-start
      * position / phases / frame counters advance (icw_advance) */
-    for (hipStream_t x : {sK, sA, sD, sR, sF})
+    for (hipStream_t x : {sK, sA, sD, sR, sF, sC})
         if (x && x != st && (hipEventRecord(c->join, x) != hipSuccess || hipStreamWaitEvent(st, c->join, 0) != hipSuccess))
             return ICW_EDEVICE;
     {
@@ -1318,7 +1364,7 @@ int icw_process_streams(icw_ctx *c, int first, int count, const void *in, size_t
     if (!dev) {
         unsigned char *h_out = pinned ? c->h_stage + stage_in : nullptr;
         if (pinned ? hipMemcpyAsync(h_out, d_out, dos * S + sizeof(int), hipMemcpyDeviceToHost, st) != hipSuccess
-                   : hipMemcpy2DAsync(out, out_stride, d_out, dos, dos, S, hipMemcpyDeviceToHost, st) != hipSuccess)
+                   : (!pipe_io && hipMemcpy2DAsync(out, out_stride, d_out, dos, dos, S, hipMemcpyDeviceToHost, st) != hipSuccess))
             return ICW_EDEVICE;
         if (d_pre && hipMemcpyAsync(dbg, d_pre, S * (size_t)n_frames * 2 * sizeof(double), hipMemcpyDeviceToHost, st) != hipSuccess)
             return ICW_EDEVICE;
@@ -1356,6 +1402,18 @@ int icw_process_batch(icw_ctx *c, const void *in, size_t in_stride, void *out, s
 {
     if (!c) return ICW_EINVAL;
     return icw_process_streams(c, 0, c->n_streams, in, in_stride, out, out_stride, n_frames, flags, dbg, hip_stream);
+}
+
+int icw_host_alloc(size_t bytes, void **p)
+{
+    if (!p || !bytes) return ICW_EINVAL;
+    *p = nullptr;
+    return hipHostMalloc(p, bytes, hipHostMallocDefault) == hipSuccess ? ICW_OK : ICW_ENOMEM;
+}
+
+int icw_host_free(void *p)
+{
+    return (!p || hipHostFree(p) == hipSuccess) ? ICW_OK : ICW_EINVAL;
 }
 
 int icw_synchronize(icw_ctx *c)

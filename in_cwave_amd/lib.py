@@ -64,6 +64,38 @@ def _ptr(x):
     raise TypeError(type(x))
 
 
+class _HostBuffer:
+    """owner of an icw_host_alloc block; freed when the last array view over it goes away"""
+
+    def __init__(self, nbytes):
+        p = C.c_void_p()
+        _check(load().icw_host_alloc(nbytes, C.byref(p)), "icw_host_alloc")
+        self.ptr = p.value
+
+    def __del__(self):
+        if self.ptr and _lib is not None:
+            _lib.icw_host_free(self.ptr)
+            self.ptr = None
+
+
+class HostArray(np.ndarray):
+    """a numpy array over an icw_host_alloc block; the block lives as long as the array or any view"""
+    _icw_owner = None
+
+
+def host_array(shape, dtype=np.uint8):
+    """a numpy array in pinned host memory (icw_host_alloc): as a call's in / out buffer its copies
+    run block by block beside the kernels"""
+    dt = np.dtype(dtype)
+    n = max(1, int(np.prod(shape)) * dt.itemsize)
+    owner = _HostBuffer(n)
+    buf = (C.c_uint8 * n).from_address(owner.ptr)
+    a = np.frombuffer(buf, dtype=np.uint8, count=int(np.prod(shape)) * dt.itemsize).view(dt).reshape(shape)
+    a = a.view(HostArray)
+    a._icw_owner = owner
+    return a
+
+
 class Context:
     """One icw_ctx: n_streams streams sharing a config and a DSP list, state resident in HBM."""
 

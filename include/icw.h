@@ -184,8 +184,9 @@ int icw_set_input(icw_ctx *ctx, uint32_t sample_rate, uint32_t fmt, uint32_t cha
  *         in cfg->in_format (what xwave_read_samples leaves in xr->tbuff).
  *   out : stream s starts at (char*)out + s*out_stride_bytes, interleaved L,R, 2 or 3 bytes LE.
  *   dbg : ICW_F_DEBUG_PRE only -- double[n_streams][n_frames][2] pre-render values (lOut,rOut).
- * Host pointers are staged through pinned buffers; with ICW_F_DEVICE_PTRS nothing crosses
- * PCIe.  hip_stream: the hipStream_t the call is ordered on (it starts after the work queued there,
+ * Host pointers are staged through pinned buffers; host buffers that are pinned themselves
+ * (icw_host_alloc, hipHostMalloc, hipHostRegister) are copied block by block on a copy stream,
+ * beside the kernels of the other launch blocks.  With ICW_F_DEVICE_PTRS nothing crosses PCIe.  hip_stream: the hipStream_t the call is ordered on (it starts after the work queued there,
  * and the stream's later work sees its results; the call returns before the kernels finish).
  * NULL: with host pointers the context's own stream (the call returns when its output is in
  * `out`); with ICW_F_DEVICE_PTRS the legacy default stream (stream 0, torch's default stream): the
@@ -200,6 +201,10 @@ int icw_process_streams(icw_ctx *ctx, int first, int count, const void *in,
                         int n_frames, unsigned flags, void *dbg, void *hip_stream);
 
 int icw_synchronize(icw_ctx *ctx);
+/* Pinned (page-locked) host memory for a call's in / out buffers: their copies then overlap the
+ * kernels (cudaMallocHost-style helper; the reference's buffers are the caller's own).  0 / ICW_ENOMEM. */
+int icw_host_alloc(size_t bytes, void **p);
+int icw_host_free(void *p);
 /* Meters of stream s (amod_get_clips_peaks, adv_modulator.c:445-465).  reset != 0 clears the clip
  * counters and peaks FIRST, as the reference does, so the call returns 0 clips and
  * ICW_SR_ZERO_SIGNAL_DB peaks; the de-subnorm count is not reset (mod_context_get_desubnorm_counter,
