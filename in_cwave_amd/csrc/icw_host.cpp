@@ -51,6 +51,7 @@ double u2d(unsigned long long u)
 constexpr int kMaxBlockFrames = 1 << 16;
 constexpr int kDefBlockFrames = 1 << 14;   /* launch block: shorter pipeline fill / drain */
 constexpr int kSets = 3;                    /* most block scratch sets (ICW_SETS); default 2 */
+constexpr double kAutoTaper = 0.85;          /* tail block ratio where the taper is on by default */
 constexpr int kRowRenderMax = 2048;          /* channels up to which the render runs a row per channel */
 constexpr size_t kPinnedStage = 1u << 20;   /* host-pointer calls up to this size stage through pinned memory */
 
@@ -120,12 +121,13 @@ struct icw_ctx {
     int max_sets = 2;                     /* ICW_SETS: block scratch sets (2..kSets) */
     /* block schedule of long calls (plan_blocks): a short first block (the pipeline fill is K0 of
      * block 0 alone: C3 +2.5 %, C4 +1.4 %) and an optional geometric tail (the drain is K2 / K3 of
-     * the last block alone).  The tail is off by default: it pays only if K0 + K2 of a block fit
-     * beside K1 of a block r times shorter, and in C3 / C4 they take 0.87 / 0.94 of K1's time per
-     * frame -- r = 0.85 measured C3 -4 %, C4 -8 %, and r >= 0.9 leaves no room for a tail in a
-     * 2^18-frame call.  C5's drain is the serial render's, which a tail does not shorten. */
+     * the last block alone).  The tail pays only if K0 + K2 (and K3) of a block fit beside K1 of a
+     * block r times shorter: in C3 / C4 they take 0.87 / 0.94 of K1's time per frame, and r = 0.85
+     * measured C3 -4 %, C4 -8 %; in C5 (K1r, K2 0.12 and the row render K3r 0.64 of K1r on their own
+     * streams) r = 0.85 measured +2 %.  So it is on by default for the row kernel with a serial
+     * render only (icw_process_streams). */
     int first_block = 4096;               /* ICW_FIRST_BLOCK (0: uniform blocks) */
-    double taper = 0.0;                   /* ICW_TAPER: tail block ratio (0: no tail) */
+    double taper = -1.0;                  /* ICW_TAPER: tail block ratio (0: no tail; -1: auto) */
     int taper_min = 1024;                 /* ICW_TAPER_MIN: smallest tail block */
     /* dither generation (K3a) runs on its own stream, double-buffered like the block scratch */
     hipStream_t stream3 = nullptr;
@@ -964,8 +966,30 @@ int icw_process_streams(icw_ctx *c, int first, int count, const void *in, size_t
     const size_t S = (size_t)count;
     if (!dev && (in_stride < (size_t)n_frames * fsz || out_stride < (size_t)n_frames * osz)) return ICW_EINVAL;
 
+    const bool cw = cfg.in_format >= ICW_FMT_CW_F64;
+    const bool bus = c->prog.is_bus;
+    /* mono dedup: every stream of the call known to hold identical left / right converters */
+    const bool fcm = c->cfg.fp_check != 0;                /* FP_CHECK: FC() kernels, no shortcuts */
+    bool dedup = !cw && !fcm && nch == 1 && c->dedup_ok && (c->k1_mode <= 0 || c->k1_mode == 3);   /* plain / row K1 */
+    for (int i = 0; dedup && i < count; ++i) dedup = c->lr_known[first + i] != 0;
+    /* K1 variant of this call.  Auto: the row-broadcast kernel (4 chains per wave, ~17 % fewer
+     * instructions per sample) when its waves fit k1_wpc per CU on at most half the chip, else the
+     * lane-per-chain kernel (64 chains per wave).  The row kernel needs Kahan + the reject.  (Round
+     * 1 kept it off with a serial render; with the partition working, C5 gains 9 % from it.) */
+    const int row_waves = (int)(((dedup ? count : 2L * count) + 3) / 4) * 2;
+    const bool row_ok = cfg.iir_kahan && cfg.iir_subnorm_reject;
+    int k1_mode = c->k1_mode;
+    if (k1_mode < 0) k1_mode = (row_ok && row_waves <= (c->n_cu / 2) * c->k1_wpc) ? 3 : 0;
+    if (k1_mode == 3 && !row_ok) k1_mode = 0;
+    if (fcm) k1_mode = ICW_K1_FC;
+    if (!cw) c->last_k1 = k1_mode;
+    /* launch blocks.  The tail taper (plan_blocks) is on by default where it fits: a small batch
+     * (the row kernel K1r) with a serial render -- its drain is the render of the last block, and
+     * the frame-parallel kernels take well under K1r's time per frame (C5: +2 %).  Large batches
+     * keep uniform blocks (K0 + K2 take ~0.9 of K1's time there), ICW_TAPER overrides. */
     const int Tb = std::min(n_frames, c->max_block);
-    const std::vector<std::pair<int, int>> blocks = plan_blocks(n_frames, Tb, c->first_block, c->taper, c->taper_min);
+    const double taper = c->taper >= 0.0 ? c->taper : ((!cw && k1_mode == 3 && c->serial_render) ? kAutoTaper : 0.0);
+    const std::vector<std::pair<int, int>> blocks = plan_blocks(n_frames, Tb, c->first_block, taper, c->taper_min);
     const int n_blocks = (int)blocks.size();
 
     const unsigned char *d_in;
@@ -1037,23 +1061,6 @@ int icw_process_streams(icw_ctx *c, int first, int count, const void *in, size_t
     if (c->serial_render && !d_pre)
         for (int p = 0; p < n_sets; ++p)
             if (grow((void **)&c->rpre[p], &c->rpre_bytes[p], S * (size_t)Tb * 2 * sizeof(double))) return ICW_ENOMEM;
-    const bool cw = cfg.in_format >= ICW_FMT_CW_F64;
-    const bool bus = c->prog.is_bus;
-    /* mono dedup: every stream of the call known to hold identical left / right converters */
-    const bool fcm = c->cfg.fp_check != 0;                /* FP_CHECK: FC() kernels, no shortcuts */
-    bool dedup = !cw && !fcm && nch == 1 && c->dedup_ok && (c->k1_mode <= 0 || c->k1_mode == 3);   /* plain / row K1 */
-    for (int i = 0; dedup && i < count; ++i) dedup = c->lr_known[first + i] != 0;
-    /* K1 variant of this call.  Auto: the row-broadcast kernel (4 chains per wave, ~17 % fewer
-     * instructions per sample) when its waves fit k1_wpc per CU on at most half the chip, else the
-     * lane-per-chain kernel (64 chains per wave).  The row kernel needs Kahan + the reject.  (Round
-     * 1 kept it off with a serial render; with the partition working, C5 gains 9 % from it.) */
-    const int row_waves = (int)(((dedup ? count : 2L * count) + 3) / 4) * 2;
-    const bool row_ok = cfg.iir_kahan && cfg.iir_subnorm_reject;
-    int k1_mode = c->k1_mode;
-    if (k1_mode < 0) k1_mode = (row_ok && row_waves <= (c->n_cu / 2) * c->k1_wpc) ? 3 : 0;
-    if (k1_mode == 3 && !row_ok) k1_mode = 0;
-    if (fcm) k1_mode = ICW_K1_FC;
-    if (!cw) c->last_k1 = k1_mode;
     /* the shared rotation table pays from two streams on; one stream computes its factors inline */
     const bool table = c->prog.needs_omega && !bus && c->prog.n_trig > 0 && count > 1;
     if (table && grow((void **)&c->trig, &c->trig_bytes, (size_t)Tb * 2 * c->prog.n_trig * sizeof(double)))
