@@ -85,6 +85,16 @@ WORKLOADS = {
                bytes=14, desc="C5: 256 x 192kHz float32 stereo streams/GPU, Hilbert + Master, 24-bit TPDF + "
                               "MEW44 noise shaping"),
 }
+# The same configs through the FIR Hilbert converter (icw_set_fir_hilbert) with the tap counts
+# BASELINE.json names (255 / 511 / 1023 taps = order 254 / 510 / 1022, Kaiser beta 8) instead of the
+# reference's quadrature IIR: the converter a CWAVE header records (cwave.h:56-58), run on the fly.
+# Reported under other_workloads only; the headline stays the reference's own IIR path.
+FIR_BETA = 8.0
+for _w, _order in (("c2", 254), ("c3", 510), ("c4", 254), ("c5", 1022)):
+    _d = WORKLOADS[_w]["desc"].replace("Type-1 (order 19) Kahan quadrature Hilbert", "Hilbert")
+    _d = _d.replace("streams/GPU, PM", "streams/GPU, Hilbert + PM")
+    WORKLOADS[_w + "fir"] = dict(WORKLOADS[_w], fir=_order,
+                                 desc=_d.replace("Hilbert", f"{_order + 1}-tap FIR Hilbert (Kaiser beta {FIR_BETA:g})", 1))
 IIR_ORDER = 19                  # Type-1 filter of every workload (hblpf.c:740-820)
 
 
@@ -204,6 +214,8 @@ def _cpu_worker(args):
     cfg, nodes, fmt = workload_config(w)
     raw = synth.stream_pcm(s, n_frames, w["fs"], channels=w["ch"], fmt=fmt)
     st = O.Stream(cfg, nodes)
+    if w.get("fir"):
+        st.set_fir(w["fir"], FIR_BETA)
     t0 = time.perf_counter()
     st.process(raw, n_frames)
     return time.perf_counter() - t0
@@ -315,6 +327,32 @@ def measure_c1(steps, warmup, block, with_cpu):
 
 
 # ----------------------------------------------------------------------------- GPU leg ------
+def fir_roofline(W, S, T, kf_ms, kf_n, k2_ms, k2_n):
+    """roofline of the FIR converter KF (icw_fir_hilbert) per launch, from its HIP events: per
+    channel-sample nt taps x (1 subtract + 1 FMA = 3 flops) and 2 LDS reads of 8 B; its HBM bytes
+    are the raw input (read) and the I/Q rows it hands to K2 (4 x 8 B per frame, written)"""
+    M = W["fir"]
+    nt = (M // 2 + 1) // 2
+    chans = 1 if W["ch"] == 1 else 2
+    frames_per_launch = float(S) * T / max(1, kf_n)
+    avg_s = kf_ms / 1e3 / max(1, kf_n)
+    flops_per_frame = chans * nt * 3
+    in_b = {"i16": 2, "f32": 4}[W["fmt"]] * W["ch"]
+    kbytes = in_b + 32
+    tf = flops_per_frame * frames_per_launch / avg_s / 1e12 if avg_s > 0 else None
+    gbs = kbytes * frames_per_launch / avg_s / 1e9 if avg_s > 0 else None
+    lds_tbs = chans * nt * 16 * frames_per_launch / avg_s / 1e12 if avg_s > 0 else None
+    return {"bound": "fp64", "achieved": tf, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+            "frac": (tf / FP64_PEAK_TFLOPS) if tf else None, "traffic": None, "kernel": "icw_fir_hilbert",
+            "fir_order": M, "taps_odd": nt, "flops_per_frame": flops_per_frame, "frames_per_launch": frames_per_launch,
+            "avg_launch_ms": avg_s * 1e3, "output_kernel_avg_launch_ms": k2_ms / max(1, k2_n),
+            "hbm": {"achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": (gbs / HBM_PEAK_GBS) if gbs else None,
+                    "kernel_bytes_per_frame": kbytes},
+            "lds_read_tbs": lds_tbs,
+            "note": "FIR Hilbert converter KF: per channel-sample nt odd taps, each 2 LDS reads + subtract + FMA; "
+                    "frame-parallel (no recurrence), so it fills the chip"}
+
+
 def measure_gpu(wname, streams, frames, steps, warmup, e2e_steps, dev, local_dev, dist, rank, world):
     """one workload on this rank's device: W untimed steps, then K steps between barriers +
     synchronize, max over ranks; the K1 roofline from the HIP-event timing of the timed steps"""
@@ -328,6 +366,8 @@ def measure_gpu(wname, streams, frames, steps, warmup, e2e_steps, dev, local_dev
     fs = W["fs"]
     cfg, nodes, fmt = workload_config(W)
     ctx = L.Context(cfg, nodes, S, device=local_dev)
+    if W.get("fir"):
+        ctx.set_fir_hilbert(W["fir"], FIR_BETA)
     # synthetic input of the workload's shape for this rank's shard of streams (SURVEY 8(d)
     # generator); 16 distinct generated streams are tiled over the shard to bound setup time
     n_gen = min(S, 16)
@@ -393,6 +433,12 @@ def measure_gpu(wname, streams, frames, steps, warmup, e2e_steps, dev, local_dev
                "note": "host input and output in pinned memory (icw_host_alloc): H2D of each launch "
                        "block's input, the kernels and D2H of its output, the copies on a copy stream "
                        "beside the other blocks' kernels; one GPU"}
+
+    if W.get("fir"):
+        roof = fir_roofline(W, S, T, k1_ms, k1_n, k2_ms, k2_n)
+        ctx.close()
+        return {"value": value, "ms_per_step": ms_per_step, "roofline": roof, "e2e": e2e, "W": W, "S": S, "T": T,
+                "fs": fs}
 
     # ---- roofline of the dominant kernel K1 (the serial recurrence), per launch, from HIP events
     # recorded on the stream K1 runs on (icw_last_timing)
@@ -490,7 +536,7 @@ def main():
         others = {}
         import gc
         import torch
-        for w in os.environ.get("ICW_BENCH_OTHERS", "c3,c4,c5").split(","):
+        for w in os.environ.get("ICW_BENCH_OTHERS", "c3,c4,c5,c2fir,c3fir,c4fir,c5fir").split(","):
             gc.collect()
             torch.cuda.empty_cache()
             o = measure_gpu(w, None, None, 2, 1, 0, dev, local_dev, None, 0, 1)
@@ -500,6 +546,11 @@ def main():
                          "frames_per_stream_per_step": o["T"], "k1_kernel": ro["kernel"],
                          "k1_avg_launch_ms": ro["avg_launch_ms"], "k2_avg_launch_ms": ro["output_kernel_avg_launch_ms"],
                          "fp64_frac": ro["frac"]}
+            if o["W"].get("fir"):
+                others[w].update({"fir_kernel_avg_launch_ms": ro["avg_launch_ms"], "fir_tflops": ro["achieved"],
+                                  "fir_hbm_gbs": ro["hbm"]["achieved"]})
+                for k in ("k1_kernel", "k1_avg_launch_ms"):
+                    others[w].pop(k)
         try:
             c1 = measure_c1(1, 1, 576, True)
             others["c1"] = {k: c1[k] for k in ("value", "unit", "ms_per_step", "block_latency_us", "realtime_x",

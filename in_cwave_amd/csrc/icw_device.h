@@ -37,6 +37,30 @@ struct IcwK0Args {
     size_t x_pitch;
 };
 
+/* Arguments of the FIR Hilbert converter kernel (KF, the CWAVE converter of cwave.h:40,56-58:
+ * a Kaiser-windowed Hilbert FIR of order M = k_M, window parameter k_beta).  A workgroup owns
+ * ICW_FIR_TF output frames of one channel of one stream; it stages the inputs x[t - M .. t + TF)
+ * (unpacked and faded like K0, the M before the block from the history) in LDS and writes the
+ * analytic signal I = x[n - M/2], Q = sum_m g_m (x[n - M/2 - m] - x[n - M/2 + m]) into the complex
+ * rows K2 reads for CWAVE input. */
+#define ICW_FIR_TF     1024   /* output frames per FIR workgroup (256 lanes x 4) */
+#define ICW_FIR_MAX_M  4096   /* largest FIR order */
+struct IcwFirArgs {
+    const unsigned char *in;       /* stream s at in + s*in_stride */
+    size_t in_stride;
+    uint32_t fmt, csz, fsz, nch;   /* real sample format, channel/frame bytes, file channels */
+    int32_t n_streams, T;
+    long long t0;                  /* block offset into the call */
+    const long long *pos;          /* [n_streams] reader position at the call's start */
+    const long long *fade;         /* [n_streams][3] n_samples, n_fade_in, n_fade_out */
+    int32_t M, nt;                 /* order (even), odd taps m = 1, 3, .., 2nt-1 <= M/2 */
+    const double *g;               /* [nt] g_m = 2 w(m) / (pi m) */
+    const double *hist_in;         /* [n_streams][2][M] the channel's last M inputs, oldest first */
+    double *hist_out;              /* the same after this block (the other buffer) */
+    double *xd;                    /* [n_streams*4][x_pitch] rows s*4 + ch*2 + {0: I, 1: Q} */
+    size_t x_pitch;
+};
+
 /* Arguments of the call-end bookkeeping kernel: one thread per stream.  During a call every
  * kernel reads the call-start position / phases / frame counter and adds its block offset; this
  * kernel advances them once, after the last block. */

@@ -35,6 +35,7 @@ extern "C" hipError_t icw_launch_output(const IcwK2Args *a, int nord, int kahan,
 extern "C" hipError_t icw_launch_trig_table(const IcwTrigArgs *a, hipStream_t st);
 extern "C" hipError_t icw_launch_graph_serial(const IcwK4Args *a, hipStream_t st);
 extern "C" hipError_t icw_launch_advance(const IcwAdvArgs *a, hipStream_t st);
+extern "C" hipError_t icw_launch_fir(const IcwFirArgs *a, hipStream_t st);
 
 #define ICW_PI_H (3.1415926535897932384626433832795029)
 
@@ -177,6 +178,13 @@ struct icw_ctx {
     double last_ms[2]{};
     int last_launches[2]{};
     int last_k1 = -1;                     /* ICW_K1_* of the last real-input call */
+    /* FIR Hilbert converter (icw_set_fir_hilbert): order (0: the quadrature IIR), taps, and the
+     * per-stream input history [streams][2][M], double-buffered by launch block (fir_par) */
+    int fir_M = 0, fir_nt = 0;
+    double fir_beta = 0.0;
+    double *d_fir_g = nullptr;
+    double *fir_hist[2] = {};
+    int fir_par = 0;
     std::mutex mu;
 };
 
@@ -595,11 +603,36 @@ const CuSplit *cu_split(icw_ctx *c, int k1_cus)
     return &g_splits.back().second;
 }
 
+/* modified Bessel function I0 by its power series sum ((x/2)^k / k!)^2, to a relative 1e-17 */
+double bessel_i0(double x)
+{
+    const double h = x / 2.0;
+    double sum = 1.0, term = 1.0;
+    for (int k = 1; k < 1000; ++k) {
+        term *= h / (double)k;
+        const double t2 = term * term;
+        sum += t2;
+        if (t2 < sum * 1e-17) break;
+    }
+    return sum;
+}
+
+/* FIR histories of streams [f, f+n) to zero (a fresh or reset converter) */
+bool fir_clear(icw_ctx *c, size_t f, size_t n, hipStream_t st)
+{
+    bool ok = true;
+    const size_t row = 2 * (size_t)c->fir_M;
+    for (double *h : c->fir_hist)
+        if (h) ok &= hipMemsetAsync(h + f * row, 0, n * row * sizeof(double), st) == hipSuccess;
+    return ok;
+}
+
 void free_all(icw_ctx *c)
 {
     DevState &s = c->st;
     void *ptrs[] = {s.mt, s.mt_idx, s.rs, s.lr_equal, s.fes, s.err, s.hist, s.sncnt, s.hq_phase, s.pos, s.fade,
-                    s.n_frame, s.bus, s.clips, s.peak_bits, c->d_prog, c->trig, c->d_in, c->d_out, c->d_pre};
+                    s.n_frame, s.bus, s.clips, s.peak_bits, c->d_prog, c->trig, c->d_in, c->d_out, c->d_pre,
+                    c->d_fir_g, c->fir_hist[0], c->fir_hist[1]};
     for (void *p : ptrs)
         if (p) (void)hipFree(p);
     for (int p = 0; p < kSets; ++p) {
@@ -833,6 +866,7 @@ int icw_stream_init(icw_ctx *c, int first, int count)
     ok &= hipMemsetAsync(s.clips + f * 2, 0, n * 2 * sizeof(uint32_t), st) == hipSuccess;
     ok &= hipMemsetAsync(s.peak_bits + f * 2, 0, n * 2 * sizeof(unsigned long long), st) == hipSuccess;
     if (s.fes) ok &= hipMemsetAsync(s.fes + f * 4 * ICW_FES_PITCH, 0, n * 4 * ICW_FES_PITCH * 4, st) == hipSuccess;
+    ok &= fir_clear(c, f, n, st);
     /* no track open: n_samples "infinite", no fades (xwave_unpack_csample never fades) */
     std::vector<long long> fd(n * 3);
     for (size_t i = 0; i < n; ++i) { fd[i * 3] = (long long)1 << 62; fd[i * 3 + 1] = 0; fd[i * 3 + 2] = 0; }
@@ -884,6 +918,7 @@ int icw_stream_open(icw_ctx *c, int s, int64_t n_samples, uint32_t fade_in, uint
         ok &= hipMemset(c->st.hq_phase + (size_t)s * 2, 0, 2 * sizeof(uint32_t)) == hipSuccess;
         ok &= hipMemsetD32((hipDeviceptr_t)(c->st.lr_equal + (size_t)s * 2), 1, 2) == hipSuccess;
         c->lr_known[s] = 1;
+        ok &= fir_clear(c, (size_t)s, 1, c->stream) && hipStreamSynchronize(c->stream) == hipSuccess;
     }
     /* sound_render_set_outbits -> sound_render_recalc: prev_rnd, shaper buffers and prev_ns_err
      * reset, the RNG is not (sound_render.c:527-580) */
@@ -903,6 +938,57 @@ int icw_stream_reset_hilbert(icw_ctx *c, int s)
     ok &= hipMemset(c->st.hq_phase + (size_t)s * 2, 0, 2 * sizeof(uint32_t)) == hipSuccess;
     ok &= hipMemsetD32((hipDeviceptr_t)(c->st.lr_equal + (size_t)s * 2), 1, 2) == hipSuccess;
     c->lr_known[s] = 1;
+    ok &= fir_clear(c, (size_t)s, 1, c->stream) && hipStreamSynchronize(c->stream) == hipSuccess;
+    return ok ? ICW_OK : ICW_EDEVICE;
+}
+
+int icw_fir_taps(int32_t M, double beta, double *g, int n)
+{
+    if (M < 2 || M > ICW_FIR_MAX_ORDER || (M & 1) || !(beta >= 0.0 && beta < 1e3) || !g) return ICW_EINVAL;
+    const int c = M / 2, nt = (c + 1) / 2;
+    if (n < nt) return ICW_EINVAL;
+    const double i0b = bessel_i0(beta);
+    for (int k = 0; k < nt; ++k) {
+        const int m = 2 * k + 1;
+        const double r = (double)m / (double)c;
+        const double w = bessel_i0(beta * sqrt(1.0 - r * r)) / i0b;
+        g[k] = (2.0 / (ICW_PI_H * (double)m)) * w;
+    }
+    return nt;
+}
+
+int icw_set_fir_hilbert(icw_ctx *c, int32_t M, double beta)
+{
+    static_assert(ICW_FIR_MAX_ORDER == ICW_FIR_MAX_M, "FIR order limit of the header and the kernel");
+    if (!c || (M != 0 && (M < 2 || M > ICW_FIR_MAX_ORDER || (M & 1))) || !(beta >= 0.0 && beta < 1e3))
+        return ICW_EINVAL;
+    std::lock_guard<std::mutex> lk(c->mu);
+    if (set_dev(c) || quiesce(c) != hipSuccess) return ICW_EDEVICE;
+    for (double *&h : c->fir_hist)
+        if (h) { (void)hipFree(h); h = nullptr; }
+    if (c->d_fir_g) { (void)hipFree(c->d_fir_g); c->d_fir_g = nullptr; }
+    c->fir_M = c->fir_nt = 0;
+    c->fir_beta = 0.0;
+    c->fir_par = 0;
+    if (M == 0) return ICW_OK;
+    std::vector<double> g((size_t)(M / 2 + 1) / 2);
+    const int nt = icw_fir_taps(M, beta, g.data(), (int)g.size());
+    if (nt <= 0) return ICW_EINVAL;
+    const size_t hb = (size_t)c->n_streams * 2 * (size_t)M;
+    int rc = dalloc(&c->d_fir_g, (size_t)nt);
+    rc |= dalloc(&c->fir_hist[0], hb);
+    rc |= dalloc(&c->fir_hist[1], hb);
+    if (rc != ICW_OK || hipMemcpy(c->d_fir_g, g.data(), (size_t)nt * sizeof(double), hipMemcpyHostToDevice) != hipSuccess) {
+        for (double *&h : c->fir_hist)
+            if (h) { (void)hipFree(h); h = nullptr; }
+        if (c->d_fir_g) { (void)hipFree(c->d_fir_g); c->d_fir_g = nullptr; }
+        return rc == ICW_ENOMEM ? ICW_ENOMEM : ICW_EDEVICE;
+    }
+    c->fir_M = M;
+    c->fir_nt = nt;
+    c->fir_beta = beta;
+    bool ok = fir_clear(c, 0, (size_t)c->n_streams, c->stream);
+    ok &= hipStreamSynchronize(c->stream) == hipSuccess;
     return ok ? ICW_OK : ICW_EDEVICE;
 }
 
@@ -966,7 +1052,10 @@ int icw_process_streams(icw_ctx *c, int first, int count, const void *in, size_t
     const size_t S = (size_t)count;
     if (!dev && (in_stride < (size_t)n_frames * fsz || out_stride < (size_t)n_frames * osz)) return ICW_EINVAL;
 
-    const bool cw = cfg.in_format >= ICW_FMT_CW_F64;
+    /* FIR Hilbert converter (icw_set_fir_hilbert): real input becomes complex samples in KF and
+     * the block continues as CWAVE input does */
+    const bool fir = c->fir_M > 0 && cfg.in_format < ICW_FMT_CW_F64;
+    const bool cw = cfg.in_format >= ICW_FMT_CW_F64 || fir;
     const bool bus = c->prog.is_bus;
     /* mono dedup: every stream of the call known to hold identical left / right converters */
     const bool fcm = c->cfg.fp_check != 0;                /* FP_CHECK: FC() kernels, no shortcuts */
@@ -1159,7 +1248,36 @@ int icw_process_streams(icw_ctx *c, int first, int count, const void *in, size_t
                 hipEventRecord(c->ev_io[b], sC) != hipSuccess || hipStreamWaitEvent(s0, c->ev_io[b], 0) != hipSuccess)
                 return ICW_EDEVICE;
         }
-        if (icw_launch_unpack(&a0, s0) != hipSuccess) return ICW_EDEVICE;
+        if (fir) {
+            /* KF reads the history buffer the previous block wrote (same stream, block order) */
+            IcwFirArgs af;
+            memset(&af, 0, sizeof(af));
+            af.in = a0.in;
+            af.in_stride = dis;
+            af.fmt = cfg.in_format;
+            af.csz = csz;
+            af.fsz = fsz;
+            af.nch = nch;
+            af.n_streams = count;
+            af.T = T;
+            af.t0 = t0;
+            af.pos = a0.pos;
+            af.fade = a0.fade;
+            af.M = c->fir_M;
+            af.nt = c->fir_nt;
+            af.g = c->d_fir_g;
+            const size_t hrow = 2 * (size_t)c->fir_M;
+            af.hist_in = c->fir_hist[c->fir_par] + f0 * hrow;
+            af.hist_out = c->fir_hist[c->fir_par ^ 1] + f0 * hrow;
+            c->fir_par ^= 1;
+            af.xd = a0.xd;
+            af.x_pitch = x_pitch;
+            if (timing && hipEventRecord(c->ev[4 * b], s0) != hipSuccess) return ICW_EDEVICE;
+            if (icw_launch_fir(&af, s0) != hipSuccess) return ICW_EDEVICE;
+            if (timing && hipEventRecord(c->ev[4 * b + 1], s0) != hipSuccess) return ICW_EDEVICE;
+        } else if (icw_launch_unpack(&a0, s0) != hipSuccess) {
+            return ICW_EDEVICE;
+        }
         if (hipEventRecord(c->k0done[p], s0) != hipSuccess) return ICW_EDEVICE;
         return ICW_OK;
     };
@@ -1213,7 +1331,7 @@ int icw_process_streams(icw_ctx *c, int first, int count, const void *in, size_t
             /* real input: K0(b + n_sets) reuses xd[p], which K1(b) read; queued before K2(b) it
              * runs beside K1(b+1) instead of between two recurrences */
             if (b + n_sets < n_blocks && (rc0 = launch_k0(b + n_sets)) != ICW_OK) return rc0;
-        } else if (timing) {
+        } else if (timing && !fir) {
             if (hipEventRecord(c->ev[4 * b], sA) != hipSuccess || hipEventRecord(c->ev[4 * b + 1], sA) != hipSuccess)
                 return ICW_EDEVICE;
         }
@@ -1512,11 +1630,12 @@ struct IcwBlob {
 };
 constexpr uint64_t kBlobMagic = 0x32574349ull;   /* "ICW2" */
 
-size_t icw_state_size(const icw_ctx *c) { return c ? sizeof(IcwBlob) : 0; }
+/* with the FIR Hilbert converter on, its history (2 x k_M doubles, oldest first) follows the blob */
+size_t icw_state_size(const icw_ctx *c) { return c ? sizeof(IcwBlob) + 2 * (size_t)c->fir_M * sizeof(double) : 0; }
 
 int icw_get_state(icw_ctx *c, int s, void *blob, size_t size)
 {
-    if (!c || !blob || size < sizeof(IcwBlob) || s < 0 || s >= c->n_streams) return ICW_EINVAL;
+    if (!c || !blob || size < icw_state_size(c) || s < 0 || s >= c->n_streams) return ICW_EINVAL;
     std::lock_guard<std::mutex> lk(c->mu);
     if (set_dev(c)) return ICW_EDEVICE;
     IcwBlob b;
@@ -1541,6 +1660,11 @@ int icw_get_state(icw_ctx *c, int s, void *blob, size_t size)
         ok &= hipMemcpy(b.rs, c->st.rs + (size_t)s * 2 * ICW_RSTATE, sizeof(b.rs), hipMemcpyDeviceToHost) == hipSuccess;
     }
     b.n_samples = fd[0]; b.n_fade_in = fd[1]; b.n_fade_out = fd[2];
+    if (c->fir_M) {
+        const size_t hrow = 2 * (size_t)c->fir_M;
+        ok &= hipMemcpy((unsigned char *)blob + sizeof(b), c->fir_hist[c->fir_par] + (size_t)s * hrow,
+                        hrow * sizeof(double), hipMemcpyDeviceToHost) == hipSuccess;
+    }
     if (!ok) return ICW_EDEVICE;
     memcpy(blob, &b, sizeof(b));
     return ICW_OK;
@@ -1548,7 +1672,7 @@ int icw_get_state(icw_ctx *c, int s, void *blob, size_t size)
 
 int icw_set_state(icw_ctx *c, int s, const void *blob, size_t size)
 {
-    if (!c || !blob || size < sizeof(IcwBlob) || s < 0 || s >= c->n_streams) return ICW_EINVAL;
+    if (!c || !blob || size < icw_state_size(c) || s < 0 || s >= c->n_streams) return ICW_EINVAL;
     IcwBlob b;
     memcpy(&b, blob, sizeof(b));
     if (b.magic != kBlobMagic || b.nord != (uint32_t)c->nord || b.has_render != (c->serial_render ? 1u : 0u))
@@ -1574,6 +1698,11 @@ int icw_set_state(icw_ctx *c, int s, const void *blob, size_t size)
             ok &= hipMemcpy2D(c->st.mt + (size_t)s * 2 + ch, G * 4, b.mt[ch], 4, 4, 624, hipMemcpyHostToDevice) == hipSuccess;
         ok &= hipMemcpy(c->st.mt_idx + (size_t)s * 2, b.mt_idx, sizeof(b.mt_idx), hipMemcpyHostToDevice) == hipSuccess;
         ok &= hipMemcpy(c->st.rs + (size_t)s * 2 * ICW_RSTATE, b.rs, sizeof(b.rs), hipMemcpyHostToDevice) == hipSuccess;
+    }
+    if (c->fir_M) {
+        const size_t hrow = 2 * (size_t)c->fir_M;
+        ok &= hipMemcpy(c->fir_hist[c->fir_par] + (size_t)s * hrow, (const unsigned char *)blob + sizeof(b),
+                        hrow * sizeof(double), hipMemcpyHostToDevice) == hipSuccess;
     }
     return ok ? ICW_OK : ICW_EDEVICE;
 }

@@ -152,6 +152,88 @@ __global__ __launch_bounds__(256) void icw_unpack_frames(IcwK0Args a)
     }
 }
 
+/* FIR Hilbert converter (KF): real PCM -> the analytic signal a CWAVE file holds (cwave.h:40,56-58:
+ * "Hilbert FIR filter order" k_M, "filter parameter" k_beta; the converter itself is not part of
+ * in_cwave).  Order M (even, M + 1 taps), centre c = M/2, odd taps only:
+ *     I[n] = x[n - c],   Q[n] = sum_{m = 1, 3, .., <= c} g_m * (x[n - c - m] - x[n - c + m])
+ * with the sum taken in ascending m as acc = fma(g_m, d_m, acc) from +0.0 -- the oracle's order, so
+ * the result is bit-identical.  x is the unpacked, faded input of K0 (xwave_unpack_csample,
+ * xwave_reader.c:908-936), mono feeding R with L.  The workgroup stages x[tt - M, tt + TF) of its
+ * channel in LDS (coalesced loads; the M inputs before the block come from the history) and each
+ * lane sums 4 outputs 256 frames apart, so every LDS read of a wave is 64 consecutive doubles
+ * (conflict-free ds_read_b64) and the tap g_m is a scalar load shared by the wave.  Per output
+ * and tap: 2 LDS reads, one subtract, one FMA.  The block's last M inputs go to the other history
+ * buffer (read and write buffers differ, so the workgroups of a stream never race). */
+__global__ __launch_bounds__(256) void icw_fir_hilbert(IcwFirArgs a)
+{
+    extern __shared__ double xs[];                   /* xs[i] = x[tt - M + i], i < TF + M; then the taps */
+    constexpr int R = ICW_FIR_TF / 256;
+    const int ch = blockIdx.y, s = blockIdx.z;
+    const int tt = blockIdx.x * ICW_FIR_TF;
+    const int T = a.T, M = a.M, c = M >> 1;
+    const int nf = min(ICW_FIR_TF, T - tt);
+    const unsigned char *src = a.in + (size_t)s * a.in_stride + (size_t)ch * a.csz;
+    const long long p0 = a.pos[s] + a.t0;
+    const long long ns = a.fade[s * 3 + 0], fi = a.fade[s * 3 + 1], fo = a.fade[s * 3 + 2];
+    const double *hin = a.hist_in + ((size_t)s * 2 + ch) * M;
+    double *hout = a.hist_out + ((size_t)s * 2 + ch) * M;
+    const bool mono = a.nch == 1;                    /* R = L: its history follows L's */
+    for (int i = threadIdx.x; i < nf + M; i += 256) {
+        const int j = tt - M + i;                    /* frame index in the block */
+        double v;
+        if (j < 0) {
+            v = hin[M + j];
+        } else {
+            v = icw_unpack(src + (size_t)j * a.fsz, a.fmt);
+            const double fd = icw_fade(p0 + j, ns, fi, fo);
+            if (fd >= 0.0) v *= fd;
+        }
+        xs[i] = v;
+        /* history after the block: inputs [T - M, T), each written by the tile that owns it (the
+         * ones before the block, when T < M, by tile 0) */
+        if (j >= T - M && (j >= tt || tt == 0)) {
+            hout[j - (T - M)] = v;
+            if (mono) hout[M + j - (T - M)] = v;
+        }
+    }
+    /* the taps, after the staged inputs (a broadcast LDS read per tap: the compiler cannot keep
+     * them in scalar loads, the workgroup writes memory) */
+    double *gs = xs + ICW_FIR_TF + M;
+    for (int k = threadIdx.x; k < a.nt; k += 256) gs[k] = a.g[k];
+    __syncthreads();
+
+    double acc[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) acc[r] = 0.0;
+    const int base = threadIdx.x + M - c;            /* LDS index of x[tt + lane - c] */
+#pragma unroll 1
+    for (int k = 0; k < a.nt; ++k) {
+        const int m = 2 * k + 1;
+        const double gm = gs[k];
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const int i = base + 256 * r;
+            acc[r] = __builtin_fma(gm, xs[i - m] - xs[i + m], acc[r]);
+        }
+    }
+
+    double *rowI = a.xd + ((size_t)s * 4 + ch * 2) * a.x_pitch + tt;
+    double *rowQ = rowI + a.x_pitch;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const int f = threadIdx.x + 256 * r;
+        if (f < nf) {
+            const double vi = xs[f + M - c];
+            rowI[f] = vi;
+            rowQ[f] = acc[r];
+            if (mono) {
+                rowI[f + 2 * a.x_pitch] = vi;
+                rowQ[f + 2 * a.x_pitch] = acc[r];
+            }
+        }
+    }
+}
+
 
 /* ------------------------------------------------------------- output kernel (K2) ------- */
 struct IcwLR { double lre, lim, rre, rim; };
@@ -1621,6 +1703,16 @@ extern "C" hipError_t icw_launch_unpack(const IcwK0Args *a, hipStream_t st)
 {
     dim3 grid((a->T + 255) / 256, a->n_streams);
     hipLaunchKernelGGL(icw_unpack_frames, grid, dim3(256), a->lds_guard, st, *a);
+    return hipGetLastError();
+}
+
+extern "C" hipError_t icw_launch_fir(const IcwFirArgs *a, hipStream_t st)
+{
+    if (a->M < 2 || a->M > ICW_FIR_MAX_M || (a->M & 1) || a->nt < 1 || 2 * a->nt - 1 > a->M / 2)
+        return hipErrorInvalidValue;
+    dim3 grid((a->T + ICW_FIR_TF - 1) / ICW_FIR_TF, a->nch > 1 ? 2 : 1, a->n_streams);
+    const size_t lds = (size_t)(ICW_FIR_TF + a->M + a->nt) * sizeof(double);
+    hipLaunchKernelGGL(icw_fir_hilbert, grid, dim3(256), lds, st, *a);
     return hipGetLastError();
 }
 

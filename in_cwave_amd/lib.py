@@ -134,6 +134,11 @@ class Context:
         _check(self._lib.icw_set_input(self.h, sample_rate, fmt, channels), "icw_set_input")
         self.fsz = abi.FMT_BYTES[fmt] * channels
 
+    def set_fir_hilbert(self, order, beta=8.0):
+        """icw_set_fir_hilbert: real input through the FIR Hilbert converter (order k_M, Kaiser
+        beta k_beta, cwave.h:56-58) instead of the quadrature IIR; order 0 restores the IIR"""
+        _check(self._lib.icw_set_fir_hilbert(self.h, order, beta), "icw_set_fir_hilbert")
+
     def stream_open(self, s, n_samples, fade_in_ms=0, fade_out_ms=0, sec_align=0, clr_nframe=0, clr_hilb=0):
         _check(self._lib.icw_stream_open(self.h, s, n_samples, fade_in_ms, fade_out_ms, sec_align,
                                          clr_nframe, clr_hilb), "icw_stream_open")
@@ -206,6 +211,15 @@ class Context:
         n = (C.c_int * 2)()
         _check(self._lib.icw_last_timing(self.h, ms, n), "icw_last_timing")
         return (ms[0], ms[1]), (n[0], n[1])
+
+
+def fir_taps(order, beta=8.0):
+    """icw_fir_taps: the converter's taps g_m, m = 1, 3, .. (host arithmetic, no device call)"""
+    g = np.zeros((order // 2 + 1) // 2, dtype=np.float64)
+    nt = load().icw_fir_taps(order, beta, _ptr(g), g.size)
+    if nt < 0:
+        _check(nt, "icw_fir_taps")
+    return g
 
 
 # ------------------------------------------------------------------ CWAVE files / CRC-32 -------

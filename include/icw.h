@@ -179,6 +179,23 @@ int icw_stream_seek(icw_ctx *ctx, int s, int64_t frame_pos);
  * channels; applies to every stream of the context */
 int icw_set_input(icw_ctx *ctx, uint32_t sample_rate, uint32_t fmt, uint32_t channels);
 
+/* FIR Hilbert converter: the converter that CWAVE files record in their header (cwave.h:40,56-58:
+ * "Hilbert FIR filter order" k_M, "Hilbert FIR filter parameter" k_beta; gui_cwave.c:159-172 shows
+ * them; the converter program is not part of in_cwave).  With k_M > 0, real input is turned on the
+ * device into the analytic signal such a file would hold -- a Kaiser-windowed (beta = k_beta)
+ * Hilbert FIR of order k_M, odd taps m only, delay k_M/2:
+ *     I[n] = x[n - k_M/2],  Q[n] = sum_{m odd <= k_M/2} g_m (x[n - k_M/2 - m] - x[n - k_M/2 + m]),
+ *     g_m = 2 I0(beta sqrt(1 - (2m/k_M)^2)) / (pi m I0(beta)),  summed in ascending m with an FMA
+ * per tap -- and the block continues as CWAVE input does (no quadrature IIR; graph and render as
+ * for complex samples).  k_M = 0 restores the reference's own quadrature IIR Hilbert (the default).
+ * k_M even, 2..ICW_FIR_MAX_ORDER.  Every stream's FIR history (its last k_M inputs) starts at zero;
+ * icw_stream_init / icw_stream_reset_hilbert / icw_stream_open(clr_hilb) clear it too.
+ * No reference implementation exists for this stage: its parity is unpinned. */
+#define ICW_FIR_MAX_ORDER 4096
+int icw_set_fir_hilbert(icw_ctx *ctx, int32_t k_M, double k_beta);
+/* The taps of that design: g[k] = g_{2k+1}, k < nt = (k_M/2 + 1)/2.  Returns nt (or ICW_EINVAL). */
+int icw_fir_taps(int32_t k_M, double k_beta, double *g, int n);
+
 /* Process n_frames frames of every stream (the batched amod_process_samples).
  *   in  : stream s starts at (char*)in  + s*in_stride_bytes,  frames interleaved by channel
  *         in cfg->in_format (what xwave_read_samples leaves in xr->tbuff).

@@ -438,8 +438,19 @@ static int render_value(unsigned char **buf, double input, uint32_t *clips, doub
 /* ------------------------------------------------------------------- one stream ---------- */
 typedef struct { double lre, lim, rre, rim; } lrc;
 
+/* FIR Hilbert converter (icw_set_fir_hilbert; the CWAVE converter cwave.h:40,56-58 names by its
+ * order k_M and Kaiser parameter k_beta -- no reference implementation, parity unpinned).  Per
+ * channel a ring of the last M+1 inputs (newest at head). */
+#define ORC_FIR_MAX 4096
+typedef struct {
+    int M, nt, head;
+    double g[ORC_FIR_MAX / 4 + 1];
+    double x[2][ORC_FIR_MAX + 1];
+} orc_fir;
+
 typedef struct orc_stream {
     icw_config cfg;
+    orc_fir fir;
     orc_fes fes_hilb[2];               /* mc->fes_hilb_left / _right (in_cwave.c:72-79) */
     icw_node nodes[64];
     int n_nodes;
@@ -517,6 +528,70 @@ static unsigned fmt_size(unsigned fmt)
 {
     static const unsigned sz[9] = {1, 2, 3, 4, 4, 16, 4, 6, 8};
     return fmt < 9 ? sz[fmt] : 0;
+}
+
+/* I0(x) = sum_k ((x/2)^k / k!)^2 */
+static double orc_i0(double x)
+{
+    double half = x / 2.0, sum = 1.0, term = 1.0;
+    int k;
+    for (k = 1; k < 1000; ++k) {
+        double t2;
+        term *= half / (double)k;
+        t2 = term * term;
+        sum += t2;
+        if (t2 < sum * 1e-17) break;
+    }
+    return sum;
+}
+
+/* taps g[k] of odd tap m = 2k+1 <= M/2: 2 w(m) / (pi m), Kaiser w(m) = I0(beta sqrt(1-(m/c)^2)) / I0(beta) */
+int orc_fir_taps(int M, double beta, double *g, int n)
+{
+    int c = M / 2, nt = (c + 1) / 2, k;
+    double ib;
+    if (M < 2 || M > ORC_FIR_MAX || (M & 1) || n < nt || beta < 0.0) return -1;
+    ib = orc_i0(beta);
+    for (k = 0; k < nt; ++k) {
+        int m = 2 * k + 1;
+        double r = (double)m / (double)c;
+        g[k] = (2.0 / (ORC_PI * (double)m)) * (orc_i0(beta * sqrt(1.0 - r * r)) / ib);
+    }
+    return nt;
+}
+
+static void fir_reset(orc_fir *f)
+{
+    memset(f->x, 0, sizeof(f->x));
+    f->head = 0;
+}
+
+/* one input of channel ch -> (I, Q): I = x[n-c], Q = sum over odd m <= c of g_m (x[n-c-m] - x[n-c+m]),
+ * ascending m, one fma per tap from +0.0 */
+static void fir_process(orc_fir *f, int ch, double x, double *oI, double *oQ)
+{
+    int L = f->M + 1, c = f->M / 2, k;
+    double *r = f->x[ch];
+    int h = f->head;                                /* slot of x[n]; advanced after both channels */
+    double acc = 0.0;
+    r[h] = x;
+    for (k = 0; k < f->nt; ++k) {
+        int m = 2 * k + 1;
+        double a = r[((h - (c + m)) % L + L) % L], b = r[((h - (c - m)) % L + L) % L];
+        acc = fma(f->g[k], a - b, acc);
+    }
+    *oI = r[((h - c) % L + L) % L];
+    *oQ = acc;
+}
+
+int orc_set_fir(orc_stream *s, int M, double beta)
+{
+    if (M == 0) { s->fir.M = 0; return 0; }
+    if (orc_fir_taps(M, beta, s->fir.g, ORC_FIR_MAX / 4 + 1) < 0) return -1;
+    s->fir.M = M;
+    s->fir.nt = (M / 2 + 1) / 2;
+    fir_reset(&s->fir);
+    return 0;
 }
 
 /* amod_init normalisation (adv_modulator.c:216-331), shared with the product by semantics */
@@ -626,7 +701,10 @@ int64_t orc_stream_open(orc_stream *s, int64_t n_samples, uint32_t fade_in, uint
     }
     s->pos = 0;
     if (clr_nframe) s->n_frame = 0;
-    if (clr_hilb) for (int c = 0; c < 2; ++c) { iir_reset(&s->hq[c].I); iir_reset(&s->hq[c].Q); s->hq[c].k = 0; }
+    if (clr_hilb) {
+        for (int c = 0; c < 2; ++c) { iir_reset(&s->hq[c].I); iir_reset(&s->hq[c].Q); s->hq[c].k = 0; }
+        fir_reset(&s->fir);
+    }
     render_recalc(&s->rd[0]);
     render_recalc(&s->rd[1]);
     return n_tail;
@@ -706,6 +784,17 @@ int orc_process(orc_stream *s, const void *in, unsigned n_frames, void *out, dou
             if (nch > 1) unpack_iq(fp + csz, cfg->in_format, &b->rre, &b->rim);
             else { b->rre = b->lre; b->rim = b->lim; }
             if (fade >= 0.0) { b->lre *= fade; b->lim *= fade; b->rre *= fade; b->rim *= fade; }
+        } else if (s->fir.M) {
+            /* FIR Hilbert converter: the analytic signal of a CWAVE file, then as complex input */
+            double val = unpack1(fp, cfg->in_format);
+            if (fade >= 0.0) val *= fade;
+            fir_process(&s->fir, 0, val, &s->bus[0].lre, &s->bus[0].lim);
+            if (nch > 1) {
+                val = unpack1(fp + csz, cfg->in_format);
+                if (fade >= 0.0) val *= fade;
+            }
+            fir_process(&s->fir, 1, val, &s->bus[0].rre, &s->bus[0].rim);
+            s->fir.head = (s->fir.head + 1) % (s->fir.M + 1);
         } else {
             double val = unpack1(fp, cfg->in_format);
             if (fade >= 0.0) val *= fade;

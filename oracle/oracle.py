@@ -52,6 +52,10 @@ def load():
         lib.orc_hilbert_block.argtypes = [C.c_int, C.c_int, C.c_int, vp, C.c_int, vp, vp]
         lib.orc_render_block.argtypes = [C.POINTER(abi.RenderCfg), C.c_int, C.c_uint32, vp, C.c_int, vp, vp,
                                          C.POINTER(C.c_uint32), C.POINTER(C.c_double)]
+        lib.orc_set_fir.restype = C.c_int
+        lib.orc_set_fir.argtypes = [vp, C.c_int, C.c_double]
+        lib.orc_fir_taps.restype = C.c_int
+        lib.orc_fir_taps.argtypes = [C.c_int, C.c_double, vp, C.c_int]
         lib.orc_mt_new.restype = vp
         lib.orc_mt_free.argtypes = [vp]
         lib.orc_mt_seed.argtypes = [vp, C.c_uint32]
@@ -92,6 +96,11 @@ class Stream:
     def set_mt(self, ch, words, idx):
         w = np.ascontiguousarray(words, dtype=np.uint32)
         load().orc_set_mt(self.h, ch, w.ctypes.data, idx)
+
+    def set_fir(self, order, beta):
+        """the FIR Hilbert converter (icw_set_fir_hilbert); order 0: the quadrature IIR"""
+        if load().orc_set_fir(self.h, order, beta) != 0:
+            raise ValueError("bad FIR order / beta")
 
     def set_input(self, sample_rate, fmt, channels):
         load().orc_set_input(self.h, sample_rate, fmt, channels)
@@ -189,12 +198,24 @@ class MT:
         return self.lib.orc_mt_dsopen(self.h)
 
 
-def process_streams(cfg, nodes, raw, n_frames, want_pre=False, n_samples=None, census=None):
+def fir_taps(order, beta):
+    """the oracle's own taps g_m (m = 1, 3, ..) of the FIR Hilbert converter"""
+    g = np.zeros((order // 2 + 1) // 2, dtype=np.float64)
+    nt = load().orc_fir_taps(order, beta, g.ctypes.data, g.size)
+    if nt < 0:
+        raise ValueError("bad FIR order / beta")
+    return g
+
+
+def process_streams(cfg, nodes, raw, n_frames, want_pre=False, n_samples=None, census=None, fir=None):
     """Run every row of raw [S, bytes] through its own fresh oracle stream.  census (a list):
-    receives each stream's FP-exception census [4, 7]."""
+    receives each stream's FP-exception census [4, 7].  fir: (order, beta) of the FIR Hilbert
+    converter."""
     outs, pres = [], []
     for s in range(raw.shape[0]):
         st = Stream(cfg, nodes)
+        if fir:
+            st.set_fir(*fir)
         if n_samples is not None:
             st.open(n_samples)
         o, p = st.process(raw[s], n_frames, want_pre)

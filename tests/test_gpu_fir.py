@@ -1,0 +1,170 @@
+"""GPU parity of the FIR Hilbert converter (icw_set_fir_hilbert, kernel KF `icw_fir_hilbert`)
+against the oracle's restatement (oracle/icw_oracle.c fir_process): pre-render doubles and
+rendered bytes bit for bit.
+
+The converter is the one CWAVE headers name (cwave.h:40,56-58, k_M / k_beta); in_cwave does not
+ship it, so the oracle is pinned only by the design's definition (tests/test_fir.py: scipy's
+Kaiser window, numpy convolution, the analytic-signal property) -- parity unpinned against any
+reference output.  After the converter the block runs the CWAVE path (graph, render), which
+tests/test_gpu_cwave_graph.py checks against the reference restatement.
+"""
+import numpy as np
+import pytest
+
+from in_cwave_amd import abi, graph, synth
+
+from test_gpu_parity import assert_parity
+
+pytestmark = pytest.mark.gpu
+
+BETA = 8.0
+
+
+def run_fir(oracle, icw, cfg, nodes, raw, n_frames, order, beta=BETA, blocks=None):
+    ctx = icw.Context(cfg, nodes, raw.shape[0])
+    ctx.set_fir_hilbert(order, beta)
+    if blocks is None:
+        out, pre = ctx.process(raw, n_frames, want_pre=True)
+    else:
+        outs, pres, t = [], [], 0
+        for b in blocks:
+            o, p = ctx.process(np.ascontiguousarray(raw[:, t * ctx.fsz:(t + b) * ctx.fsz]), b, want_pre=True)
+            outs.append(o)
+            pres.append(p)
+            t += b
+        out, pre = np.concatenate(outs, axis=1), np.concatenate(pres, axis=1)
+    ref_out, ref_pre = oracle.process_streams(cfg, nodes, raw, n_frames, want_pre=True, fir=(order, beta))
+    return ctx, out, pre, ref_out, ref_pre
+
+
+@pytest.mark.parametrize("order", [2, 30, 254, 510, 1022])
+@pytest.mark.parametrize("fmt,ch", [(abi.FMT_I16, 2), (abi.FMT_F32, 2), (abi.FMT_U8, 1), (abi.FMT_I24, 2),
+                                    (abi.FMT_I32, 1)])
+def test_fir_formats_shift_master(oracle, icw, order, fmt, ch):
+    cfg = graph.default_config(48000, fmt=fmt, channels=ch)
+    raw = synth.batch_pcm(3, 3000, 48000, channels=ch, fmt=fmt)
+    ctx, out, pre, ro, rp = run_fir(oracle, icw, cfg, graph.graph_shift_master(), raw, 3000, order)
+    assert_parity(out, pre, ro, rp)
+    ctx.close()
+
+
+@pytest.mark.parametrize("order", [30, 254, 1022])
+def test_fir_launch_blocks_and_calls(oracle, icw, order, monkeypatch):
+    """263-frame launch blocks (shorter than the 1022-order history) and ragged calls: the history
+    hand-off between blocks and calls is exact"""
+    monkeypatch.setenv("ICW_BLOCK", "263")
+    cfg = graph.default_config(44100)
+    raw = synth.batch_pcm(4, 5000, 44100)
+    ctx, out, pre, ro, rp = run_fir(oracle, icw, cfg, graph.graph_shift_master(), raw, 5000, order,
+                                    blocks=[100, 1, 577, 2322, 2000])
+    assert_parity(out, pre, ro, rp)
+    ctx.close()
+
+
+def test_fir_many_tiles_c4_graph(oracle, icw):
+    """several 1024-frame tiles per launch block, the PM -> Shift -> Mix -> Master list"""
+    cfg = graph.default_config(48000)
+    raw = synth.batch_pcm(6, 20000, 48000)
+    ctx, out, pre, ro, rp = run_fir(oracle, icw, cfg, graph.graph_pm_shift_mix(), raw, 20000, 254)
+    assert_parity(out, pre, ro, rp)
+    ctx.close()
+
+
+@pytest.mark.parametrize("order", [254, 1022])
+def test_fir_dithered_noise_shaped_24bit(oracle, icw, order):
+    """the C5 render (24-bit TPDF + MEW44) after the converter: serial render path"""
+    cfg = graph.default_config(192000, fmt=abi.FMT_F32, need24bits=True)
+    cfg.render.render_type = abi.RENDER_TPDF
+    cfg.render.nshape_type = abi.NSHAPE_MEW44
+    raw = synth.batch_pcm(3, 6000, 192000, fmt=abi.FMT_F32)
+    ctx, out, pre, ro, rp = run_fir(oracle, icw, cfg, graph.graph_master_only(), raw, 6000, order)
+    assert_parity(out, pre, ro, rp)
+    ctx.close()
+
+
+def test_fir_bus_form_graph(oracle, icw):
+    cfg = graph.default_config(48000)
+    raw = synth.batch_pcm(3, 3000, 48000)
+    ctx, out, pre, ro, rp = run_fir(oracle, icw, cfg, graph.graph_feedback_pm_shift(), raw, 3000, 30)
+    assert_parity(out, pre, ro, rp)
+    ctx.close()
+
+
+def test_fir_fades(oracle, icw):
+    cfg = graph.default_config(48000)
+    n = 30000
+    raw = synth.batch_pcm(2, n, 48000)
+    nodes = graph.graph_shift_master()
+    ctx = icw.Context(cfg, nodes, 2)
+    ctx.set_fir_hilbert(254, BETA)
+    for s in range(2):
+        ctx.stream_open(s, n, fade_in_ms=100, fade_out_ms=200)
+    out, pre = ctx.process(raw, n, want_pre=True)
+    for s in range(2):
+        st = oracle.Stream(cfg, nodes)
+        st.set_fir(254, BETA)
+        st.open(n, 100, 200)
+        ro, rp = st.process(raw[s], n, want_pre=True)
+        assert np.array_equal(pre[s].view(np.uint64), rp.view(np.uint64))
+        assert np.array_equal(out[s], ro)
+    ctx.close()
+
+
+def test_fir_mono_then_stereo_track(oracle, icw):
+    """a mono track then a stereo one without clearing the converter: R's history follows L's"""
+    cfg = graph.default_config(48000, channels=1)
+    nodes = graph.graph_shift_master()
+    mono = synth.batch_pcm(2, 1500, 48000, channels=1)
+    stereo = synth.batch_pcm(2, 1500, 48000, channels=2, first=7)
+    ctx = icw.Context(cfg, nodes, 2)
+    ctx.set_fir_hilbert(254, BETA)
+    o1, p1 = ctx.process(mono, 1500, want_pre=True)
+    ctx.set_input(48000, abi.FMT_I16, 2)
+    o2, p2 = ctx.process(stereo, 1500, want_pre=True)
+    for s in range(2):
+        st = oracle.Stream(cfg, nodes)
+        st.set_fir(254, BETA)
+        r1, q1 = st.process(mono[s], 1500, want_pre=True)
+        st.set_input(48000, abi.FMT_I16, 2)
+        r2, q2 = st.process(stereo[s], 1500, want_pre=True)
+        assert np.array_equal(p1[s].view(np.uint64), q1.view(np.uint64))
+        assert np.array_equal(p2[s].view(np.uint64), q2.view(np.uint64))
+        assert np.array_equal(o2[s], r2)
+    ctx.close()
+
+
+def test_fir_state_roundtrip(oracle, icw):
+    """checkpoint after 2500 frames (the FIR history travels in the state blob), resume in a new
+    context: the continuation equals an uninterrupted run"""
+    cfg = graph.default_config(48000)
+    nodes = graph.graph_shift_master()
+    raw = synth.batch_pcm(2, 5000, 48000)
+    full = icw.Context(cfg, nodes, 2)
+    full.set_fir_hilbert(510, BETA)
+    ref, refp = full.process(raw, 5000, want_pre=True)
+    a = icw.Context(cfg, nodes, 2)
+    a.set_fir_hilbert(510, BETA)
+    a.process(np.ascontiguousarray(raw[:, :2500 * 4]), 2500)
+    blobs = [a.get_state(s) for s in range(2)]
+    b = icw.Context(cfg, nodes, 2)
+    b.set_fir_hilbert(510, BETA)
+    for s in range(2):
+        b.set_state(s, blobs[s])
+    out, pre = b.process(np.ascontiguousarray(raw[:, 2500 * 4:]), 2500, want_pre=True)
+    assert np.array_equal(pre.view(np.uint64), refp[:, 2500:].view(np.uint64))
+    assert np.array_equal(out, ref[:, 2500 * 4:])
+    for c in (full, a, b):
+        c.close()
+
+
+def test_fir_off_restores_quadrature_iir(oracle, icw):
+    cfg = graph.default_config(48000)
+    nodes = graph.graph_shift_master()
+    raw = synth.batch_pcm(3, 2000, 48000)
+    ctx = icw.Context(cfg, nodes, 3)
+    ctx.set_fir_hilbert(254, BETA)
+    ctx.set_fir_hilbert(0, 0.0)
+    out, pre = ctx.process(raw, 2000, want_pre=True)
+    ro, rp = oracle.process_streams(cfg, nodes, raw, 2000, want_pre=True)
+    assert_parity(out, pre, ro, rp)
+    ctx.close()
