@@ -59,6 +59,7 @@ struct IcwFirArgs {
     double *hist_out;              /* the same after this block (the other buffer) */
     double *xd;                    /* [n_streams*4][x_pitch] rows s*4 + ch*2 + {0: I, 1: Q} */
     size_t x_pitch;
+    int32_t zero;                  /* always 0: keeps the lane's 4 output strides opaque (no LDS read pairing) */
 };
 
 /* Arguments of the call-end bookkeeping kernel: one thread per stream.  During a call every

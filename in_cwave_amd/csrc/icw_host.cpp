@@ -1217,6 +1217,7 @@ int icw_process_streams(icw_ctx *c, int first, int count, const void *in, size_t
     }
     const unsigned long long ssr = (unsigned long long)cfg.sample_rate * ICW_HZ_SCALE;
 
+    const bool fir_async = fir && sK != sA;
     /* K0 of block b on sA: xd[p] was last read by K1 of block b-2 (and, complex input, by K2 of
      * block b-2, which precedes it on sA) */
     auto launch_k0 = [&](int b) -> int {
@@ -1241,6 +1242,12 @@ int icw_process_streams(icw_ctx *c, int first, int count, const void *in, size_t
         a0.dedup = dedup ? 1 : 0;
         if (b >= n_sets && !cw && sK != sA && hipStreamWaitEvent(sA, c->k1done[p], 0) != hipSuccess) return ICW_EDEVICE;
         hipStream_t s0 = (b == 0 && sF) ? sF : sA;         /* the fill: nothing else runs yet */
+        /* the FIR converter runs on the caller's stream (K1's, idle without the IIR), so KF of the
+         * next block overlaps K2 of this one; it rewrites xd[p] after K2(b - n_sets) has read it */
+        if (fir_async) {
+            s0 = sK;
+            if (b >= n_sets && hipStreamWaitEvent(sK, c->k2done[p], 0) != hipSuccess) return ICW_EDEVICE;
+        }
         if (pipe_io) {
             /* this block's input slice of every stream, on the copy stream */
             if (hipMemcpy2DAsync(c->d_in + (size_t)t0 * fsz, dis, (const unsigned char *)in + (size_t)t0 * fsz, in_stride,
@@ -1406,6 +1413,7 @@ int icw_process_streams(icw_ctx *c, int first, int count, const void *in, size_t
         if (c->serial_render && b >= n_sets && sR != s2 && hipStreamWaitEvent(s2, c->k3done[p], 0) != hipSuccess)
             return ICW_EDEVICE;
         if (timing && hipEventRecord(c->ev[4 * b + 2], s2) != hipSuccess) return ICW_EDEVICE;
+        if (fir_async && hipStreamWaitEvent(s2, c->k0done[p], 0) != hipSuccess) return ICW_EDEVICE;
         if (icw_launch_output(&a2, N, cfg.iir_kahan, s2) != hipSuccess) return ICW_EDEVICE;
         if (hipEventRecord(c->k2done[p], s2) != hipSuccess) return ICW_EDEVICE;
         /* the serial part (K4, K3b) on sR after K2(b): it then overlaps K2(b+1) instead of

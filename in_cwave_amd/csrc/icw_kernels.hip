@@ -206,13 +206,17 @@ __global__ __launch_bounds__(256) void icw_fir_hilbert(IcwFirArgs a)
 #pragma unroll
     for (int r = 0; r < R; ++r) acc[r] = 0.0;
     const int base = threadIdx.x + M - c;            /* LDS index of x[tt + lane - c] */
+    /* the outputs' stride, opaque to the compiler: with a constant 256 it pairs the reads of two
+     * outputs into ds_read2st64_b64, which takes 8 LDS cycles per wave for what two ds_read_b64
+     * (2 cycles each, 64 consecutive doubles, conflict-free) deliver in 4 -- and KF is LDS-bound */
+    const int rs = 256 + a.zero;
 #pragma unroll 1
     for (int k = 0; k < a.nt; ++k) {
         const int m = 2 * k + 1;
         const double gm = gs[k];
 #pragma unroll
         for (int r = 0; r < R; ++r) {
-            const int i = base + 256 * r;
+            const int i = base + rs * r;
             acc[r] = __builtin_fma(gm, xs[i - m] - xs[i + m], acc[r]);
         }
     }
