@@ -36,6 +36,8 @@ extern "C" hipError_t icw_launch_trig_table(const IcwTrigArgs *a, hipStream_t st
 extern "C" hipError_t icw_launch_graph_serial(const IcwK4Args *a, hipStream_t st);
 extern "C" hipError_t icw_launch_advance(const IcwAdvArgs *a, hipStream_t st);
 extern "C" hipError_t icw_launch_fir(const IcwFirArgs *a, hipStream_t st);
+extern "C" hipError_t icw_launch_fir_graph(const IcwFirArgs *f, const IcwK2Args *a, hipStream_t st);
+extern "C" size_t icw_fir_graph_lds(int M, int nt, int nch, int n_regs);
 
 #define ICW_PI_H (3.1415926535897932384626433832795029)
 
@@ -118,6 +120,7 @@ struct icw_ctx {
     bool fill_drain = true;               /* ICW_FILL_DRAIN=0: first K0 / last K2 stay partitioned (A/B) */
     uint32_t lds_cu = 0;                  /* LDS bytes per CU a workgroup may hold */
     int max_block = kDefBlockFrames;      /* ICW_BLOCK: frames per launch block */
+    bool block_env = false;               /* ICW_BLOCK given */
     bool dedup_ok = true;                 /* ICW_DEDUP=0 disables the mono K1 dedup (A/B) */
     int max_sets = 2;                     /* ICW_SETS: block scratch sets (2..kSets) */
     /* block schedule of long calls (plan_blocks): a short first block (the pipeline fill is K0 of
@@ -185,6 +188,7 @@ struct icw_ctx {
     double *d_fir_g = nullptr;
     double *fir_hist[2] = {};
     int fir_par = 0;
+    bool fir_fuse = true;                 /* ICW_FIR_FUSED=0: KF + K2 as two kernels (A/B) */
     std::mutex mu;
 };
 
@@ -798,7 +802,7 @@ int icw_create(const icw_config *cfg, const icw_node *nodes, int n_nodes, int n_
         const char *wpc = getenv("ICW_K1_WPC");
         if (wpc && atoi(wpc) >= 1 && atoi(wpc) <= 8) c->k1_wpc = atoi(wpc);
         const char *bl = getenv("ICW_BLOCK");
-        if (bl && atoi(bl) >= 256 && atoi(bl) <= kMaxBlockFrames) c->max_block = atoi(bl);
+        if (bl && atoi(bl) >= 256 && atoi(bl) <= kMaxBlockFrames) { c->max_block = atoi(bl); c->block_env = true; }
         const char *ns = getenv("ICW_SETS");
         if (ns && atoi(ns) >= 2 && atoi(ns) <= kSets) c->max_sets = atoi(ns);
         const char *zc = getenv("ICW_ZEROCOPY");
@@ -813,6 +817,8 @@ int icw_create(const icw_config *cfg, const icw_node *nodes, int n_nodes, int n_
         if (dd && !strcmp(dd, "0")) c->dedup_ok = false;
         const char *fd = getenv("ICW_FILL_DRAIN");
         if (fd && !strcmp(fd, "0")) c->fill_drain = false;
+        const char *ff = getenv("ICW_FIR_FUSED");
+        if (ff && !strcmp(ff, "0")) c->fir_fuse = false;
         const char *kl = getenv("ICW_K1_LDS");
         c->k1_lds = kl && !strcmp(kl, "1");
         {
@@ -1076,9 +1082,16 @@ int icw_process_streams(icw_ctx *c, int first, int count, const void *in, size_t
      * (the row kernel K1r) with a serial render -- its drain is the render of the last block, and
      * the frame-parallel kernels take well under K1r's time per frame (C5: +2 %).  Large batches
      * keep uniform blocks (K0 + K2 take ~0.9 of K1's time there), ICW_TAPER overrides. */
-    const int Tb = std::min(n_frames, c->max_block);
+    /* FIR converter: fused with the graph and render (KF2, one kernel per block) where its LDS fits;
+     * else KF on its own stream (the caller's: K1's, idle without the IIR) beside K2.  KF2 needs no
+     * block scratch and has no recurrence to pipeline against, so its blocks are as long as the
+     * scratch bound allows (fewer launches, fewer partly filled waves of workgroups at their ends) */
+    const bool fir_fused = fir && c->fir_fuse &&
+                           icw_fir_graph_lds(c->fir_M, c->fir_nt, (int)nch, c->prog.n_regs) > 0 && !c->prog.is_bus;
+    const int Tb = std::min(n_frames, (fir_fused && !c->block_env) ? kMaxBlockFrames : c->max_block);
     const double taper = c->taper >= 0.0 ? c->taper : ((!cw && k1_mode == 3 && c->serial_render) ? kAutoTaper : 0.0);
-    const std::vector<std::pair<int, int>> blocks = plan_blocks(n_frames, Tb, c->first_block, taper, c->taper_min);
+    const std::vector<std::pair<int, int>> blocks =
+        plan_blocks(n_frames, Tb, fir_fused ? 0 : c->first_block, taper, c->taper_min);
     const int n_blocks = (int)blocks.size();
 
     const unsigned char *d_in;
@@ -1143,8 +1156,8 @@ int icw_process_streams(icw_ctx *c, int first, int count, const void *in, size_t
     const size_t w_pitch = (size_t)Tb + N + 1;
     const size_t x_pitch = ((size_t)Tb + ICW_MAX_IIR_ORDER + 2) & ~(size_t)1;   /* look-ahead pad */
     const int n_sets = std::min(n_blocks, c->max_sets);
-    for (int p = 0; p < n_sets; ++p) {
-        if (grow((void **)&c->w[p], &c->w_bytes[p], S * 4 * w_pitch * sizeof(double))) return ICW_ENOMEM;
+    for (int p = 0; p < n_sets && !fir_fused; ++p) {
+        if (!cw && grow((void **)&c->w[p], &c->w_bytes[p], S * 4 * w_pitch * sizeof(double))) return ICW_ENOMEM;
         if (grow((void **)&c->xd[p], &c->xd_bytes[p], S * 4 * x_pitch * sizeof(double))) return ICW_ENOMEM;
     }
     if (c->serial_render && !d_pre)
@@ -1217,10 +1230,38 @@ int icw_process_streams(icw_ctx *c, int first, int count, const void *in, size_t
     }
     const unsigned long long ssr = (unsigned long long)cfg.sample_rate * ICW_HZ_SCALE;
 
-    const bool fir_async = fir && sK != sA;
+    const bool fir_async = fir && !fir_fused && sK != sA;
+    /* KF's arguments for launch block b; it reads the history buffer the previous block wrote
+     * (same stream, block order) and writes the other one */
+    auto fir_args = [&](int b) {
+        IcwFirArgs af;
+        memset(&af, 0, sizeof(af));
+        af.in = d_in + (size_t)blocks[b].first * fsz;
+        af.in_stride = dis;
+        af.fmt = cfg.in_format;
+        af.csz = csz;
+        af.fsz = fsz;
+        af.nch = nch;
+        af.n_streams = count;
+        af.T = blocks[b].second;
+        af.t0 = blocks[b].first;
+        af.pos = ds.pos + f0;
+        af.fade = ds.fade + f0 * 3;
+        af.M = c->fir_M;
+        af.nt = c->fir_nt;
+        af.g = c->d_fir_g;
+        const size_t hrow = 2 * (size_t)c->fir_M;
+        af.hist_in = c->fir_hist[c->fir_par] + f0 * hrow;
+        af.hist_out = c->fir_hist[c->fir_par ^ 1] + f0 * hrow;
+        c->fir_par ^= 1;
+        af.xd = c->xd[b % n_sets];
+        af.x_pitch = x_pitch;
+        return af;
+    };
     /* K0 of block b on sA: xd[p] was last read by K1 of block b-2 (and, complex input, by K2 of
      * block b-2, which precedes it on sA) */
     auto launch_k0 = [&](int b) -> int {
+        if (fir_fused) return ICW_OK;                   /* KF2 converts inside the block's kernel */
         const int t0 = blocks[b].first, T = blocks[b].second, p = b % n_sets;
         IcwK0Args a0;
         memset(&a0, 0, sizeof(a0));
@@ -1256,29 +1297,7 @@ int icw_process_streams(icw_ctx *c, int first, int count, const void *in, size_t
                 return ICW_EDEVICE;
         }
         if (fir) {
-            /* KF reads the history buffer the previous block wrote (same stream, block order) */
-            IcwFirArgs af;
-            memset(&af, 0, sizeof(af));
-            af.in = a0.in;
-            af.in_stride = dis;
-            af.fmt = cfg.in_format;
-            af.csz = csz;
-            af.fsz = fsz;
-            af.nch = nch;
-            af.n_streams = count;
-            af.T = T;
-            af.t0 = t0;
-            af.pos = a0.pos;
-            af.fade = a0.fade;
-            af.M = c->fir_M;
-            af.nt = c->fir_nt;
-            af.g = c->d_fir_g;
-            const size_t hrow = 2 * (size_t)c->fir_M;
-            af.hist_in = c->fir_hist[c->fir_par] + f0 * hrow;
-            af.hist_out = c->fir_hist[c->fir_par ^ 1] + f0 * hrow;
-            c->fir_par ^= 1;
-            af.xd = a0.xd;
-            af.x_pitch = x_pitch;
+            IcwFirArgs af = fir_args(b);
             if (timing && hipEventRecord(c->ev[4 * b], s0) != hipSuccess) return ICW_EDEVICE;
             if (icw_launch_fir(&af, s0) != hipSuccess) return ICW_EDEVICE;
             if (timing && hipEventRecord(c->ev[4 * b + 1], s0) != hipSuccess) return ICW_EDEVICE;
@@ -1413,8 +1432,15 @@ int icw_process_streams(icw_ctx *c, int first, int count, const void *in, size_t
         if (c->serial_render && b >= n_sets && sR != s2 && hipStreamWaitEvent(s2, c->k3done[p], 0) != hipSuccess)
             return ICW_EDEVICE;
         if (timing && hipEventRecord(c->ev[4 * b + 2], s2) != hipSuccess) return ICW_EDEVICE;
-        if (fir_async && hipStreamWaitEvent(s2, c->k0done[p], 0) != hipSuccess) return ICW_EDEVICE;
-        if (icw_launch_output(&a2, N, cfg.iir_kahan, s2) != hipSuccess) return ICW_EDEVICE;
+        if (fir_fused) {
+            const IcwFirArgs af = fir_args(b);
+            if (timing && hipEventRecord(c->ev[4 * b], s2) != hipSuccess) return ICW_EDEVICE;
+            if (icw_launch_fir_graph(&af, &a2, s2) != hipSuccess) return ICW_EDEVICE;
+            if (timing && hipEventRecord(c->ev[4 * b + 1], s2) != hipSuccess) return ICW_EDEVICE;
+        } else {
+            if (fir_async && hipStreamWaitEvent(s2, c->k0done[p], 0) != hipSuccess) return ICW_EDEVICE;
+            if (icw_launch_output(&a2, N, cfg.iir_kahan, s2) != hipSuccess) return ICW_EDEVICE;
+        }
         if (hipEventRecord(c->k2done[p], s2) != hipSuccess) return ICW_EDEVICE;
         /* the serial part (K4, K3b) on sR after K2(b): it then overlaps K2(b+1) instead of
          * delaying it on sA */

@@ -525,6 +525,100 @@ __device__ __forceinline__ bool icw_exec_op(const IcwOp &op, IcwLR d, double ome
     }
 }
 
+/* One frame's `in` through the rest of the block (K2 and the fused converter KF2): the bus-form
+ * hand-off, or the DSP list (adv_modulator.c:637-751) on the LDS register file, the pre-render
+ * doubles and the elementwise ROUND render with the meters' per-thread parts. */
+template <bool TRIG>
+__device__ __forceinline__ void icw_frame_graph(const IcwK2Args &a, const IcwProg *P, const IcwRegFile &R, int s,
+                                                int t, const IcwLR &in, bool use_tab, unsigned &clip_l,
+                                                unsigned &clip_r, double &pk_l, double &pk_r)
+{
+    const int T = a.T;
+    if (a.iq_out) {
+        /* bus-form graph: the serial graph kernel takes it from here (do_render == 0) */
+        double *q = a.iq_out + ((size_t)s * T + t) * 4;
+        q[0] = in.lre; q[1] = in.lim; q[2] = in.rre; q[3] = in.rim;
+    } else {
+        const double *trow = use_tab ? a.trig_tab + (size_t)t * a.trig_pitch : nullptr;
+        const double omega = (TRIG && !use_tab) ? icw_omega(a.n_frame[s], a.t0 + t, a.scaled, a.ssr, a.sample_rate)
+                                                : 0.0;
+        /* DSP list (adv_modulator.c:637-751) */
+        R.set(0, in);
+        /* persistent bus at the block's last frame: slot 0 = in, then each written slot's
+         * final value from the op that writes it (compile_graph: op.wb_slot) */
+        const bool last = t == T - 1;
+        double *bus_s = a.bus + (size_t)s * ICW_N_INPUTS * 4;
+        if (last) { bus_s[0] = in.lre; bus_s[1] = in.lim; bus_s[2] = in.rre; bus_s[3] = in.rim; }
+        double lOut = 0.0, rOut = 0.0;
+        for (int oi = 0; oi < P->n_ops; ++oi) {
+            const IcwOp &op = P->ops[oi];
+            IcwLR d;
+            if (P->bypass) {
+                d = in;
+            } else {
+                d.lre = d.lim = d.rre = d.rim = 0.0;
+                for (int q = 0; q < op.n_in; ++q) {
+                    IcwLR v;
+                    R.get(op.in_reg[q], v);
+                    d.lre += v.lre; d.lim += v.lim; d.rre += v.rre; d.rim += v.rim;
+                }
+            }
+            IcwLR o;
+            if (icw_exec_op<TRIG>(op, d, omega, o, lOut, rOut, trow)) {
+                R.set(op.out_reg, o);
+                if (last && op.wb_slot >= 0) {
+                    double *b = bus_s + op.wb_slot * 4;
+                    b[0] = o.lre; b[1] = o.lim; b[2] = o.rre; b[3] = o.rim;
+                }
+            }
+        }
+
+        if (a.pre) {
+            double *p = a.pre + (size_t)s * a.pre_stride + (size_t)t * 2;
+            p[0] = lOut; p[1] = rOut;
+        }
+        if (a.do_render) {
+            const int vl = icw_render_round(lOut, a.rk, clip_l, pk_l);
+            const int vr = icw_render_round(rOut, a.rk, clip_r, pk_r);
+            unsigned char *o = a.out + (size_t)s * a.out_stride;
+            if (a.rk.is24) {
+                unsigned char *q = o + (size_t)t * 6;
+                q[0] = (unsigned char)vl; q[1] = (unsigned char)(vl >> 8); q[2] = (unsigned char)(vl >> 16);
+                q[3] = (unsigned char)vr; q[4] = (unsigned char)(vr >> 8); q[5] = (unsigned char)(vr >> 16);
+            } else {
+                const unsigned pk = ((unsigned)vl & 0xffffu) | ((unsigned)vr << 16);
+                *(unsigned *)(o + (size_t)t * 4) = pk;
+            }
+        }
+    }
+}
+
+/* per-workgroup meters (ICW_K2_TILE threads): wave reduce, LDS, one atomic per stream/channel */
+__device__ __forceinline__ void icw_meters_wg(const IcwK2Args &a, int s, unsigned clip_l, unsigned clip_r, double pk_l,
+                                              double pk_r, unsigned (*red_clip)[ICW_K2_TILE / 64],
+                                              double (*red_pk)[ICW_K2_TILE / 64])
+{
+    const int tl = threadIdx.x;
+    for (int off = 32; off > 0; off >>= 1) {
+        clip_l += __shfl_xor(clip_l, off);
+        clip_r += __shfl_xor(clip_r, off);
+        pk_l = fmax(pk_l, __shfl_xor(pk_l, off));
+        pk_r = fmax(pk_r, __shfl_xor(pk_r, off));
+    }
+    const int wv = tl >> 6;
+    if ((tl & 63) == 0) {
+        red_clip[0][wv] = clip_l; red_clip[1][wv] = clip_r;
+        red_pk[0][wv] = pk_l; red_pk[1][wv] = pk_r;
+    }
+    __syncthreads();
+    if (tl < 2) {
+        unsigned cs = 0; double pm = 0.0;
+        for (int i = 0; i < ICW_K2_TILE / 64; ++i) { cs += red_clip[tl][i]; pm = fmax(pm, red_pk[tl][i]); }
+        if (cs) atomicAdd(&a.clips[s * 2 + tl], cs);
+        if (pm > 0.0) atomicMax(&a.peak_bits[s * 2 + tl], (unsigned long long)__double_as_longlong(pm));
+    }
+}
+
 /* Output kernel (K2).  A workgroup owns a.tpw (<= ICW_K2_TPW) consecutive 256-frame tiles of one
  * stream (fewer when a launch would have too few workgroups to spread over the chip).
  * The w window of tile k+1 is loaded into registers while tile k is computed, then written to the
@@ -656,63 +750,7 @@ __global__ __launch_bounds__(ICW_K2_TILE, ICW_K2_MINWG) void icw_output(IcwK2Arg
                 in.lre = oI[0]; in.lim = oQ[0]; in.rre = oI[1]; in.rim = oQ[1];
             }
 
-            if (a.iq_out) {
-                /* bus-form graph: the serial graph kernel takes it from here (do_render == 0) */
-                double *q = a.iq_out + ((size_t)s * T + t) * 4;
-                q[0] = in.lre; q[1] = in.lim; q[2] = in.rre; q[3] = in.rim;
-            } else {
-                const double *trow = use_tab ? a.trig_tab + (size_t)t * a.trig_pitch : nullptr;
-                const double omega = (TRIG && !use_tab) ? icw_omega(a.n_frame[s], a.t0 + t, a.scaled, a.ssr, a.sample_rate)
-                                                        : 0.0;
-                /* DSP list (adv_modulator.c:637-751) */
-                R.set(0, in);
-                /* persistent bus at the block's last frame: slot 0 = in, then each written slot's
-                 * final value from the op that writes it (compile_graph: op.wb_slot) */
-                const bool last = t == T - 1;
-                double *bus_s = a.bus + (size_t)s * ICW_N_INPUTS * 4;
-                if (last) { bus_s[0] = in.lre; bus_s[1] = in.lim; bus_s[2] = in.rre; bus_s[3] = in.rim; }
-                double lOut = 0.0, rOut = 0.0;
-                for (int oi = 0; oi < P->n_ops; ++oi) {
-                    const IcwOp &op = P->ops[oi];
-                    IcwLR d;
-                    if (P->bypass) {
-                        d = in;
-                    } else {
-                        d.lre = d.lim = d.rre = d.rim = 0.0;
-                        for (int q = 0; q < op.n_in; ++q) {
-                            IcwLR v;
-                            R.get(op.in_reg[q], v);
-                            d.lre += v.lre; d.lim += v.lim; d.rre += v.rre; d.rim += v.rim;
-                        }
-                    }
-                    IcwLR o;
-                    if (icw_exec_op<TRIG>(op, d, omega, o, lOut, rOut, trow)) {
-                        R.set(op.out_reg, o);
-                        if (last && op.wb_slot >= 0) {
-                            double *b = bus_s + op.wb_slot * 4;
-                            b[0] = o.lre; b[1] = o.lim; b[2] = o.rre; b[3] = o.rim;
-                        }
-                    }
-                }
-
-                if (a.pre) {
-                    double *p = a.pre + (size_t)s * a.pre_stride + (size_t)t * 2;
-                    p[0] = lOut; p[1] = rOut;
-                }
-                if (a.do_render) {
-                    const int vl = icw_render_round(lOut, a.rk, clip_l, pk_l);
-                    const int vr = icw_render_round(rOut, a.rk, clip_r, pk_r);
-                    unsigned char *o = a.out + (size_t)s * a.out_stride;
-                    if (a.rk.is24) {
-                        unsigned char *q = o + (size_t)t * 6;
-                        q[0] = (unsigned char)vl; q[1] = (unsigned char)(vl >> 8); q[2] = (unsigned char)(vl >> 16);
-                        q[3] = (unsigned char)vr; q[4] = (unsigned char)(vr >> 8); q[5] = (unsigned char)(vr >> 16);
-                    } else {
-                        const unsigned pk = ((unsigned)vl & 0xffffu) | ((unsigned)vr << 16);
-                        *(unsigned *)(o + (size_t)t * 4) = pk;
-                    }
-                }
-            }
+            icw_frame_graph<TRIG>(a, P, R, s, t, in, use_tab, clip_l, clip_r, pk_l, pk_r);
         }
         if (more) {
             /* the other half was last read in tile k-1, before the previous barrier */
@@ -742,27 +780,108 @@ __global__ __launch_bounds__(ICW_K2_TILE, ICW_K2_MINWG) void icw_output(IcwK2Arg
             if (tot) atomicAdd(&a.sncnt[(size_t)s * 4 + tl], tot);
         }
     }
-    if (a.do_render) {
-        /* per-workgroup meters: wave reduce, LDS, one atomic per stream/channel */
-        for (int off = 32; off > 0; off >>= 1) {
-            clip_l += __shfl_xor(clip_l, off);
-            clip_r += __shfl_xor(clip_r, off);
-            pk_l = fmax(pk_l, __shfl_xor(pk_l, off));
-            pk_r = fmax(pk_r, __shfl_xor(pk_r, off));
-        }
-        const int wv = tl >> 6;
-        if ((tl & 63) == 0) {
-            red_clip[0][wv] = clip_l; red_clip[1][wv] = clip_r;
-            red_pk[0][wv] = pk_l; red_pk[1][wv] = pk_r;
-        }
-        __syncthreads();
-        if (tl < 2) {
-            unsigned cs = 0; double pm = 0.0;
-            for (int i = 0; i < TILE / 64; ++i) { cs += red_clip[tl][i]; pm = fmax(pm, red_pk[tl][i]); }
-            if (cs) atomicAdd(&a.clips[s * 2 + tl], cs);
-            if (pm > 0.0) atomicMax(&a.peak_bits[s * 2 + tl], (unsigned long long)__double_as_longlong(pm));
+    if (a.do_render) icw_meters_wg(a, s, clip_l, clip_r, pk_l, pk_r, red_clip, red_pk);
+}
+
+/* Fused FIR converter + graph + render (KF2): KF's converter for both channels of one stream's
+ * 1024-frame tile, then each lane takes its 4 frames straight through K2's per-frame code
+ * (icw_frame_graph: DSP list, pre-render, ROUND render, meters) -- the analytic signal never
+ * leaves the CU (KF + K2 move 32 B per frame through HBM twice).  The sums are KF's, in the same
+ * order, so the results are KF + K2's bit for bit.  Dynamic LDS: the staged inputs of the
+ * computed channels, the taps, the DSP register file. */
+template <bool TRIG>
+__global__ __launch_bounds__(256, 4) void icw_fir_graph(IcwFirArgs f, IcwK2Args a)
+{
+    extern __shared__ double lds[];
+    __shared__ unsigned red_clip[2][ICW_K2_TILE / 64];
+    __shared__ double red_pk[2][ICW_K2_TILE / 64];
+    constexpr int R = ICW_FIR_TF / 256;
+    const int s = blockIdx.y;
+    const int tt = blockIdx.x * ICW_FIR_TF;
+    const int T = f.T, M = f.M, c = M >> 1;
+    const int nf = min(ICW_FIR_TF, T - tt);
+    const int nchc = f.nch > 1 ? 2 : 1;
+    const int Lx = ICW_FIR_TF + M;
+    double *gs = lds + nchc * Lx;
+    double *lregs = gs + ((f.nt + 1) & ~1);
+    const long long p0 = f.pos[s] + f.t0;
+    const long long ns = f.fade[s * 3 + 0], fi = f.fade[s * 3 + 1], fo = f.fade[s * 3 + 2];
+    for (int ch = 0; ch < nchc; ++ch) {
+        const unsigned char *src = f.in + (size_t)s * f.in_stride + (size_t)ch * f.csz;
+        const double *hin = f.hist_in + ((size_t)s * 2 + ch) * M;
+        double *hout = f.hist_out + ((size_t)s * 2 + ch) * M;
+        double *xs = lds + ch * Lx;
+        for (int i = threadIdx.x; i < nf + M; i += 256) {
+            const int j = tt - M + i;
+            double v;
+            if (j < 0) {
+                v = hin[M + j];
+            } else {
+                v = icw_unpack(src + (size_t)j * f.fsz, f.fmt);
+                const double fd = icw_fade(p0 + j, ns, fi, fo);
+                if (fd >= 0.0) v *= fd;
+            }
+            xs[i] = v;
+            if (j >= T - M && (j >= tt || tt == 0)) {
+                hout[j - (T - M)] = v;
+                if (nchc == 1) hout[M + j - (T - M)] = v;
+            }
         }
     }
+    for (int k = threadIdx.x; k < f.nt; k += 256) gs[k] = f.g[k];
+    __syncthreads();
+
+    const int base = threadIdx.x + M - c;
+    const int rs = 256 + f.zero;
+    double acc[2][R];
+#pragma unroll
+    for (int ch = 0; ch < 2; ++ch) {
+#pragma unroll
+        for (int r = 0; r < R; ++r) acc[ch][r] = 0.0;
+        if (ch < nchc) {
+            const double *xs = lds + ch * Lx;
+#pragma unroll 1
+            for (int k = 0; k < f.nt; ++k) {
+                const int m = 2 * k + 1;
+                const double gm = gs[k];
+#pragma unroll
+                for (int r = 0; r < R; ++r) {
+                    const int i = base + rs * r;
+                    acc[ch][r] = __builtin_fma(gm, xs[i - m] - xs[i + m], acc[ch][r]);
+                }
+            }
+        }
+    }
+
+    const IcwProg *P = a.prog;
+    IcwRegFile Rf;
+    Rf.base = lregs + threadIdx.x;
+    for (int r = 0; r < P->n_persist; ++r) {
+        const double *b = a.bus + ((size_t)s * ICW_N_INPUTS + P->persist_slot[r]) * 4;
+        IcwLR v; v.lre = b[0]; v.lim = b[1]; v.rre = b[2]; v.rim = b[3];
+        Rf.set(P->persist_reg[r], v);
+    }
+    const bool use_tab = TRIG && a.trig_tab && a.n_frame[s] == a.n_frame[0];
+    unsigned clip_l = 0, clip_r = 0;
+    double pk_l = 0.0, pk_r = 0.0;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const int fr = threadIdx.x + 256 * r;
+        if (fr < nf) {
+            IcwLR in;
+            in.lre = lds[fr + M - c];
+            in.lim = acc[0][r];
+            if (nchc == 2) {
+                in.rre = lds[Lx + fr + M - c];
+                in.rim = acc[1][r];
+            } else {
+                in.rre = in.lre;
+                in.rim = in.lim;
+            }
+            icw_frame_graph<TRIG>(a, P, Rf, s, tt + fr, in, use_tab, clip_l, clip_r, pk_l, pk_r);
+        }
+    }
+    if (a.do_render) icw_meters_wg(a, s, clip_l, clip_r, pk_l, pk_r, red_clip, red_pk);
 }
 
 /* Per-frame rotation table: the Shift / PM factors of frame t depend only on the modulator frame
@@ -1717,6 +1836,26 @@ extern "C" hipError_t icw_launch_fir(const IcwFirArgs *a, hipStream_t st)
     dim3 grid((a->T + ICW_FIR_TF - 1) / ICW_FIR_TF, a->nch > 1 ? 2 : 1, a->n_streams);
     const size_t lds = (size_t)(ICW_FIR_TF + a->M + a->nt) * sizeof(double);
     hipLaunchKernelGGL(icw_fir_hilbert, grid, dim3(256), lds, st, *a);
+    return hipGetLastError();
+}
+
+/* bytes of dynamic LDS the fused converter needs (0: too many for one workgroup -- run KF + K2) */
+extern "C" size_t icw_fir_graph_lds(int M, int nt, int nch, int n_regs)
+{
+    const size_t n = (size_t)(nch > 1 ? 2 : 1) * (ICW_FIR_TF + M) + (size_t)((nt + 1) & ~1) +
+                     (size_t)n_regs * 4 * ICW_K2_TILE;
+    return n * sizeof(double) <= 64 * 1024 ? n * sizeof(double) : 0;
+}
+
+extern "C" hipError_t icw_launch_fir_graph(const IcwFirArgs *f, const IcwK2Args *a, hipStream_t st)
+{
+    if (f->M < 2 || f->M > ICW_FIR_MAX_M || (f->M & 1) || f->nt < 1 || 2 * f->nt - 1 > f->M / 2)
+        return hipErrorInvalidValue;
+    const size_t lds = icw_fir_graph_lds(f->M, f->nt, f->nch, a->n_regs);
+    if (!lds) return hipErrorInvalidValue;
+    dim3 grid((f->T + ICW_FIR_TF - 1) / ICW_FIR_TF, f->n_streams);
+    if (a->trig) hipLaunchKernelGGL(icw_fir_graph<true>, grid, dim3(256), lds, st, *f, *a);
+    else hipLaunchKernelGGL(icw_fir_graph<false>, grid, dim3(256), lds, st, *f, *a);
     return hipGetLastError();
 }
 

@@ -1,4 +1,5 @@
-"""GPU parity of the FIR Hilbert converter (icw_set_fir_hilbert, kernel KF `icw_fir_hilbert`)
+"""GPU parity of the FIR Hilbert converter (icw_set_fir_hilbert: kernel KF2 `icw_fir_graph`, or KF
+`icw_fir_hilbert` + K2)
 against the oracle's restatement (oracle/icw_oracle.c fir_process): pre-render doubles and
 rendered bytes bit for bit.
 
@@ -18,6 +19,13 @@ from test_gpu_parity import assert_parity
 pytestmark = pytest.mark.gpu
 
 BETA = 8.0
+
+
+@pytest.fixture(autouse=True, params=["fused", "split"])
+def fir_form(request, monkeypatch):
+    """KF2 (converter, graph and render in one kernel) and KF + K2 (ICW_FIR_FUSED=0)"""
+    monkeypatch.setenv("ICW_FIR_FUSED", "1" if request.param == "fused" else "0")
+    return request.param
 
 
 def run_fir(oracle, icw, cfg, nodes, raw, n_frames, order, beta=BETA, blocks=None):
