@@ -37,13 +37,12 @@ struct IcwK0Args {
     size_t x_pitch;
 };
 
-/* Arguments of the FIR Hilbert converter kernel (KF, the CWAVE converter of cwave.h:40,56-58:
- * a Kaiser-windowed Hilbert FIR of order M = k_M, window parameter k_beta).  A workgroup owns
- * ICW_FIR_TF output frames of one channel of one stream; it stages the inputs x[t - M .. t + TF)
- * (unpacked and faded like K0, the M before the block from the history) in LDS and writes the
- * analytic signal I = x[n - M/2], Q = sum_m g_m (x[n - M/2 - m] - x[n - M/2 + m]) into the complex
- * rows K2 reads for CWAVE input. */
-#define ICW_FIR_TF     1024   /* output frames per FIR workgroup (256 lanes x 4) */
+/* Arguments of the FIR Hilbert converter kernels (KF / KF2, the CWAVE converter of cwave.h:40,56-58:
+ * a Kaiser-windowed Hilbert FIR of order M = k_M, window parameter k_beta).  A workgroup stages the
+ * inputs x[t - M .. t + tile) of its channels (unpacked and faded like K0, the M before the block
+ * from the history) in LDS and forms the analytic signal I = x[n - M/2],
+ * Q = sum_m g_m (x[n - M/2 - m] - x[n - M/2 + m]); KF writes it to the complex rows K2 reads for
+ * CWAVE input, KF2 takes it through the graph and render itself. */
 #define ICW_FIR_MAX_M  4096   /* largest FIR order */
 struct IcwFirArgs {
     const unsigned char *in;       /* stream s at in + s*in_stride */

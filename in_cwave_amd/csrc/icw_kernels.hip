@@ -152,88 +152,162 @@ __global__ __launch_bounds__(256) void icw_unpack_frames(IcwK0Args a)
     }
 }
 
-/* FIR Hilbert converter (KF): real PCM -> the analytic signal a CWAVE file holds (cwave.h:40,56-58:
+/* FIR Hilbert converter: real PCM -> the analytic signal a CWAVE file holds (cwave.h:40,56-58:
  * "Hilbert FIR filter order" k_M, "filter parameter" k_beta; the converter itself is not part of
  * in_cwave).  Order M (even, M + 1 taps), centre c = M/2, odd taps only:
  *     I[n] = x[n - c],   Q[n] = sum_{m = 1, 3, .., <= c} g_m * (x[n - c - m] - x[n - c + m])
  * with the sum taken in ascending m as acc = fma(g_m, d_m, acc) from +0.0 -- the oracle's order, so
  * the result is bit-identical.  x is the unpacked, faded input of K0 (xwave_unpack_csample,
- * xwave_reader.c:908-936), mono feeding R with L.  The workgroup stages x[tt - M, tt + TF) of its
- * channel in LDS (coalesced loads; the M inputs before the block come from the history) and each
- * lane sums 4 outputs 256 frames apart, so every LDS read of a wave is 64 consecutive doubles
- * (conflict-free ds_read_b64) and the tap g_m is a scalar load shared by the wave.  Per output
- * and tap: 2 LDS reads, one subtract, one FMA.  The block's last M inputs go to the other history
- * buffer (read and write buffers differ, so the workgroups of a stream never race). */
+ * xwave_reader.c:908-936), mono feeding R with L.
+ *
+ * Register blocking.  A lane sums 8 consecutive outputs of one channel.  For 8 taps at a time it
+ * loads the 22 inputs their left operands span and the 22 of the right ones, then runs the 64
+ * subtract + FMA pairs from registers: 44 LDS reads per 64 output-taps instead of 128.  The staged
+ * inputs carry one pad double after every 8 (physical index i + i/8), so the 32 lanes of a
+ * ds_read_b64 group, 9 doubles apart, hit 64 distinct banks; a staging shift `sh` puts every lane's
+ * window at the same phase of that pattern, so all offsets inside a block are immediates.  Taps past
+ * the last multiple of 8 run one at a time. */
+#define ICW_FIR_R 8                                  /* outputs per lane */
+
+__device__ __forceinline__ int icw_fir_phys(int i) { return i + (i >> 3); }
+
+/* inputs of channel ch for the outputs [tt, tt + nout) of a launch block, at logical index
+ * i <-> frame j = tt - M + i - sh (zero outside [-M, T)); the history after the block is written by
+ * the tile that owns each of its frames */
+__device__ __forceinline__ void icw_fir_stage(const IcwFirArgs &f, int s, int ch, double *xs, int tt, int nout,
+                                              int sh, int tid, int nthr)
+{
+    const int T = f.T, M = f.M;
+    const unsigned char *src = f.in + (size_t)s * f.in_stride + (size_t)ch * f.csz;
+    const long long p0 = f.pos[s] + f.t0;
+    const long long ns = f.fade[s * 3 + 0], fi = f.fade[s * 3 + 1], fo = f.fade[s * 3 + 2];
+    const double *hin = f.hist_in + ((size_t)s * 2 + ch) * M;
+    double *hout = f.hist_out + ((size_t)s * 2 + ch) * M;
+    const bool mono = f.nch == 1;
+    const int nl = sh + M + nout + 24;               /* logical extent: pad, history, tile, margin */
+    const int nf = min(nout, T - tt);
+    /* 8 consecutive inputs per thread and pass, their loads issued together (clamped in range,
+     * selected after): the staging is load-latency bound otherwise */
+    constexpr int V = 8;
+    for (int i0 = tid * V; i0 < nl; i0 += nthr * V) {
+        double raw[V], his[V];
+#pragma unroll
+        for (int e = 0; e < V; ++e) {
+            const int j = tt - M + i0 + e - sh;
+            const int jr = min(max(j, 0), T - 1);
+            raw[e] = icw_unpack(src + (size_t)jr * f.fsz, f.fmt);
+            his[e] = hin[min(max(M + j, 0), M - 1)];
+        }
+#pragma unroll
+        for (int e = 0; e < V; ++e) {
+            const int i = i0 + e;
+            const int j = tt - M + i - sh;
+            double v = 0.0;
+            if (i >= sh && j < tt + nf) {
+                if (j < 0) {
+                    v = his[e];
+                } else {
+                    v = raw[e];
+                    const double fd = icw_fade(p0 + j, ns, fi, fo);
+                    if (fd >= 0.0) v *= fd;
+                }
+                if (j >= T - M && (j >= tt || tt == 0)) {
+                    hout[j - (T - M)] = v;
+                    if (mono) hout[M + j - (T - M)] = v;
+                }
+            }
+            if (i < nl) xs[icw_fir_phys(i)] = v;
+        }
+    }
+}
+
+/* one 8-tap block (k0 = 8b) of a lane's 8 outputs: bl / br = physical index of the first input of
+ * the left / right window (both at phase 2 of the pad pattern) */
+__device__ __forceinline__ void icw_fir_block8(const double *xs, const double *gs, int k0, int bl, int br,
+                                               double (&acc)[ICW_FIR_R])
+{
+    constexpr int W = ICW_FIR_R + 14;
+    double L[W], Rt[W], g[8];
+#pragma unroll
+    for (int e = 0; e < W; ++e) {
+        L[e] = xs[bl + e + ((e + 2) >> 3)];
+        asm volatile("" ::: "memory");               /* no ds_read2 pairing: 2 x 2 cycles, not 8 */
+    }
+#pragma unroll
+    for (int e = 0; e < W; ++e) {
+        Rt[e] = xs[br + e + ((e + 2) >> 3)];
+        asm volatile("" ::: "memory");
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) g[j] = gs[k0 + j];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+#pragma unroll
+        for (int r = 0; r < ICW_FIR_R; ++r)
+            acc[r] = __builtin_fma(g[j], L[r - 2 * j + 14] - Rt[r + 2 * j], acc[r]);
+    }
+}
+
+/* Q of a lane's 8 outputs tt + 8 ll + r; a = (c - 1 + sh) / 8 */
+__device__ __forceinline__ void icw_fir_sums(const double *xs, const double *gs, int nt, int ll, int a, int sh, int c,
+                                             double (&acc)[ICW_FIR_R])
+{
+#pragma unroll
+    for (int r = 0; r < ICW_FIR_R; ++r) acc[r] = 0.0;
+    const int nb = nt >> 3;
+    int bl = 9 * (ll + a - 2) + 2, br = 9 * (ll + a) + 2;
+#pragma unroll 1
+    for (int b = 0; b < nb; ++b) {
+        icw_fir_block8(xs, gs, 8 * b, bl, br, acc);
+        bl -= 18;
+        br += 18;
+    }
+    const int A = 8 * a;
+#pragma unroll 1
+    for (int k = nb * 8; k < nt; ++k) {
+        const double gk = gs[k];
+#pragma unroll
+        for (int r = 0; r < ICW_FIR_R; ++r) {
+            const int li = 8 * ll + A + r - 2 * k, ri = 8 * ll + A + 2 + r + 2 * k;
+            acc[r] = __builtin_fma(gk, xs[icw_fir_phys(li)] - xs[icw_fir_phys(ri)], acc[r]);
+        }
+    }
+    (void)sh; (void)c;
+}
+
+/* KF: the converter alone, one workgroup per channel and 2048-frame tile of a stream; I / Q rows
+ * go out coalesced through LDS to the CWAVE rows K2 reads */
 __global__ __launch_bounds__(256) void icw_fir_hilbert(IcwFirArgs a)
 {
-    extern __shared__ double xs[];                   /* xs[i] = x[tt - M + i], i < TF + M; then the taps */
-    constexpr int R = ICW_FIR_TF / 256;
+    extern __shared__ double xs[];                   /* staged inputs (padded), taps, Q */
+    constexpr int TF = 256 * ICW_FIR_R;
     const int ch = blockIdx.y, s = blockIdx.z;
-    const int tt = blockIdx.x * ICW_FIR_TF;
-    const int T = a.T, M = a.M, c = M >> 1;
-    const int nf = min(ICW_FIR_TF, T - tt);
-    const unsigned char *src = a.in + (size_t)s * a.in_stride + (size_t)ch * a.csz;
-    const long long p0 = a.pos[s] + a.t0;
-    const long long ns = a.fade[s * 3 + 0], fi = a.fade[s * 3 + 1], fo = a.fade[s * 3 + 2];
-    const double *hin = a.hist_in + ((size_t)s * 2 + ch) * M;
-    double *hout = a.hist_out + ((size_t)s * 2 + ch) * M;
-    const bool mono = a.nch == 1;                    /* R = L: its history follows L's */
-    for (int i = threadIdx.x; i < nf + M; i += 256) {
-        const int j = tt - M + i;                    /* frame index in the block */
-        double v;
-        if (j < 0) {
-            v = hin[M + j];
-        } else {
-            v = icw_unpack(src + (size_t)j * a.fsz, a.fmt);
-            const double fd = icw_fade(p0 + j, ns, fi, fo);
-            if (fd >= 0.0) v *= fd;
-        }
-        xs[i] = v;
-        /* history after the block: inputs [T - M, T), each written by the tile that owns it (the
-         * ones before the block, when T < M, by tile 0) */
-        if (j >= T - M && (j >= tt || tt == 0)) {
-            hout[j - (T - M)] = v;
-            if (mono) hout[M + j - (T - M)] = v;
-        }
-    }
-    /* the taps, after the staged inputs (a broadcast LDS read per tap: the compiler cannot keep
-     * them in scalar loads, the workgroup writes memory) */
-    double *gs = xs + ICW_FIR_TF + M;
+    const int tt = blockIdx.x * TF;
+    const int M = a.M, c = M >> 1;
+    const int sh = (8 - ((c - 1) & 7)) & 7;          /* c - 1 + sh = 8 a */
+    const int av = (c - 1 + sh) >> 3;
+    const int nf = min(TF, a.T - tt);
+    icw_fir_stage(a, s, ch, xs, tt, TF, sh, threadIdx.x, 256);
+    const int px = icw_fir_phys(sh + M + TF + 24) + 1;
+    double *gs = xs + px;
+    double *qs = gs + ((a.nt + 1) & ~1);
     for (int k = threadIdx.x; k < a.nt; k += 256) gs[k] = a.g[k];
     __syncthreads();
-
-    double acc[R];
+    double acc[ICW_FIR_R];
+    icw_fir_sums(xs, gs, a.nt, threadIdx.x, av, sh, c, acc);
 #pragma unroll
-    for (int r = 0; r < R; ++r) acc[r] = 0.0;
-    const int base = threadIdx.x + M - c;            /* LDS index of x[tt + lane - c] */
-    /* the outputs' stride, opaque to the compiler: with a constant 256 it pairs the reads of two
-     * outputs into ds_read2st64_b64, which takes 8 LDS cycles per wave for what two ds_read_b64
-     * (2 cycles each, 64 consecutive doubles, conflict-free) deliver in 4 -- and KF is LDS-bound */
-    const int rs = 256 + a.zero;
-#pragma unroll 1
-    for (int k = 0; k < a.nt; ++k) {
-        const int m = 2 * k + 1;
-        const double gm = gs[k];
-#pragma unroll
-        for (int r = 0; r < R; ++r) {
-            const int i = base + rs * r;
-            acc[r] = __builtin_fma(gm, xs[i - m] - xs[i + m], acc[r]);
-        }
-    }
-
+    for (int r = 0; r < ICW_FIR_R; ++r) qs[ICW_FIR_R * threadIdx.x + r] = acc[r];
+    __syncthreads();
     double *rowI = a.xd + ((size_t)s * 4 + ch * 2) * a.x_pitch + tt;
     double *rowQ = rowI + a.x_pitch;
-#pragma unroll
-    for (int r = 0; r < R; ++r) {
-        const int f = threadIdx.x + 256 * r;
-        if (f < nf) {
-            const double vi = xs[f + M - c];
-            rowI[f] = vi;
-            rowQ[f] = acc[r];
-            if (mono) {
-                rowI[f + 2 * a.x_pitch] = vi;
-                rowQ[f + 2 * a.x_pitch] = acc[r];
-            }
+    const bool mono = a.nch == 1;
+    for (int f = threadIdx.x; f < nf; f += 256) {
+        const double vi = xs[icw_fir_phys(f + 8 * av + 1)], vq = qs[f];
+        rowI[f] = vi;
+        rowQ[f] = vq;
+        if (mono) {
+            rowI[f + 2 * a.x_pitch] = vi;
+            rowQ[f + 2 * a.x_pitch] = vq;
         }
     }
 }
@@ -783,75 +857,43 @@ __global__ __launch_bounds__(ICW_K2_TILE, ICW_K2_MINWG) void icw_output(IcwK2Arg
     if (a.do_render) icw_meters_wg(a, s, clip_l, clip_r, pk_l, pk_r, red_clip, red_pk);
 }
 
-/* Fused FIR converter + graph + render (KF2): KF's converter for both channels of one stream's
- * 1024-frame tile, then each lane takes its 4 frames straight through K2's per-frame code
- * (icw_frame_graph: DSP list, pre-render, ROUND render, meters) -- the analytic signal never
- * leaves the CU (KF + K2 move 32 B per frame through HBM twice).  The sums are KF's, in the same
- * order, so the results are KF + K2's bit for bit.  Dynamic LDS: the staged inputs of the
- * computed channels, the taps, the DSP register file. */
+/* Fused FIR converter + graph + render (KF2): one workgroup per stream and 1024-frame tile (2048
+ * for mono).  Wave w owns frames [256 w, 256 w + 256) of the tile: lanes 0-31 sum channel L's
+ * outputs and lanes 32-63 channel R's, 8 consecutive frames each (icw_fir_sums).  A lane pair
+ * (l, l + 32) then swaps half of its I / Q values (__shfl_xor 32), so lane l holds both channels
+ * of frames 0-3 of its eight and lane l + 32 of frames 4-7, and each takes its 4 frames straight
+ * through K2's per-frame code (icw_frame_graph: DSP list, pre-render, ROUND render, meters).  The
+ * analytic signal never leaves the registers (KF + K2 move 32 B per frame through HBM twice); the
+ * sums are KF's, in the same order, so the results are KF + K2's bit for bit.  Dynamic LDS: the
+ * padded inputs of each computed channel, the taps, the DSP register file. */
 template <bool TRIG>
 __global__ __launch_bounds__(256, 4) void icw_fir_graph(IcwFirArgs f, IcwK2Args a)
 {
     extern __shared__ double lds[];
     __shared__ unsigned red_clip[2][ICW_K2_TILE / 64];
     __shared__ double red_pk[2][ICW_K2_TILE / 64];
-    constexpr int R = ICW_FIR_TF / 256;
     const int s = blockIdx.y;
-    const int tt = blockIdx.x * ICW_FIR_TF;
-    const int T = f.T, M = f.M, c = M >> 1;
-    const int nf = min(ICW_FIR_TF, T - tt);
     const int nchc = f.nch > 1 ? 2 : 1;
-    const int Lx = ICW_FIR_TF + M;
-    double *gs = lds + nchc * Lx;
+    const int TF = 256 * ICW_FIR_R / nchc;
+    const int tt = blockIdx.x * TF;
+    const int M = f.M, c = M >> 1;
+    const int sh = (8 - ((c - 1) & 7)) & 7;
+    const int av = (c - 1 + sh) >> 3;
+    const int nf = min(TF, f.T - tt);
+    const int px = icw_fir_phys(sh + M + TF + 24) + 1;     /* doubles per staged channel */
+    double *gs = lds + nchc * px;
     double *lregs = gs + ((f.nt + 1) & ~1);
-    const long long p0 = f.pos[s] + f.t0;
-    const long long ns = f.fade[s * 3 + 0], fi = f.fade[s * 3 + 1], fo = f.fade[s * 3 + 2];
-    for (int ch = 0; ch < nchc; ++ch) {
-        const unsigned char *src = f.in + (size_t)s * f.in_stride + (size_t)ch * f.csz;
-        const double *hin = f.hist_in + ((size_t)s * 2 + ch) * M;
-        double *hout = f.hist_out + ((size_t)s * 2 + ch) * M;
-        double *xs = lds + ch * Lx;
-        for (int i = threadIdx.x; i < nf + M; i += 256) {
-            const int j = tt - M + i;
-            double v;
-            if (j < 0) {
-                v = hin[M + j];
-            } else {
-                v = icw_unpack(src + (size_t)j * f.fsz, f.fmt);
-                const double fd = icw_fade(p0 + j, ns, fi, fo);
-                if (fd >= 0.0) v *= fd;
-            }
-            xs[i] = v;
-            if (j >= T - M && (j >= tt || tt == 0)) {
-                hout[j - (T - M)] = v;
-                if (nchc == 1) hout[M + j - (T - M)] = v;
-            }
-        }
-    }
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int ch = nchc == 2 ? lane >> 5 : 0;
+    const int ll = nchc == 2 ? wv * 32 + (lane & 31) : threadIdx.x;   /* lane index within the channel */
+    for (int k = 0; k < nchc; ++k) icw_fir_stage(f, s, k, lds + k * px, tt, TF, sh, threadIdx.x, 256);
     for (int k = threadIdx.x; k < f.nt; k += 256) gs[k] = f.g[k];
     __syncthreads();
-
-    const int base = threadIdx.x + M - c;
-    const int rs = 256 + f.zero;
-    double acc[2][R];
+    double q[ICW_FIR_R], vi[ICW_FIR_R];
+    icw_fir_sums(lds + ch * px, gs, f.nt, ll, av, sh, c, q);
+    const int ix = 8 * av + 1;                               /* logical index of x[tt - c] */
 #pragma unroll
-    for (int ch = 0; ch < 2; ++ch) {
-#pragma unroll
-        for (int r = 0; r < R; ++r) acc[ch][r] = 0.0;
-        if (ch < nchc) {
-            const double *xs = lds + ch * Lx;
-#pragma unroll 1
-            for (int k = 0; k < f.nt; ++k) {
-                const int m = 2 * k + 1;
-                const double gm = gs[k];
-#pragma unroll
-                for (int r = 0; r < R; ++r) {
-                    const int i = base + rs * r;
-                    acc[ch][r] = __builtin_fma(gm, xs[i - m] - xs[i + m], acc[ch][r]);
-                }
-            }
-        }
-    }
+    for (int r = 0; r < ICW_FIR_R; ++r) vi[r] = lds[ch * px + icw_fir_phys(ICW_FIR_R * ll + r + ix)];
 
     const IcwProg *P = a.prog;
     IcwRegFile Rf;
@@ -864,21 +906,31 @@ __global__ __launch_bounds__(256, 4) void icw_fir_graph(IcwFirArgs f, IcwK2Args 
     const bool use_tab = TRIG && a.trig_tab && a.n_frame[s] == a.n_frame[0];
     unsigned clip_l = 0, clip_r = 0;
     double pk_l = 0.0, pk_r = 0.0;
+    if (nchc == 2) {
+        /* lane l (L) keeps frames 0-3 and gets R's values of them; lane l + 32 (R) frames 4-7 */
+        const int h = ch ? 4 : 0;
 #pragma unroll
-    for (int r = 0; r < R; ++r) {
-        const int fr = threadIdx.x + 256 * r;
-        if (fr < nf) {
-            IcwLR in;
-            in.lre = lds[fr + M - c];
-            in.lim = acc[0][r];
-            if (nchc == 2) {
-                in.rre = lds[Lx + fr + M - c];
-                in.rim = acc[1][r];
-            } else {
-                in.rre = in.lre;
-                in.rim = in.lim;
+        for (int r = 0; r < 4; ++r) {
+            const double oi = __shfl_xor(ch ? vi[r] : vi[r + 4], 32);
+            const double oq = __shfl_xor(ch ? q[r] : q[r + 4], 32);
+            const int fr = ICW_FIR_R * ll + h + r;
+            if (fr < nf) {
+                IcwLR in;
+                if (ch) { in.lre = oi; in.lim = oq; in.rre = vi[r + 4]; in.rim = q[r + 4]; }
+                else { in.lre = vi[r]; in.lim = q[r]; in.rre = oi; in.rim = oq; }
+                icw_frame_graph<TRIG>(a, P, Rf, s, tt + fr, in, use_tab, clip_l, clip_r, pk_l, pk_r);
             }
-            icw_frame_graph<TRIG>(a, P, Rf, s, tt + fr, in, use_tab, clip_l, clip_r, pk_l, pk_r);
+        }
+    } else {
+#pragma unroll 1
+        for (int r = 0; r < ICW_FIR_R; ++r) {
+            const int fr = ICW_FIR_R * ll + r;
+            if (fr < nf) {
+                IcwLR in;
+                in.lre = in.rre = vi[r];
+                in.lim = in.rim = q[r];
+                icw_frame_graph<TRIG>(a, P, Rf, s, tt + fr, in, use_tab, clip_l, clip_r, pk_l, pk_r);
+            }
         }
     }
     if (a.do_render) icw_meters_wg(a, s, clip_l, clip_r, pk_l, pk_r, red_clip, red_pk);
@@ -1829,31 +1881,56 @@ extern "C" hipError_t icw_launch_unpack(const IcwK0Args *a, hipStream_t st)
     return hipGetLastError();
 }
 
+/* dynamic LDS of the FIR kernels: staged channels (padded), taps, Q, the DSP register file */
+static size_t fir_lds(int M, int nt, int nchc, int tf, int n_regs)
+{
+    const int sh = (8 - ((M / 2 - 1) & 7)) & 7;
+    const int nl = sh + M + tf + 24;
+    const size_t px = (size_t)(nl + (nl >> 3)) + 1;
+    return ((size_t)nchc * px + (size_t)((nt + 1) & ~1) + (size_t)nchc * tf + (size_t)n_regs * 4 * ICW_K2_TILE) *
+           sizeof(double);
+}
+
+static bool fir_ok(int M, int nt)
+{
+    return M >= 2 && M <= ICW_FIR_MAX_M && !(M & 1) && nt >= 1 && 2 * nt - 1 <= M / 2;
+}
+
+/* LDS above 64 KB per workgroup needs the kernel attribute (gfx950: 160 KB per CU) */
+static hipError_t fir_lds_attr(const void *fn, size_t lds)
+{
+    return lds > 64 * 1024 ? hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) : hipSuccess;
+}
+
 extern "C" hipError_t icw_launch_fir(const IcwFirArgs *a, hipStream_t st)
 {
-    if (a->M < 2 || a->M > ICW_FIR_MAX_M || (a->M & 1) || a->nt < 1 || 2 * a->nt - 1 > a->M / 2)
-        return hipErrorInvalidValue;
-    dim3 grid((a->T + ICW_FIR_TF - 1) / ICW_FIR_TF, a->nch > 1 ? 2 : 1, a->n_streams);
-    const size_t lds = (size_t)(ICW_FIR_TF + a->M + a->nt) * sizeof(double);
+    if (!fir_ok(a->M, a->nt)) return hipErrorInvalidValue;
+    constexpr int TF = 256 * ICW_FIR_R;
+    const size_t lds = fir_lds(a->M, a->nt, 1, TF, 0);
+    if (lds > 160 * 1024) return hipErrorInvalidValue;
+    if (fir_lds_attr((const void *)icw_fir_hilbert, lds) != hipSuccess) return hipErrorInvalidValue;
+    dim3 grid((a->T + TF - 1) / TF, a->nch > 1 ? 2 : 1, a->n_streams);
     hipLaunchKernelGGL(icw_fir_hilbert, grid, dim3(256), lds, st, *a);
     return hipGetLastError();
 }
 
-/* bytes of dynamic LDS the fused converter needs (0: too many for one workgroup -- run KF + K2) */
+/* bytes of dynamic LDS the fused converter needs (0: more than a workgroup may hold -- run KF + K2) */
 extern "C" size_t icw_fir_graph_lds(int M, int nt, int nch, int n_regs)
 {
-    const size_t n = (size_t)(nch > 1 ? 2 : 1) * (ICW_FIR_TF + M) + (size_t)((nt + 1) & ~1) +
-                     (size_t)n_regs * 4 * ICW_K2_TILE;
-    return n * sizeof(double) <= 64 * 1024 ? n * sizeof(double) : 0;
+    const int nchc = nch > 1 ? 2 : 1;
+    const size_t lds = fir_lds(M, nt, nchc, 256 * ICW_FIR_R / nchc, n_regs) - (size_t)256 * ICW_FIR_R * sizeof(double);
+    return lds <= 96 * 1024 ? lds : 0;
 }
 
 extern "C" hipError_t icw_launch_fir_graph(const IcwFirArgs *f, const IcwK2Args *a, hipStream_t st)
 {
-    if (f->M < 2 || f->M > ICW_FIR_MAX_M || (f->M & 1) || f->nt < 1 || 2 * f->nt - 1 > f->M / 2)
-        return hipErrorInvalidValue;
+    if (!fir_ok(f->M, f->nt)) return hipErrorInvalidValue;
     const size_t lds = icw_fir_graph_lds(f->M, f->nt, f->nch, a->n_regs);
     if (!lds) return hipErrorInvalidValue;
-    dim3 grid((f->T + ICW_FIR_TF - 1) / ICW_FIR_TF, f->n_streams);
+    const int TF = 256 * ICW_FIR_R / (f->nch > 1 ? 2 : 1);
+    dim3 grid((f->T + TF - 1) / TF, f->n_streams);
+    const void *fn = a->trig ? (const void *)icw_fir_graph<true> : (const void *)icw_fir_graph<false>;
+    if (fir_lds_attr(fn, lds) != hipSuccess) return hipErrorInvalidValue;
     if (a->trig) hipLaunchKernelGGL(icw_fir_graph<true>, grid, dim3(256), lds, st, *f, *a);
     else hipLaunchKernelGGL(icw_fir_graph<false>, grid, dim3(256), lds, st, *f, *a);
     return hipGetLastError();
