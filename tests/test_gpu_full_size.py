@@ -8,6 +8,9 @@ one full step through libicw with device pointers.  Checked:
     produce identical bytes (stream s and s + 16), and a per-stream checksum table has exactly
     16 distinct rows -- no stream is skipped, duplicated or cross-wired anywhere in the batch;
   * the meters of a sampled stream equal the oracle's.
+
+The c2fir-c5fir variants run the same shapes through the FIR Hilbert converter (bench.py's FIR
+legs, DESIGN 4d: no reference implementation, parity against the oracle's restatement only).
 """
 import numpy as np
 import pytest
@@ -17,12 +20,17 @@ pytestmark = pytest.mark.gpu
 N_GEN = 16
 
 
+def _fir_beta():
+    import bench
+    return bench.FIR_BETA
+
+
 def _workload(name):
     import bench
     return bench.WORKLOADS[name], bench.workload_config(bench.WORKLOADS[name])
 
 
-@pytest.mark.parametrize("name", ["c2", "c3", "c4", "c5"])
+@pytest.mark.parametrize("name", ["c2", "c3", "c4", "c5", "c2fir", "c3fir", "c4fir", "c5fir"])
 def test_full_size_step(oracle, icw, name):
     import torch
     from in_cwave_amd import synth
@@ -33,6 +41,9 @@ def test_full_size_step(oracle, icw, name):
     g = torch.from_numpy(gen).to(dev)
     d_in = g.repeat((S + N_GEN - 1) // N_GEN, 1)[:S].contiguous()
     ctx = icw.Context(cfg, nodes, S, device=0)
+    fir = (W["fir"], _fir_beta()) if W.get("fir") else None
+    if fir:
+        ctx.set_fir_hilbert(*fir)
     osz = 2 * ctx.render_size
     d_out = torch.empty((S, T * osz), dtype=torch.uint8, device=dev)
     ctx.process_device(d_in, d_in.stride(0), d_out, d_out.stride(0), T)
@@ -50,6 +61,8 @@ def test_full_size_step(oracle, icw, name):
     # the sampled streams, full length, against the oracle
     for s in sorted({0, S // 2, S - 1}):
         st = oracle.Stream(cfg, nodes)
+        if fir:
+            st.set_fir(*fir)
         ref, _ = st.process(gen[s % N_GEN], T)
         got = rows[s].cpu().numpy()
         bad = np.flatnonzero(got != ref)
