@@ -55,6 +55,7 @@ constexpr int kMaxBlockFrames = 1 << 16;
 constexpr int kDefBlockFrames = 1 << 14;   /* launch block: shorter pipeline fill / drain */
 constexpr int kSets = 3;                    /* most block scratch sets (ICW_SETS); default 2 */
 constexpr double kAutoTaper = 0.85;          /* tail block ratio where the taper is on by default */
+constexpr double kRowTaper = 0.25;           /* tail ratio of the row kernel's long blocks (no serial render) */
 constexpr int kRowRenderMax = 2048;          /* channels up to which the render runs a row per channel */
 constexpr size_t kPinnedStage = 1u << 20;   /* host-pointer calls up to this size stage through pinned memory */
 
@@ -1088,8 +1089,14 @@ int icw_process_streams(icw_ctx *c, int first, int count, const void *in, size_t
      * scratch bound allows (fewer launches, fewer partly filled waves of workgroups at their ends) */
     const bool fir_fused = fir && c->fir_fuse &&
                            icw_fir_graph_lds(c->fir_M, c->fir_nt, (int)nch, c->prog.n_regs) > 0 && !c->prog.is_bus;
-    const int Tb = std::min(n_frames, (fir_fused && !c->block_env) ? kMaxBlockFrames : c->max_block);
-    const double taper = c->taper >= 0.0 ? c->taper : ((!cw && k1_mode == 3 && c->serial_render) ? kAutoTaper : 0.0);
+    /* The row kernel without a serial render (C2) has K2 at ~0.16 of K1r's time per frame: 65 536-frame
+     * blocks (a quarter of the launches, of their gaps and prologues) ending in a steep tail
+     * (65 536 -> 16 384 -> 4 096 -> 1 024: the drain stays one short K2) measured +0.8 % on C2
+     * (3 170 -> 3 196 Msamples/s; 32 768 with r = 0.5 +0.5 %, 65 536 with no tail +0.5 %). */
+    const bool row_long = !cw && k1_mode == 3 && !c->serial_render && !c->block_env && n_frames >= 4 * kMaxBlockFrames;
+    const int Tb = std::min(n_frames, ((fir_fused || row_long) && !c->block_env) ? kMaxBlockFrames : c->max_block);
+    const double taper = c->taper >= 0.0 ? c->taper
+                       : (!cw && k1_mode == 3) ? (c->serial_render ? kAutoTaper : (row_long ? kRowTaper : 0.0)) : 0.0;
     const std::vector<std::pair<int, int>> blocks =
         plan_blocks(n_frames, Tb, fir_fused ? 0 : c->first_block, taper, c->taper_min);
     const int n_blocks = (int)blocks.size();
