@@ -132,9 +132,14 @@ SIGNATURES = {
     "icw_stream_seek": (_i, [_vp, _i, C.c_int64]),
     "icw_set_input": (_i, [_vp, C.c_uint32, C.c_uint32, C.c_uint32]),
     "icw_set_fir_hilbert": (_i, [_vp, C.c_int32, C.c_double]),
+    "icw_set_graph": (_i, [_vp, C.POINTER(Node), _i, _i, C.POINTER(_i)]),
+    "icw_set_render": (_i, [_vp, C.POINTER(RenderCfg)]),
+    "icw_set_hilbert_filter": (_i, [_vp, C.c_uint32]),
+    "icw_set_hilbert_config": (_i, [_vp, _i, _i]),
     "icw_fir_taps": (_i, [C.c_int32, C.c_double, _vp, C.c_int]),
     "icw_mod_context_create": (_vp, [C.POINTER(Config), C.POINTER(Node), _i, _i, C.POINTER(_i)]),
     "icw_mod_context_destroy": (None, [_vp]),
+    "icw_mod_context_ctx": (_vp, [_vp]),
     "icw_mod_context_fopen": (_i, [_vp, C.c_uint32, C.c_uint32, C.c_uint32, C.c_int64, C.c_uint32, C.c_uint32,
                                    C.c_uint32, _i, _i]),
     "icw_amod_process_samples": (_i, [_vp, _vp, _vp, _u]),

@@ -43,6 +43,8 @@ icw_mod_context *icw_mod_context_create(const icw_config *cfg, const icw_node *n
     return mc;
 }
 
+icw_ctx *icw_mod_context_ctx(icw_mod_context *mc) { return mc ? mc->ctx : NULL; }
+
 void icw_mod_context_destroy(icw_mod_context *mc)
 {
     if (!mc) return;

@@ -489,6 +489,40 @@ void render_consts(const icw_render_cfg &cfg, int is24, IcwRenderK &k)
     for (int i = 0; i < nc; ++i) k.ns_c[i] = u2d(icw_ns_c[t][i]);
 }
 
+/* The normalised list (graph_accept) as the device program: register form, or the bus form when a
+ * slot is read before its writer runs.  With frmod_scaled the PM frequencies are scaled from f
+ * (dsp_pm) and the Shift ones from |f| (dsp_shift), as DGET_SCALED_FR does per frame. */
+int build_prog(const icw_config &cfg, std::vector<icw_node> &nodes, IcwProg &P)
+{
+    if (cfg.frmod_scaled)
+        for (auto &n : nodes)
+            if (n.mode == ICW_MODE_PM)
+                for (int ch = 0; ch < 2; ++ch) n.pm_freq[ch] = scaled_fr(n.pm_freq[ch]);
+    int rc = compile_graph(nodes, cfg.bypass_list, P);
+    if (rc == ICW_EUNSUPPORTED) rc = compile_bus(nodes, cfg.bypass_list, P);
+    if (rc) return rc;
+    if (cfg.frmod_scaled)
+        for (int i = 0; i < P.n_ops; ++i)
+            if (P.ops[i].mode == ICW_MODE_SHIFT)
+                for (int ch = 0; ch < 2; ++ch) P.ops[i].f[ch] = scaled_fr(P.ops[i].f[ch]);
+    return ICW_OK;
+}
+
+/* ROUND + flat is elementwise (rendered inside the output kernel); every other render keeps serial
+ * per-channel state and runs in the serial render kernel, and so does every render behind a
+ * bus-form graph (frame-serial, hands lOut / rOut over) or with FP_CHECK (the FC() render
+ * arithmetic lives in the serial render kernel only) */
+bool needs_serial(const icw_config &cfg, const IcwRenderK &rk, const IcwProg &P)
+{
+    return !(cfg.render.render_type == ICW_RENDER_ROUND && rk.ns_kind == 0) || P.is_bus || cfg.fp_check;
+}
+
+bool render_cfg_ok(const icw_render_cfg &r)
+{
+    return r.sign_bits16 >= 2 && r.sign_bits16 <= 16 && r.sign_bits24 >= 2 && r.sign_bits24 <= 24 &&
+           r.quantz_type <= 1 && r.render_type <= 4;
+}
+
 int grow(void **p, size_t *cur, size_t need)
 {
     if (*cur >= need) return ICW_OK;
@@ -658,6 +692,81 @@ void free_all(icw_ctx *c)
     if (c->stream) (void)hipStreamDestroy(c->stream);
 }
 
+/* filter coefficients of cfg.hilbert_type exactly as iir_rp_create (hblpf.c:849-856) */
+void set_filter(icw_ctx *c)
+{
+    const int t = (int)c->cfg.hilbert_type;
+    c->nord = icw_hb_order[t];
+    const double a0 = u2d(icw_hb_a[t][0]);
+    c->d0 = u2d(icw_hb_b[t][0]) / a0;
+    for (int i = 0; i < ICW_MAX_IIR_ORDER; ++i) c->pc[i] = c->pd[i] = 0.0;
+    for (int i = 0; i < c->nord; ++i) {
+        c->pc[i] = -u2d(icw_hb_a[t][i + 1]) / a0;
+        c->pd[i] = u2d(icw_hb_b[t][i + 1]) / a0;
+    }
+}
+
+/* renders of streams [f, f + n) as sound_render_init leaves them (in_cwave.c:69-70): MT19937
+ * seeded (mtrnd_init_seed), next draw twists, shaping state zero.  Synchronous. */
+bool seed_renders(icw_ctx *c, size_t f, size_t n, hipStream_t st)
+{
+    DevState &s = c->st;
+    const size_t G = (size_t)c->n_streams * 2;
+    std::vector<uint32_t> col((size_t)624 * n * 2);
+    for (int i = 0; i < 624; ++i)
+        for (size_t k = 0; k < n * 2; ++k) col[(size_t)i * n * 2 + k] = c->mt_seed_state[k & 1][i];
+    std::vector<int32_t> idx(n * 2, 624);
+    bool ok = hipMemcpy2DAsync(s.mt + f * 2, G * 4, col.data(), n * 2 * 4, n * 2 * 4, 624, hipMemcpyHostToDevice,
+                               st) == hipSuccess;
+    ok &= hipMemcpyAsync(s.mt_idx + f * 2, idx.data(), idx.size() * 4, hipMemcpyHostToDevice, st) == hipSuccess;
+    ok &= hipMemsetAsync(s.rs + f * 2 * ICW_RSTATE, 0, n * 2 * ICW_RSTATE * sizeof(double), st) == hipSuccess;
+    ok &= hipStreamSynchronize(st) == hipSuccess;   /* the host sources live until here */
+    return ok;
+}
+
+/* the serial render's per-channel state, allocated when a live change first needs it.  Until then
+ * every render was ROUND + flat, which draws no random numbers and keeps no shaping state, so the
+ * freshly seeded state is the reference's state at this point. */
+int ensure_render_state(icw_ctx *c)
+{
+    DevState &s = c->st;
+    if (s.mt) return ICW_OK;
+    const size_t S = (size_t)c->n_streams;
+    int rc = dalloc(&s.mt, (size_t)624 * S * 2);
+    rc |= dalloc(&s.mt_idx, S * 2);
+    rc |= dalloc(&s.rs, S * 2 * ICW_RSTATE);
+    if (rc == ICW_OK && !seed_renders(c, 0, S, c->stream)) rc = ICW_EDEVICE;
+    if (rc != ICW_OK) {
+        for (void *p : {(void *)s.mt, (void *)s.mt_idx, (void *)s.rs})
+            if (p) (void)hipFree(p);
+        s.mt = nullptr;
+        s.mt_idx = nullptr;
+        s.rs = nullptr;
+        return rc == ICW_ENOMEM ? ICW_ENOMEM : ICW_EDEVICE;
+    }
+    return ICW_OK;
+}
+
+/* The device keeps each channel's largest |q| and get_meters turns it into dB against the render's
+ * current hi bound.  Before a render change moves that bound, the peaks so far are folded into the
+ * host's dB meters against the old bound (the reference converts every sample with the bound of
+ * its time, sound_render.c:769-780) and the device maxima start again. */
+bool fold_peaks(icw_ctx *c)
+{
+    const size_t n = (size_t)c->n_streams * 2;
+    std::vector<unsigned long long> pb(n);
+    bool ok = hipMemcpy(pb.data(), c->st.peak_bits, n * 8, hipMemcpyDeviceToHost) == hipSuccess;
+    ok &= hipMemset(c->st.peak_bits, 0, n * 8) == hipSuccess;
+    if (!ok) return false;
+    for (size_t i = 0; i < n; ++i) {
+        double mx;
+        memcpy(&mx, &pb[i], 8);
+        const double cv = mx ? 20.0 * log10(mx / c->rk.hi) : ICW_SR_ZERO_SIGNAL_DB;
+        if (cv > c->peak_db[i]) c->peak_db[i] = cv;
+    }
+    return true;
+}
+
 }  // namespace
 
 extern "C" {
@@ -685,9 +794,7 @@ int icw_create(const icw_config *cfg, const icw_node *nodes, int n_nodes, int n_
     if (cfg->hilbert_type > 5 || cfg->in_format > ICW_FMT_CW_F32 || cfg->in_channels == 0 ||
         cfg->sample_rate == 0 || cfg->sample_rate > ICW_MAX_FS_SRC)
         return ICW_EINVAL;
-    if (cfg->render.sign_bits16 < 2 || cfg->render.sign_bits16 > 16 || cfg->render.sign_bits24 < 2 ||
-        cfg->render.sign_bits24 > 24 || cfg->render.quantz_type > 1 || cfg->render.render_type > 4)
-        return ICW_EINVAL;
+    if (!render_cfg_ok(cfg->render)) return ICW_EINVAL;
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return ICW_EDEVICE;
     icw_ctx *c = new (std::nothrow) icw_ctx();
@@ -702,38 +809,11 @@ int icw_create(const icw_config *cfg, const icw_node *nodes, int n_nodes, int n_
     const bool ok = graph_accept(c->nodes);
     if (!ok) c->nodes.assign(1, default_master());
     if (accepted) *accepted = ok ? 1 : 0;
-    if (cfg->frmod_scaled)
-        for (auto &n : c->nodes)
-            if (n.mode == ICW_MODE_SHIFT || n.mode == ICW_MODE_PM) {
-                /* scaled frequencies are formed from |f| (dsp_shift) or f (dsp_pm) */
-                for (int ch = 0; ch < 2; ++ch) {
-                    if (n.mode == ICW_MODE_PM) n.pm_freq[ch] = scaled_fr(n.pm_freq[ch]);
-                }
-            }
-    int rc = compile_graph(c->nodes, cfg->bypass_list, c->prog);
-    if (rc == ICW_EUNSUPPORTED) rc = compile_bus(c->nodes, cfg->bypass_list, c->prog);
+    int rc = build_prog(*cfg, c->nodes, c->prog);
     if (rc) { delete c; return rc; }
-    if (cfg->frmod_scaled)
-        for (int i = 0; i < c->prog.n_ops; ++i)
-            if (c->prog.ops[i].mode == ICW_MODE_SHIFT)
-                for (int ch = 0; ch < 2; ++ch) c->prog.ops[i].f[ch] = scaled_fr(c->prog.ops[i].f[ch]);
-    /* filter coefficients exactly as iir_rp_create (hblpf.c:849-856) */
-    const int t = (int)cfg->hilbert_type;
-    c->nord = icw_hb_order[t];
-    const double a0 = u2d(icw_hb_a[t][0]);
-    c->d0 = u2d(icw_hb_b[t][0]) / a0;
-    for (int i = 0; i < c->nord; ++i) {
-        c->pc[i] = -u2d(icw_hb_a[t][i + 1]) / a0;
-        c->pd[i] = u2d(icw_hb_b[t][i + 1]) / a0;
-    }
+    set_filter(c);
     render_consts(cfg->render, cfg->need24bits, c->rk);
-    /* ROUND + flat is elementwise (rendered inside the output kernel); every other render keeps
-     * serial per-channel state and runs in the serial render kernel */
-    c->serial_render = !(cfg->render.render_type == ICW_RENDER_ROUND && c->rk.ns_kind == 0);
-    /* the bus-form graph runs frame-serially and hands lOut/rOut to the serial render */
-    if (c->prog.is_bus) c->serial_render = true;
-    /* FP_CHECK: the FC() render arithmetic lives in the serial render kernel only */
-    if (cfg->fp_check) c->serial_render = true;
+    c->serial_render = needs_serial(*cfg, c->rk, c->prog);
     for (int ch = 0; ch < 2; ++ch) {
         uint32_t *st = c->mt_seed_state[ch];
         st[0] = ch ? cfg->seed_right : cfg->seed_left;         /* mtrnd_init_seed, mt_jrnd.c:28-47 */
@@ -878,21 +958,9 @@ int icw_stream_init(icw_ctx *c, int first, int count)
     std::vector<long long> fd(n * 3);
     for (size_t i = 0; i < n; ++i) { fd[i * 3] = (long long)1 << 62; fd[i * 3 + 1] = 0; fd[i * 3 + 2] = 0; }
     ok &= hipMemcpyAsync(s.fade + f * 3, fd.data(), fd.size() * sizeof(long long), hipMemcpyHostToDevice, st) == hipSuccess;
-    /* host sources of async copies live until the synchronize below */
-    std::vector<uint32_t> col;
-    std::vector<int32_t> idx;
-    if (c->serial_render) {
-        /* renders re-seeded (mod_context_init -> sound_render_init, in_cwave.c:69-70) */
-        const size_t G = (size_t)c->n_streams * 2;
-        col.resize((size_t)624 * n * 2);
-        for (int i = 0; i < 624; ++i)
-            for (size_t k = 0; k < n * 2; ++k) col[(size_t)i * n * 2 + k] = c->mt_seed_state[k & 1][i];
-        ok &= hipMemcpy2DAsync(s.mt + f * 2, G * 4, col.data(), n * 2 * 4, n * 2 * 4, 624, hipMemcpyHostToDevice,
-                               st) == hipSuccess;
-        idx.assign(n * 2, 624);
-        ok &= hipMemcpyAsync(s.mt_idx + f * 2, idx.data(), idx.size() * 4, hipMemcpyHostToDevice, st) == hipSuccess;
-        ok &= hipMemsetAsync(s.rs + f * 2 * ICW_RSTATE, 0, n * 2 * ICW_RSTATE * sizeof(double), st) == hipSuccess;
-    }
+    /* renders re-seeded (mod_context_init -> sound_render_init, in_cwave.c:69-70) wherever their
+     * state exists (a context whose renders never needed it has none yet, ensure_render_state) */
+    if (s.mt) ok &= seed_renders(c, f, n, st);
     ok &= hipStreamSynchronize(st) == hipSuccess;
     for (size_t i = f * 2; i < (f + n) * 2; ++i) c->peak_db[i] = ICW_SR_ZERO_SIGNAL_DB;
     return ok ? ICW_OK : ICW_EDEVICE;
@@ -929,7 +997,7 @@ int icw_stream_open(icw_ctx *c, int s, int64_t n_samples, uint32_t fade_in, uint
     }
     /* sound_render_set_outbits -> sound_render_recalc: prev_rnd, shaper buffers and prev_ns_err
      * reset, the RNG is not (sound_render.c:527-580) */
-    if (c->serial_render)
+    if (c->st.rs)
         ok &= hipMemset(c->st.rs + (size_t)s * 2 * ICW_RSTATE, 0, 2 * ICW_RSTATE * sizeof(double)) == hipSuccess;
     return ok ? ICW_OK : ICW_EDEVICE;
 }
@@ -1027,6 +1095,88 @@ int icw_set_input(icw_ctx *c, uint32_t sample_rate, uint32_t fmt, uint32_t chann
     c->cfg.sample_rate = sample_rate;
     c->cfg.in_format = fmt;
     c->cfg.in_channels = channels;
+    return ICW_OK;
+}
+
+/* Live edits: what the reference's GUI thread changes while a decode thread runs
+ * applies here from the next call on, to every stream of the context; the running call finishes
+ * with the old parameters (quiesce).  Per-stream state carries over as in the reference. */
+int icw_set_graph(icw_ctx *c, const icw_node *nodes, int n_nodes, int bypass_list, int *accepted)
+{
+    if (!c || n_nodes < 0 || (n_nodes > 0 && !nodes)) return ICW_EINVAL;
+    std::vector<icw_node> nv(nodes, nodes + n_nodes);
+    const bool ok = graph_accept(nv);
+    if (accepted) *accepted = ok ? 1 : 0;
+    if (!ok) return ICW_EGRAPH;
+    std::lock_guard<std::mutex> lk(c->mu);
+    if (set_dev(c) || quiesce(c) != hipSuccess) return ICW_EDEVICE;
+    icw_config cfg = c->cfg;
+    cfg.bypass_list = bypass_list ? 1 : 0;
+    IcwProg P;
+    int rc = build_prog(cfg, nv, P);
+    if (rc) return rc;
+    const bool serial = needs_serial(cfg, c->rk, P);
+    if (serial && (rc = ensure_render_state(c))) return rc;
+    if (hipMemcpy(c->d_prog, &P, sizeof(IcwProg), hipMemcpyHostToDevice) != hipSuccess) return ICW_EDEVICE;
+    c->cfg.bypass_list = cfg.bypass_list;
+    c->nodes = nv;
+    c->prog = P;
+    c->serial_render = serial;
+    return ICW_OK;
+}
+
+int icw_set_render(icw_ctx *c, const icw_render_cfg *r)
+{
+    if (!c || !r || !render_cfg_ok(*r)) return ICW_EINVAL;
+    std::lock_guard<std::mutex> lk(c->mu);
+    if (set_dev(c) || quiesce(c) != hipSuccess) return ICW_EDEVICE;
+    IcwRenderK k;
+    render_consts(*r, c->cfg.need24bits, k);
+    icw_config cfg = c->cfg;
+    cfg.render = *r;
+    const bool serial = needs_serial(cfg, k, c->prog);
+    int rc;
+    if (serial && (rc = ensure_render_state(c))) return rc;
+    if (k.hi != c->rk.hi && !fold_peaks(c)) return ICW_EDEVICE;
+    /* sound_render_recalc: prev_rnd, the shaper rings and prev_ns_err start again, the RNG goes on */
+    if (c->st.rs && hipMemset(c->st.rs, 0, (size_t)c->n_streams * 2 * ICW_RSTATE * sizeof(double)) != hipSuccess)
+        return ICW_EDEVICE;
+    c->cfg.render = *r;
+    c->rk = k;
+    c->serial_render = serial;
+    return ICW_OK;
+}
+
+int icw_set_hilbert_filter(icw_ctx *c, uint32_t type)
+{
+    if (!c || type > 5) return ICW_EINVAL;
+    std::lock_guard<std::mutex> lk(c->mu);
+    if (type == c->cfg.hilbert_type) return ICW_OK;
+    if (set_dev(c) || quiesce(c) != hipSuccess) return ICW_EDEVICE;
+    /* hq_rp_create: zero rings, ring index 0, counters 0, phase 0 -- for every stream */
+    const size_t S = (size_t)c->n_streams;
+    DevState &s = c->st;
+    bool ok = hipMemset(s.hist, 0, S * 4 * ICW_HIST_PITCH * sizeof(double)) == hipSuccess;
+    ok &= hipMemset(s.sncnt, 0, S * 4 * sizeof(unsigned long long)) == hipSuccess;
+    ok &= hipMemset(s.hq_phase, 0, S * 2 * sizeof(uint32_t)) == hipSuccess;
+    ok &= hipMemsetD32((hipDeviceptr_t)s.lr_equal, 1, S * 2) == hipSuccess;
+    if (!ok) return ICW_EDEVICE;
+    c->lr_known.assign(S, 1);
+    c->cfg.hilbert_type = type;
+    set_filter(c);
+    return ICW_OK;
+}
+
+int icw_set_hilbert_config(icw_ctx *c, int kahan, int subnorm_reject)
+{
+    if (!c) return ICW_EINVAL;
+    std::lock_guard<std::mutex> lk(c->mu);
+    if (set_dev(c) || quiesce(c) != hipSuccess) return ICW_EDEVICE;
+    /* iir_rp_setcfg: the rings stay, the de-subnorm counters start again ("new world") */
+    if (hipMemset(c->st.sncnt, 0, (size_t)c->n_streams * 4 * sizeof(unsigned long long)) != hipSuccess)
+        return ICW_EDEVICE;
+    c->cfg.iir_kahan = kahan ? 1 : 0;
+    c->cfg.iir_subnorm_reject = subnorm_reject ? 1 : 0;
     return ICW_OK;
 }
 

@@ -139,6 +139,41 @@ class Context:
         beta k_beta, cwave.h:56-58) instead of the quadrature IIR; order 0 restores the IIR"""
         _check(self._lib.icw_set_fir_hilbert(self.h, order, beta), "icw_set_fir_hilbert")
 
+    def _own_cfg(self):
+        """the live setters record the context's parameters in a copy, never in the caller's Config"""
+        self.cfg = abi.Config.from_buffer_copy(self.cfg)
+
+    def set_graph(self, nodes, bypass_list=0):
+        """live DSP-list edit for the next calls (icw_set_graph); returns False when the list is
+        one amod_init would reject (the running list stays)"""
+        arr = (abi.Node * max(1, len(nodes)))(*nodes) if nodes else (abi.Node * 1)()
+        acc = C.c_int()
+        rc = self._lib.icw_set_graph(self.h, arr, len(nodes), int(bypass_list), C.byref(acc))
+        if rc == abi.EGRAPH:
+            return False
+        _check(rc, "icw_set_graph")
+        self._own_cfg()
+        self.cfg.bypass_list = int(bool(bypass_list))
+        return True
+
+    def set_render(self, render):
+        """srenders_set_vcfg for every stream (icw_set_render): an abi.RenderCfg"""
+        _check(self._lib.icw_set_render(self.h, C.byref(render)), "icw_set_render")
+        self._own_cfg()
+        self.cfg.render = render
+
+    def set_hilbert_filter(self, type_):
+        """mod_context_change_all_hilberts_filter (icw_set_hilbert_filter)"""
+        _check(self._lib.icw_set_hilbert_filter(self.h, type_), "icw_set_hilbert_filter")
+        self._own_cfg()
+        self.cfg.hilbert_type = type_
+
+    def set_hilbert_config(self, kahan, subnorm_reject):
+        """mod_context_change_all_hilberts_config (icw_set_hilbert_config)"""
+        _check(self._lib.icw_set_hilbert_config(self.h, int(kahan), int(subnorm_reject)), "icw_set_hilbert_config")
+        self._own_cfg()
+        self.cfg.iir_kahan, self.cfg.iir_subnorm_reject = int(bool(kahan)), int(bool(subnorm_reject))
+
     def stream_open(self, s, n_samples, fade_in_ms=0, fade_out_ms=0, sec_align=0, clr_nframe=0, clr_hilb=0):
         _check(self._lib.icw_stream_open(self.h, s, n_samples, fade_in_ms, fade_out_ms, sec_align,
                                          clr_nframe, clr_hilb), "icw_stream_open")

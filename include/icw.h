@@ -179,6 +179,33 @@ int icw_stream_seek(icw_ctx *ctx, int s, int64_t frame_pos);
  * channels; applies to every stream of the context */
 int icw_set_input(icw_ctx *ctx, uint32_t sample_rate, uint32_t fmt, uint32_t channels);
 
+/* Live parameter changes (the GUI thread edits the DSP list, the renders and the
+ * Hilbert converters while a decode thread runs).  Each applies to every stream of the context from
+ * the next call on; a call already queued finishes with the old parameters.  Per-stream state
+ * (bus slots, rings, MT19937, meters) carries over exactly as the reference carries it.
+ *
+ * icw_set_graph   <- amod_add_lastdsp / amod_del_lastdsp / amod_del_dsplist
+ *                    (adv_modulator.c:358-400), the node-field writes of the GUI
+ *                    (amod_gui_control.c:259-420, 1433-1482) and amod_set_bypass_list_flag
+ *                    (adv_modulator.c:422-425): the whole new list, head first, normalised as
+ *                    icw_create does (locks fanned out).  A list amod_init would reject (no Master
+ *                    at the head, two Masters, unknown mode) returns ICW_EGRAPH with *accepted = 0
+ *                    and leaves the running list in place.  The 27-slot bus keeps its values.
+ * icw_set_render  <- srenders_set_vcfg (in_cwave.c:457-469) -> sound_render_setup
+ *                    (sound_render.c:625-629): the new SR_VCONFIG for both renders of every
+ *                    stream; sound_render_recalc restarts prev_rnd, the shaper rings and
+ *                    prev_ns_err, the MT19937 generators go on.  16/24 bits stay (need24bits).
+ * icw_set_hilbert_filter <- mod_context_change_all_hilberts_filter (in_cwave.c:186-199): a
+ *                    different type re-creates every converter (hq_rp_create: zero rings, phase 0,
+ *                    de-subnorm counters 0); the same type changes nothing.  type 0..5.
+ * icw_set_hilbert_config <- mod_context_change_all_hilberts_config (in_cwave.c:171-182) ->
+ *                    iir_rp_setcfg (hblpf.c:1117-1127): Kahan / baseline summation and the
+ *                    subnormal reject; the rings stay, the de-subnorm counters restart. */
+int icw_set_graph(icw_ctx *ctx, const icw_node *nodes, int n_nodes, int bypass_list, int *accepted);
+int icw_set_render(icw_ctx *ctx, const icw_render_cfg *render);
+int icw_set_hilbert_filter(icw_ctx *ctx, uint32_t type);
+int icw_set_hilbert_config(icw_ctx *ctx, int kahan, int subnorm_reject);
+
 /* FIR Hilbert converter: the converter that CWAVE files record in their header (cwave.h:40,56-58:
  * "Hilbert FIR filter order" k_M, "Hilbert FIR filter parameter" k_beta; gui_cwave.c:159-172 shows
  * them; the converter program is not part of in_cwave).  With k_M > 0, real input is turned on the

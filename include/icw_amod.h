@@ -56,6 +56,12 @@ int icw_mod_context_out_size(const icw_mod_context *mc);
  * the cleared values, as the reference does; the de-subnorm count is kept. */
 int icw_mod_context_meters(icw_mod_context *mc, int reset, icw_meters *m);
 
+/* The context's one-stream icw_ctx, for the live edits of icw.h (icw_set_graph, icw_set_render,
+ * icw_set_hilbert_filter / _config): the reference's GUI applies each edit to both decoding
+ * contexts, the.mc_playback and the.mc_transcode (in_cwave.c:171-199, 457-469), so a port calls
+ * them once per icw_mod_context.  The pointer lives as long as mc. */
+icw_ctx *icw_mod_context_ctx(icw_mod_context *mc);
+
 #ifdef __cplusplus
 }
 #endif

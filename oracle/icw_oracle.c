@@ -679,6 +679,66 @@ void orc_set_input(orc_stream *s, uint32_t sample_rate, uint32_t fmt, uint32_t c
     s->cfg.in_channels = channels;
 }
 
+/* Live edits, applied between blocks as the GUI thread's edits land between frames
+ * of amod_process_samples at block granularity.
+ * The DSP list: amod_add_lastdsp / amod_del_* (adv_modulator.c:358-400) and the node-field
+ * writes, as a whole new list normalised like amod_init; a list amod_init would reject is refused
+ * and the running one stays.  am.is_bypass_list: amod_set_bypass_list_flag (:422-425).  The bus
+ * (mc->inout) is not touched by any of them. */
+int orc_set_graph(orc_stream *s, const icw_node *nodes, int n_nodes, int bypass)
+{
+    icw_node tmp[64];
+    if (n_nodes <= 0 || n_nodes > 64) return 0;
+    memcpy(tmp, nodes, sizeof(icw_node) * (size_t)n_nodes);
+    if (!graph_accept(tmp, n_nodes)) return 0;
+    memcpy(s->nodes, tmp, sizeof(icw_node) * (size_t)n_nodes);
+    s->n_nodes = n_nodes;
+    s->cfg.bypass_list = bypass ? 1 : 0;
+    return 1;
+}
+
+/* srenders_set_vcfg (in_cwave.c:457-469) -> sound_render_setup (sound_render.c:625-629): copy the
+ * config, sound_render_recalc (prev_rnd, shaper rings, prev_ns_err restart; the MT goes on) */
+void orc_set_render(orc_stream *s, const icw_render_cfg *cfg)
+{
+    for (int c = 0; c < 2; ++c) {
+        s->rd[c].cfg = *cfg;
+        render_recalc(&s->rd[c]);
+    }
+    s->cfg.render = *cfg;
+}
+
+/* mod_context_change_all_hilberts_filter (in_cwave.c:186-199): a different type destroys and
+ * re-creates both converters (hq_rp_create, lpf_hilbert_quad.c:80-88: iir_rp_create ->
+ * iir_rp_setcfg + iir_rp_reset, hblpf.c:828-860; sampe_ix = 0) */
+void orc_set_hilbert_filter(orc_stream *s, unsigned type)
+{
+    if (type == s->cfg.hilbert_type || type > 5) return;
+    s->cfg.hilbert_type = type;
+    for (int c = 0; c < 2; ++c) {
+        iir_init(&s->hq[c].I, (int)type, s->cfg.iir_kahan, s->cfg.iir_subnorm_reject);
+        iir_init(&s->hq[c].Q, (int)type, s->cfg.iir_kahan, s->cfg.iir_subnorm_reject);
+        s->hq[c].k = 0;
+        s->hq[c].I.fes = s->hq[c].Q.fes = &s->fes_hilb[c];
+    }
+}
+
+/* mod_context_change_all_hilberts_config (in_cwave.c:171-182) -> hq_rp_setcfg -> iir_rp_setcfg
+ * (hblpf.c:1117-1127): summation and reject switched, rings kept, subnorm_cnt = 0 */
+void orc_set_hilbert_config(orc_stream *s, int kahan, int subn)
+{
+    s->cfg.iir_kahan = kahan ? 1 : 0;
+    s->cfg.iir_subnorm_reject = subn ? 1 : 0;
+    for (int c = 0; c < 2; ++c) {
+        orc_iir *f[2] = {&s->hq[c].I, &s->hq[c].Q};
+        for (int q = 0; q < 2; ++q) {
+            f[q]->kahan = s->cfg.iir_kahan;
+            f[q]->subn = s->cfg.iir_subnorm_reject;
+            f[q]->sncnt = 0;
+        }
+    }
+}
+
 /* mod_context_fopen + xwave_reader_create fade/tail arithmetic; returns n_tail */
 int64_t orc_stream_open(orc_stream *s, int64_t n_samples, uint32_t fade_in, uint32_t fade_out,
                         uint32_t sec_align, int clr_nframe, int clr_hilb)

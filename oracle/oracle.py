@@ -52,6 +52,11 @@ def load():
         lib.orc_hilbert_block.argtypes = [C.c_int, C.c_int, C.c_int, vp, C.c_int, vp, vp]
         lib.orc_render_block.argtypes = [C.POINTER(abi.RenderCfg), C.c_int, C.c_uint32, vp, C.c_int, vp, vp,
                                          C.POINTER(C.c_uint32), C.POINTER(C.c_double)]
+        lib.orc_set_graph.restype = C.c_int
+        lib.orc_set_graph.argtypes = [vp, C.POINTER(abi.Node), C.c_int, C.c_int]
+        lib.orc_set_render.argtypes = [vp, C.POINTER(abi.RenderCfg)]
+        lib.orc_set_hilbert_filter.argtypes = [vp, C.c_uint]
+        lib.orc_set_hilbert_config.argtypes = [vp, C.c_int, C.c_int]
         lib.orc_set_fir.restype = C.c_int
         lib.orc_set_fir.argtypes = [vp, C.c_int, C.c_double]
         lib.orc_fir_taps.restype = C.c_int
@@ -101,6 +106,23 @@ class Stream:
         """the FIR Hilbert converter (icw_set_fir_hilbert); order 0: the quadrature IIR"""
         if load().orc_set_fir(self.h, order, beta) != 0:
             raise ValueError("bad FIR order / beta")
+
+    def set_graph(self, nodes, bypass_list=0):
+        """live DSP-list edit (amod_add_lastdsp / amod_del_* / field writes); False if refused"""
+        arr = (abi.Node * max(1, len(nodes)))(*nodes) if nodes else (abi.Node * 1)()
+        return bool(load().orc_set_graph(self.h, arr, len(nodes), int(bypass_list)))
+
+    def set_render(self, render):
+        """srenders_set_vcfg"""
+        load().orc_set_render(self.h, C.byref(render))
+
+    def set_hilbert_filter(self, type_):
+        """mod_context_change_all_hilberts_filter"""
+        load().orc_set_hilbert_filter(self.h, type_)
+
+    def set_hilbert_config(self, kahan, subn):
+        """mod_context_change_all_hilberts_config"""
+        load().orc_set_hilbert_config(self.h, int(kahan), int(subn))
 
     def set_input(self, sample_rate, fmt, channels):
         load().orc_set_input(self.h, sample_rate, fmt, channels)

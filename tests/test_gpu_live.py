@@ -1,0 +1,230 @@
+"""GPU parity of live parameter changes: the DSP list, the renders and the Hilbert
+converters edited between calls while the streams keep their state, against the oracle given the
+same edits at the same frames, bit for bit (pre-render doubles, rendered bytes, meters).
+
+Edits (include/icw.h):
+  icw_set_graph          amod_add_lastdsp / amod_del_* / node writes, amod_set_bypass_list_flag
+                         (adv_modulator.c:358-425): register form <-> bus form, bypass on / off
+  icw_set_render         srenders_set_vcfg -> sound_render_setup (in_cwave.c:457-469,
+                         sound_render.c:625-629): ROUND <-> dithered / shaped, sign bits (peaks)
+  icw_set_hilbert_filter mod_context_change_all_hilberts_filter (in_cwave.c:186-199)
+  icw_set_hilbert_config mod_context_change_all_hilberts_config -> iir_rp_setcfg (hblpf.c:1117-1127)
+"""
+import numpy as np
+import pytest
+
+from in_cwave_amd import abi, graph, synth
+from tests import graphgen
+from tests.test_gpu_graph_random import differing
+
+pytestmark = pytest.mark.gpu
+
+N_STREAMS = 3
+
+
+def random_render(rng):
+    r = abi.RenderCfg()
+    r.dth_bits = float(rng.choice([0.5, 1.0, 2.0]))
+    r.quantz_type = int(rng.integers(0, 2))
+    r.render_type = int(rng.choice([abi.RENDER_ROUND, abi.RENDER_ROUND, abi.RENDER_RPDF, abi.RENDER_TPDF,
+                                    abi.RENDER_STPDF, abi.RENDER_GAUSS]))
+    r.nshape_type = int(rng.choice([abi.NSHAPE_FLAT, abi.NSHAPE_FLAT, abi.NSHAPE_MEW44,
+                                    int(rng.integers(0, abi.NSHAPE_MAX + 1))]))
+    r.sign_bits16 = int(rng.choice([16, 16, 12, 8]))
+    r.sign_bits24 = int(rng.choice([24, 24, 20, 16]))
+    return r
+
+
+def bad_list(rng):
+    """a list amod_init rejects: two Masters, or none at the head"""
+    nodes = graphgen.random_list(rng, int(rng.integers(2, 5)))
+    if rng.random() < 0.5:
+        nodes[1] = graph.master(inputs=("in",))
+    else:
+        nodes = nodes[1:] + nodes[:1]
+    return nodes
+
+
+def random_edit(rng, ctx, refs, log):
+    kind = str(rng.choice(["graph", "graph", "render", "render", "filter", "config", "feedback"]))
+    if kind in ("graph", "feedback"):
+        r = rng.random()
+        if kind == "feedback":
+            mk = (graph.graph_leaky_feedback, graph.graph_feedback_pm_shift, graph.graph_pure_delay)
+            nodes, bypass = mk[int(rng.integers(0, 3))](), 0
+        elif r < 0.12:
+            nodes, bypass = bad_list(rng), 0
+        else:
+            nodes, bypass = graphgen.random_list(rng), int(rng.random() < 0.2)
+        ok = ctx.set_graph(nodes, bypass)
+        for st in refs:
+            assert st.set_graph(nodes, bypass) == ok
+        log.append(f"graph({len(nodes)} nodes, bypass={bypass}, accepted={ok})")
+    elif kind == "render":
+        r = random_render(rng)
+        ctx.set_render(r)
+        for st in refs:
+            st.set_render(r)
+        log.append(f"render(type={r.render_type}, ns={r.nshape_type}, q={r.quantz_type}, "
+                   f"sb={r.sign_bits16}/{r.sign_bits24})")
+    elif kind == "filter":
+        t = int(rng.integers(0, 6))
+        ctx.set_hilbert_filter(t)
+        for st in refs:
+            st.set_hilbert_filter(t)
+        log.append(f"filter({t})")
+    else:
+        k, sn = int(rng.random() < 0.6), int(rng.random() < 0.7)
+        ctx.set_hilbert_config(k, sn)
+        for st in refs:
+            st.set_hilbert_config(k, sn)
+        log.append(f"config(kahan={k}, subn={sn})")
+
+
+def check_meters(ctx, refs, where):
+    for s, st in enumerate(refs):
+        m, r = ctx.meters(s), st.meters()
+        assert m["clips"] == r["clips"], (where, s, m, r)
+        assert m["desubnorm"] == r["desubnorm"], (where, s, m, r)
+        assert m["peak_db"] == r["peak_db"], (where, s, m, r)
+
+
+def run_sequence(oracle, icw, seed, n_calls=6):
+    rng = np.random.default_rng(7919 * seed + 3)
+    cfg = graphgen.random_config(rng)
+    cfg.need24bits = int(rng.random() < 0.4)
+    if rng.random() < 0.5:
+        cfg.render = random_render(rng)
+    nodes = graphgen.random_list(rng)
+    lens = [int(x) for x in rng.integers(100, 700, size=n_calls)]
+    raw = synth.batch_pcm(N_STREAMS, sum(lens), cfg.sample_rate, first=300 + seed * N_STREAMS)
+    ctx = icw.Context(cfg, nodes, N_STREAMS)
+    refs = [oracle.Stream(cfg, nodes) for _ in range(N_STREAMS)]
+    log, t = [], 0
+    for call, n in enumerate(lens):
+        if call:
+            for _ in range(int(rng.integers(1, 3))):
+                random_edit(rng, ctx, refs, log)
+        seg = np.ascontiguousarray(raw[:, t * 4:(t + n) * 4])
+        out, pre = ctx.process(seg, n, want_pre=True)
+        for s, st in enumerate(refs):
+            ro, rp = st.process(seg[s], n, want_pre=True)
+            bad = differing(pre[s], rp)
+            assert bad.size == 0, (f"seed {seed} call {call} stream {s} after {log}: {bad.size} pre-render "
+                                   f"doubles differ, first {bad[:4]}")
+            assert np.array_equal(out[s], ro), f"seed {seed} call {call} stream {s} after {log}: bytes differ"
+        t += n
+        if call % 2:
+            check_meters(ctx, refs, (seed, call, tuple(log)))
+    check_meters(ctx, refs, (seed, "end", tuple(log)))
+    ctx.close()
+    return log
+
+
+@pytest.mark.parametrize("batch", range(8))
+def test_live_edit_sequences(oracle, icw, batch):
+    """random edit sequences: 8 x 10 seeds, 6 calls each, 1-2 edits before every call after the first"""
+    kinds = set()
+    for seed in range(batch * 10, (batch + 1) * 10):
+        for e in run_sequence(oracle, icw, seed):
+            kinds.add(e.split("(")[0])
+    assert kinds >= {"graph", "render", "filter"}, kinds
+
+
+def test_graph_register_bus_register_keeps_bus(oracle, icw):
+    """register form -> bus form (one-frame feedback) -> register form reading a slot the bus form
+    wrote: the 27-slot bus carries across both switches"""
+    cfg = graph.default_config(48000)
+    reg1 = graph.graph_pm_shift_mix()
+    bus = graph.graph_leaky_feedback()
+    # a register-form list that reads slot "B" without writing it: the bus form's last value
+    reg2 = [graph.master(inputs=("in", "B")), graph.shift(inputs=("in",), out="A", fr=1.5)]
+    raw = synth.batch_pcm(2, 1800, 48000, first=41)
+    ctx = icw.Context(cfg, reg1, 2)
+    refs = [oracle.Stream(cfg, reg1) for _ in range(2)]
+    t = 0
+    for nodes, n in ((None, 600), (bus, 600), (reg2, 600)):
+        if nodes is not None:
+            assert ctx.set_graph(nodes)
+            for st in refs:
+                assert st.set_graph(nodes)
+        seg = np.ascontiguousarray(raw[:, t * 4:(t + n) * 4])
+        out, pre = ctx.process(seg, n, want_pre=True)
+        for s, st in enumerate(refs):
+            ro, rp = st.process(seg[s], n, want_pre=True)
+            assert differing(pre[s], rp).size == 0 and np.array_equal(out[s], ro), (s, t)
+        t += n
+    ctx.close()
+
+
+def test_rejected_graph_keeps_running_list(oracle, icw):
+    cfg = graph.default_config(44100)
+    nodes = graph.graph_shift_master()
+    ctx = icw.Context(cfg, nodes, 1)
+    ref = oracle.Stream(cfg, nodes)
+    raw = synth.batch_pcm(1, 800, 44100, first=3)
+    ctx.process(np.ascontiguousarray(raw[:, :1600]), 400)
+    ref.process(raw[0, :1600], 400)
+    assert not ctx.set_graph([graph.shift(inputs=("in",), out="A"), graph.master(inputs=("A",))])
+    assert not ref.set_graph([graph.shift(inputs=("in",), out="A"), graph.master(inputs=("A",))])
+    out, _ = ctx.process(np.ascontiguousarray(raw[:, 1600:]), 400)
+    ro, _ = ref.process(raw[0, 1600:], 400)
+    assert np.array_equal(out[0], ro)
+    ctx.close()
+
+
+def test_render_change_folds_peaks_and_restarts_shaper(oracle, icw):
+    """16-bit ROUND (elementwise, no render state) -> TPDF + MEW44 with 12 sign bits (the serial
+    render's state is created on the fly, seeded as the reference's never-used generators) -> back;
+    the peak meters keep the maxima measured against each bound"""
+    cfg = graph.default_config(48000)
+    nodes = graph.graph_shift_master()
+    ctx = icw.Context(cfg, nodes, 2)
+    refs = [oracle.Stream(cfg, nodes) for _ in range(2)]
+    raw = synth.batch_pcm(2, 1500, 48000, first=61)
+    r2 = abi.RenderCfg.from_buffer_copy(cfg.render)
+    r2.render_type, r2.nshape_type, r2.sign_bits16 = abi.RENDER_TPDF, abi.NSHAPE_MEW44, 12
+    t = 0
+    for r, n in ((None, 500), (r2, 500), (cfg.render, 500)):
+        if r is not None:
+            ctx.set_render(r)
+            for st in refs:
+                st.set_render(r)
+        seg = np.ascontiguousarray(raw[:, t * 4:(t + n) * 4])
+        out, _ = ctx.process(seg, n)
+        for s, st in enumerate(refs):
+            ro, _ = st.process(seg[s], n)
+            assert np.array_equal(out[s], ro), (s, t)
+        check_meters(ctx, refs, t)
+        t += n
+    ctx.close()
+
+
+@pytest.mark.parametrize("dedup", [False, True])
+def test_hilbert_filter_and_config_changes(oracle, icw, dedup):
+    """type 1 -> 4 (order 20) -> 0 (order 15) -> 0 (no-op) mid-stream, then baseline summation and
+    back to Kahan with the reject off: rings re-created, counters restarted.  Mono input exercises
+    the K1 dedup, whose identical-converter bookkeeping the re-creation must restore."""
+    cfg = graph.default_config(96000, channels=1 if dedup else 2)
+    nodes = graph.graph_master_only()
+    ctx = icw.Context(cfg, nodes, 4)
+    refs = [oracle.Stream(cfg, nodes) for _ in range(4)]
+    fsz = 2 * cfg.in_channels
+    raw = synth.batch_pcm(4, 6 * 700, 96000, channels=cfg.in_channels, first=80)
+    edits = [None, ("f", 4), ("f", 0), ("f", 0), ("c", (0, 1)), ("c", (1, 0))]
+    t = 0
+    for e in edits:
+        if e is not None:
+            for tgt in [ctx] + refs:
+                if e[0] == "f":
+                    tgt.set_hilbert_filter(e[1])
+                else:
+                    tgt.set_hilbert_config(*e[1])
+        seg = np.ascontiguousarray(raw[:, t * fsz:(t + 700) * fsz])
+        out, pre = ctx.process(seg, 700, want_pre=True)
+        for s, st in enumerate(refs):
+            ro, rp = st.process(seg[s], 700, want_pre=True)
+            assert differing(pre[s], rp).size == 0 and np.array_equal(out[s], ro), (e, s)
+        check_meters(ctx, refs, e)
+        t += 700
+    ctx.close()
