@@ -255,6 +255,11 @@ __global__ __launch_bounds__(256) void icw_iir_state(IcwK1Args a)
     /* this block's start (for K2); each (stream, filter) flag is read and written by one wave */
     if (ch == 0) a.info_dup[s * 2 + f] = a.lr_equal[s * 2 + f];
     const double *xp = a.xd + (size_t)g * a.x_pitch;
+    /* the same row through a pointer the compiler cannot equate with xp: the zero-input loops of
+     * orders > 17 load each input into two registers (icw_row_step's xin2), not load + copy */
+    int zoff = 0;
+    asm volatile("" : "+s"(zoff));
+    const double *xp2 = xp + zoff;             /* still a global-memory pointer (no flat loads) */
     double *wrow = a.w + (size_t)g * a.w_pitch;
     /* history rows [0, N): row j = z_{N-1-j} = R[j] */
 #pragma unroll
@@ -403,6 +408,11 @@ __global__ __launch_bounds__(64) void icw_iir_state_fc(IcwK1Args a, int N)
 #pragma unroll 1
     for (int i = 0; i < N; ++i) R[N - 1 - i] = a.hist[(size_t)g * ICW_HIST_PITCH + i];
     const double *xp = a.xd + (size_t)g * a.x_pitch;
+    /* the same row through a pointer the compiler cannot equate with xp: the zero-input loops of
+     * orders > 17 load each input into two registers (icw_row_step's xin2), not load + copy */
+    int zoff = 0;
+    asm volatile("" : "+s"(zoff));
+    const double *xp2 = xp + zoff;             /* still a global-memory pointer (no flat loads) */
     double *wrow = a.w + (size_t)g * a.w_pitch;
 #pragma unroll 1
     for (int j = 0; j < N; ++j) wrow[j] = R[j];
@@ -462,50 +472,76 @@ __device__ __forceinline__ double icw_vmul(double a, double b)
 
 struct IcwRowC {
     double c0, c1;      /* row-uniform: newest two loop-back coefficients */
-    double pl, pl2;     /* per lane: c[l+1], c[l+17] (0 past the order) */
+    double pl, pl2;     /* per lane: c[l+1], c[l+17] (0 past the order); orders > 17 also c0 in lane
+                           N - 17 of pl2 (icw_row_c0_lane) */
     double one;         /* 1.0 in a VGPR (VOP2 src1) */
 };
+
+/* Orders > 17 keep c0 * w in a spare lane of the second product row, so a nonzero-input step reads
+ * its newest term t0 through the DPP operand like the others (icw_row_asm.inc, I0 = 0) instead of
+ * a row-uniform multiply: 77 -> 76 FP64 VALU on those steps.  Orders <= 17 have no second row to
+ * spare (its multiply would cost what it saves). */
+template <int N>
+constexpr bool icw_row_c0p() { return N > 17; }
+template <int N>
+constexpr int icw_row_c0_lane() { return N - 17; }
 
 
 /* one sample at unroll step J; zero-input step when Z != 2 and (J & 1) == Z.  Logical z_i =
  * W[(J-1-i) mod N] (row-uniform); the new w goes to W[J] and its products to P[J] / P2[J].
  * SPEC: the reject (hblpf.c:1046) is speculated away -- w = S unconditionally, and mn tracks the
- * smallest |S| so the block can be re-run exactly if any sum fell below 1 ("Speculative blocks"). */
+ * smallest |S| so the block can be re-run exactly if any sum fell below 1 ("Speculative blocks").
+ * xin2: a second register holding the same input (the zero-input loops of orders > 17 load it
+ * twice), which the I0 = 0 chain turns into T in place. */
 template <int N, int J, int Z, bool SPEC>
 __device__ __forceinline__ void icw_row_step(double (&W)[N], double (&P)[N], double (&P2)[N], double xin,
-                                             const IcwRowC &c, double &mn)
+                                             double xin2, const IcwRowC &c, double &mn)
 {
     constexpr bool ZS = Z != 2 && (J & 1) == Z;
-    double S, Y;
-    if constexpr (ZS) {
-        /* kahan_init(+0) and term 0 collapse to S = t0, C = +0; term 1's Y is t1 */
-        S = W[(J - 1 + N) % N] * c.c0;
-        Y = W[(J - 2 + 2 * N) % N] * c.c1;
+    constexpr bool C0P = icw_row_c0p<N>() && Z != 2 && !ZS;
+    double S;
+    if constexpr (C0P) {
+        /* kahan_init(sample), then every term from a product lane */
+        S = icw_row_chain<N, 0, J>(xin, 0.0, xin2, c.one, P, P2);
     } else {
-        S = xin;                               /* kahan_init(sample) */
-        Y = W[(J - 1 + N) % N] * c.c0;         /* term 0: t0 - 0 */
+        double Y;
+        if constexpr (ZS) {
+            /* kahan_init(+0) and term 0 collapse to S = t0, C = +0; term 1's Y is t1 */
+            S = W[(J - 1 + N) % N] * c.c0;
+            Y = W[(J - 2 + 2 * N) % N] * c.c1;
+        } else {
+            S = xin;                               /* kahan_init(sample) */
+            Y = W[(J - 1 + N) % N] * c.c0;         /* term 0: t0 - 0 */
+        }
+        const double T = S + Y;
+        double NC = Y - (T - S);
+        /* terms I0..N-1: Y = t_i - C with t_i = lane i-1 of P (i-17 of P2), one asm block */
+        S = icw_row_chain<N, ZS ? 2 : 1, J>(T, NC, 0.0, c.one, P, P2);
     }
-    const double T = S + Y;
-    double NC = Y - (T - S);
-    /* terms I0..N-1: Y = t_i - C with t_i = lane i-1 of P (i-17 of P2), one asm block */
-    S = icw_row_chain<N, ZS ? 2 : 1, J>(T, NC, c.one, P, P2);
-    if constexpr (SPEC) mn = icw_minabs_v(mn, S);
-    else S = fabs(S) < 1.0 ? 0.0 : S;          /* hblpf.c:1046 */
+    if constexpr (!SPEC) S = fabs(S) < 1.0 ? 0.0 : S;          /* hblpf.c:1046 */
     W[J] = S;
-    P[J] = icw_vmul(c.pl, S);
+    /* P2 first: the next step's I0 = 0 chain reads lane c0 of P2[J] through DPP, which must come
+     * two VALU instructions after the write (P[J] and the minimum, all volatile asm in order) */
     if constexpr (N > 17) P2[J] = icw_vmul(c.pl2, S);
+    P[J] = icw_vmul(c.pl, S);
+    if constexpr (SPEC) mn = icw_minabs_v(mn, S);
+    else if constexpr (icw_row_c0p<N>()) asm volatile("s_nop 1");   /* exact loops: no minimum */
 }
 
 /* a block of N samples; xv[J] is refilled with the input N samples ahead right after step J when
  * the next block's step J (zero parity ZN) consumes an input */
 template <int N, int J, int Z, int ZN, bool SPEC>
 __device__ __forceinline__ void icw_row_block(double (&W)[N], double (&P)[N], double (&P2)[N], double (&xv)[N],
-                                              const double *xnext, const IcwRowC &c, double &mn)
+                                              double (&xv2)[N], const double *xnext, const double *xnext2,
+                                              const IcwRowC &c, double &mn)
 {
     if constexpr (J < N) {
-        icw_row_step<N, J, Z, SPEC>(W, P, P2, xv[J], c, mn);
-        if constexpr (!(ZN != 2 && (J & 1) == ZN)) xv[J] = xnext[J];
-        icw_row_block<N, J + 1, Z, ZN, SPEC>(W, P, P2, xv, xnext, c, mn);
+        icw_row_step<N, J, Z, SPEC>(W, P, P2, xv[J], xv2[J], c, mn);
+        if constexpr (!(ZN != 2 && (J & 1) == ZN)) {
+            xv[J] = xnext[J];
+            if constexpr (icw_row_c0p<N>() && ZN != 2) xv2[J] = xnext2[J];
+        }
+        icw_row_block<N, J + 1, Z, ZN, SPEC>(W, P, P2, xv, xv2, xnext, xnext2, c, mn);
     }
 }
 
@@ -516,7 +552,7 @@ __device__ __forceinline__ void icw_row_block_lim(double (&W)[N], double (&P)[N]
     if constexpr (J < N) {
         if (J < lim) {
             double mn;
-            icw_row_step<N, J, 2, false>(W, P, P2, xv[J], c, mn);
+            icw_row_step<N, J, 2, false>(W, P, P2, xv[J], 0.0, c, mn);
             icw_row_block_lim<N, J + 1>(W, P, P2, xv, c, lim);
         }
     }
@@ -548,7 +584,8 @@ __device__ __forceinline__ void icw_row_products(const double (&W)[N], double (&
 /* after a failed speculative block at t: the ring from the w row, its products, the block's inputs */
 template <int N>
 __device__ __forceinline__ void icw_row_restart(double (&W)[N], double (&P)[N], double (&P2)[N], double (&xv)[N],
-                                                const double *xp, const double *wrow, int t, const IcwRowC &c)
+                                                double (&xv2)[N], const double *xp, const double *xp2,
+                                                const double *wrow, int t, const IcwRowC &c)
 {
     /* the writer lane stored the row [t, t + N): block start or the previous block */
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
@@ -556,6 +593,7 @@ __device__ __forceinline__ void icw_row_restart(double (&W)[N], double (&P)[N], 
     for (int j = 0; j < N; ++j) W[j] = wrow[t + j];
     icw_row_products<N>(W, P, P2, c);
     icw_load_x<N>(xv, xp + t);
+    if constexpr (icw_row_c0p<N>()) icw_load_x<N>(xv2, xp2 + t);
 }
 
 /* Row layout: wave v holds filter f = v & 1 of the four chain slots 4 (v >> 1) + r, r = row;
@@ -579,7 +617,7 @@ __global__ __launch_bounds__(256) void icw_iir_row(IcwK1Args a)
     c.c0 = a.pc[0];
     c.c1 = a.pc[1];
     c.pl = (lr + 1 < N) ? a.pc[lr + 1] : 0.0;
-    c.pl2 = (lr + 17 < N) ? a.pc[lr + 17] : 0.0;
+    c.pl2 = (lr + 17 < N) ? a.pc[lr + 17] : (icw_row_c0p<N>() && lr == icw_row_c0_lane<N>()) ? a.pc[0] : 0.0;
     c.one = 1.0;
 
     double W[N], P[N], P2[N];
@@ -589,14 +627,20 @@ __global__ __launch_bounds__(256) void icw_iir_row(IcwK1Args a)
 
     if (writer && ch == 0) a.info_dup[s * 2 + f] = a.lr_equal[s * 2 + f];
     const double *xp = a.xd + (size_t)g * a.x_pitch;
+    /* the same row through a pointer the compiler cannot equate with xp: the zero-input loops of
+     * orders > 17 load each input into two registers (icw_row_step's xin2), not load + copy */
+    int zoff = 0;
+    asm volatile("" : "+s"(zoff));
+    const double *xp2 = xp + zoff;             /* still a global-memory pointer (no flat loads) */
     double *wrow = a.w + (size_t)g * a.w_pitch;
     icw_row_store<N>(W, wrow, writer);
 
     const int T = a.T;
     int t = 0;
     if (T >= N) {
-        double xv[N];
+        double xv[N], xv2[N];
         icw_load_x<N>(xv, xp);
+        if constexpr (icw_row_c0p<N>()) icw_load_x<N>(xv2, xp2);
         /* block-relative sample n has a zero input iff (phi + n) is odd (see icw_iir_state) */
         const unsigned phi = (a.hq_phase[s * 2 + ch] + (unsigned)a.t0 + (unsigned)f) & 1u;
         const unsigned phi0 = __builtin_amdgcn_readfirstlane(phi);
@@ -611,34 +655,34 @@ __global__ __launch_bounds__(256) void icw_iir_row(IcwK1Args a)
                 /* odd order: the zero parity alternates block to block; pairs start on a nonzero
                  * sample */
                 if ((phi0 + (unsigned)t) & 1u) {
-                    icw_row_block<N, 0, 0, 1, false>(W, P, P2, xv, xp + t + N, c, mn);
+                    icw_row_block<N, 0, 0, 1, false>(W, P, P2, xv, xv2, xp + t + N, xp2 + t + N, c, mn);
                     icw_row_store<N>(W, wrow + N + t, writer);
                     t += N;
                 }
                 for (; t + 2 * N <= T; t += 2 * N) {
                     /* a failed pair's stores land past [t, t + N), the restart state, and the
                      * exact re-run overwrites them */
-                    icw_row_block<N, 0, 1, 0, true>(W, P, P2, xv, xp + t + N, c, mn);
+                    icw_row_block<N, 0, 1, 0, true>(W, P, P2, xv, xv2, xp + t + N, xp2 + t + N, c, mn);
                     icw_row_store<N>(W, wrow + N + t, writer);
-                    icw_row_block<N, 0, 0, 1, true>(W, P, P2, xv, xp + t + 2 * N, c, mn);
+                    icw_row_block<N, 0, 0, 1, true>(W, P, P2, xv, xv2, xp + t + 2 * N, xp2 + t + 2 * N, c, mn);
                     icw_row_store<N>(W, wrow + 2 * N + t, writer);
                     if (__any(mn < 1.0)) { fail = true; break; }
                 }
             } else if (phi0) {
                 /* even order: the same zero steps in every block */
                 for (; t + N <= T; t += N) {
-                    icw_row_block<N, 0, 0, 0, true>(W, P, P2, xv, xp + t + N, c, mn);
+                    icw_row_block<N, 0, 0, 0, true>(W, P, P2, xv, xv2, xp + t + N, xp2 + t + N, c, mn);
                     icw_row_store<N>(W, wrow + N + t, writer);
                     if (__any(mn < 1.0)) { fail = true; break; }
                 }
             } else {
                 for (; t + N <= T; t += N) {
-                    icw_row_block<N, 0, 1, 1, true>(W, P, P2, xv, xp + t + N, c, mn);
+                    icw_row_block<N, 0, 1, 1, true>(W, P, P2, xv, xv2, xp + t + N, xp2 + t + N, c, mn);
                     icw_row_store<N>(W, wrow + N + t, writer);
                     if (__any(mn < 1.0)) { fail = true; break; }
                 }
             }
-            if (fail) icw_row_restart<N>(W, P, P2, xv, xp, wrow, t, c);
+            if (fail) icw_row_restart<N>(W, P, P2, xv, xv2, xp, xp2, wrow, t, c);
             else icw_load_x<N>(xv, xp + t);   /* the zero steps left part of xv unloaded */
         }
         if (fail) {
@@ -646,31 +690,31 @@ __global__ __launch_bounds__(256) void icw_iir_row(IcwK1Args a)
             ICW_DRAIN_VMEM();
             if constexpr (N & 1) {
                 if (((phi0 + (unsigned)t) & 1u) && t + N <= T) {
-                    icw_row_block<N, 0, 0, 1, false>(W, P, P2, xv, xp + t + N, c, mn);
+                    icw_row_block<N, 0, 0, 1, false>(W, P, P2, xv, xv2, xp + t + N, xp2 + t + N, c, mn);
                     icw_row_store<N>(W, wrow + N + t, writer);
                     t += N;
                 }
                 for (; t + 2 * N <= T; t += 2 * N) {
-                    icw_row_block<N, 0, 1, 0, false>(W, P, P2, xv, xp + t + N, c, mn);
+                    icw_row_block<N, 0, 1, 0, false>(W, P, P2, xv, xv2, xp + t + N, xp2 + t + N, c, mn);
                     icw_row_store<N>(W, wrow + N + t, writer);
-                    icw_row_block<N, 0, 0, 1, false>(W, P, P2, xv, xp + t + 2 * N, c, mn);
+                    icw_row_block<N, 0, 0, 1, false>(W, P, P2, xv, xv2, xp + t + 2 * N, xp2 + t + 2 * N, c, mn);
                     icw_row_store<N>(W, wrow + 2 * N + t, writer);
                 }
             } else if (phi0) {
                 for (; t + N <= T; t += N) {
-                    icw_row_block<N, 0, 0, 0, false>(W, P, P2, xv, xp + t + N, c, mn);
+                    icw_row_block<N, 0, 0, 0, false>(W, P, P2, xv, xv2, xp + t + N, xp2 + t + N, c, mn);
                     icw_row_store<N>(W, wrow + N + t, writer);
                 }
             } else {
                 for (; t + N <= T; t += N) {
-                    icw_row_block<N, 0, 1, 1, false>(W, P, P2, xv, xp + t + N, c, mn);
+                    icw_row_block<N, 0, 1, 1, false>(W, P, P2, xv, xv2, xp + t + N, xp2 + t + N, c, mn);
                     icw_row_store<N>(W, wrow + N + t, writer);
                 }
             }
             icw_load_x<N>(xv, xp + t);
         }
         for (; t + N <= T; t += N) {
-            icw_row_block<N, 0, 2, 2, false>(W, P, P2, xv, xp + t + N, c, mn);
+            icw_row_block<N, 0, 2, 2, false>(W, P, P2, xv, xv2, xp + t + N, xp2 + t + N, c, mn);
             icw_row_store<N>(W, wrow + N + t, writer);
         }
     }
