@@ -56,9 +56,11 @@ FP64_PEAK_TFLOPS = 78.6        # MI355X FP64 vector (256 CU x 2.4 GHz x 128 flop
 CLOCK_GHZ = 2.31
 # Issue floor of the recurrence: a lone wave issues one FP64 VALU instruction per
 # ~5.0 cycles, dependent or not (profiles/r01_fp64_bank_probe.txt).  icw_iir_state<19> issues 91
-# FP64 VALU per sample (zero-input steps included), icw_iir_row<19> 75.5 (products lane-parallel,
-# the Kahan steps through v_fmac_f64_dpp row_newbcast).
-K1_VALU_PER_SAMPLE = {0: 91.1, 3: 75.6}        # by ICW_K1_* (icw_last_k1_kernel); ISA: 3461 / 2874 VALU per 38-sample pair
+# FP64 VALU per sample (zero-input steps included), icw_iir_row<19> 75.4 (products lane-parallel,
+# the Kahan steps through v_fmac_f64_dpp row_newbcast, t0 from a spare lane of the second row).
+# SQ counters: profiles/r02_c3_sq.json (K1), profiles/r02_c2_sq.json (K1r: 3955034 VALU per wave
+# and launch of 52429 samples per chain).
+K1_VALU_PER_SAMPLE = {0: 91.1, 3: 75.4}        # by ICW_K1_* (icw_last_k1_kernel)
 K1_KERNEL_NAME = {0: "icw_iir_state", 3: "icw_iir_row", 4: "icw_iir_state_fc"}
 CYC_PER_FP64_VALU = 5.0
 
