@@ -228,3 +228,42 @@ def test_hilbert_filter_and_config_changes(oracle, icw, dedup):
         check_meters(ctx, refs, e)
         t += 700
     ctx.close()
+
+
+@pytest.mark.parametrize("mono", [False, True])
+def test_edits_between_multi_block_calls(oracle, icw, mono):
+    """calls long enough for several launch blocks (the multi-stream pipeline, block scratch sets,
+    the serial render one block behind): ROUND register form -> TPDF + MEW44 behind a bus-form
+    list (serial render state created between calls) -> filter type 4 -> back to ROUND + register
+    form; every block of every call bit for bit"""
+    ch = 1 if mono else 2
+    cfg = graph.default_config(48000, channels=ch)
+    nodes = graph.graph_shift_master()
+    n = 36000
+    raw = synth.batch_pcm(3, 4 * n, 48000, channels=ch, first=500)
+    fsz = 2 * ch
+    ctx = icw.Context(cfg, nodes, 3)
+    refs = [oracle.Stream(cfg, nodes) for _ in range(3)]
+    r2 = abi.RenderCfg.from_buffer_copy(cfg.render)
+    r2.render_type, r2.nshape_type = abi.RENDER_TPDF, abi.NSHAPE_MEW44
+
+    def edit_graph(t, nn):
+        assert t.set_graph(nn)
+
+    edits = [None,
+             [lambda t: t.set_render(r2), lambda t: edit_graph(t, graph.graph_feedback_pm_shift())],
+             [lambda t: t.set_hilbert_filter(4)],
+             [lambda t: t.set_render(cfg.render), lambda t: edit_graph(t, graph.graph_pm_shift_mix())]]
+    for k, e in enumerate(edits):
+        for f in (e or []):
+            for tgt in [ctx] + refs:
+                f(tgt)
+        seg = np.ascontiguousarray(raw[:, k * n * fsz:(k + 1) * n * fsz])
+        out, pre = ctx.process(seg, n, want_pre=True)
+        for s, st in enumerate(refs):
+            ro, rp = st.process(seg[s], n, want_pre=True)
+            bad = differing(pre[s], rp)
+            assert bad.size == 0, (k, s, bad[:4])
+            assert np.array_equal(out[s], ro), (k, s)
+        check_meters(ctx, refs, k)
+    ctx.close()
