@@ -221,9 +221,14 @@ __device__ __forceinline__ void icw_fir_stage(const IcwFirArgs &f, int s, int ch
     }
 }
 
+/* The taps through the constant address space: every lane of a wave reads the same tap, so they
+ * come in by scalar loads into SGPRs (the FMA takes one SGPR operand) and leave the LDS pipe to the
+ * inputs -- which bounds the sums: 52 -> 44 LDS reads per 8-tap block of a lane's 8 outputs. */
+typedef const __attribute__((address_space(4))) double icw_ctap;
+
 /* one 8-tap block (k0 = 8b) of a lane's 8 outputs: bl / br = physical index of the first input of
  * the left / right window (both at phase 2 of the pad pattern) */
-__device__ __forceinline__ void icw_fir_block8(const double *xs, const double *gs, int k0, int bl, int br,
+__device__ __forceinline__ void icw_fir_block8(const double *xs, icw_ctap *gs, int k0, int bl, int br,
                                                double (&acc)[ICW_FIR_R])
 {
     constexpr int W = ICW_FIR_R + 14;
@@ -249,7 +254,7 @@ __device__ __forceinline__ void icw_fir_block8(const double *xs, const double *g
 }
 
 /* Q of a lane's 8 outputs tt + 8 ll + r; a = (c - 1 + sh) / 8 */
-__device__ __forceinline__ void icw_fir_sums(const double *xs, const double *gs, int nt, int ll, int a, int sh, int c,
+__device__ __forceinline__ void icw_fir_sums(const double *xs, icw_ctap *gs, int nt, int ll, int a, int sh, int c,
                                              double (&acc)[ICW_FIR_R])
 {
 #pragma unroll
@@ -289,9 +294,8 @@ __global__ __launch_bounds__(256) void icw_fir_hilbert(IcwFirArgs a)
     const int nf = min(TF, a.T - tt);
     icw_fir_stage(a, s, ch, xs, tt, TF, sh, threadIdx.x, 256);
     const int px = icw_fir_phys(sh + M + TF + 24) + 1;
-    double *gs = xs + px;
-    double *qs = gs + ((a.nt + 1) & ~1);
-    for (int k = threadIdx.x; k < a.nt; k += 256) gs[k] = a.g[k];
+    double *qs = xs + px + ((a.nt + 1) & ~1);
+    icw_ctap *gs = (icw_ctap *)a.g;
     __syncthreads();
     double acc[ICW_FIR_R];
     icw_fir_sums(xs, gs, a.nt, threadIdx.x, av, sh, c, acc);
@@ -881,13 +885,12 @@ __global__ __launch_bounds__(256, 4) void icw_fir_graph(IcwFirArgs f, IcwK2Args 
     const int av = (c - 1 + sh) >> 3;
     const int nf = min(TF, f.T - tt);
     const int px = icw_fir_phys(sh + M + TF + 24) + 1;     /* doubles per staged channel */
-    double *gs = lds + nchc * px;
-    double *lregs = gs + ((f.nt + 1) & ~1);
+    double *lregs = lds + nchc * px + ((f.nt + 1) & ~1);
+    icw_ctap *gs = (icw_ctap *)f.g;
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const int ch = nchc == 2 ? lane >> 5 : 0;
     const int ll = nchc == 2 ? wv * 32 + (lane & 31) : threadIdx.x;   /* lane index within the channel */
     for (int k = 0; k < nchc; ++k) icw_fir_stage(f, s, k, lds + k * px, tt, TF, sh, threadIdx.x, 256);
-    for (int k = threadIdx.x; k < f.nt; k += 256) gs[k] = f.g[k];
     __syncthreads();
     double q[ICW_FIR_R], vi[ICW_FIR_R];
     icw_fir_sums(lds + ch * px, gs, f.nt, ll, av, sh, c, q);
