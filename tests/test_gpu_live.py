@@ -267,3 +267,36 @@ def test_edits_between_multi_block_calls(oracle, icw, mono):
             assert np.array_equal(out[s], ro), (k, s)
         check_meters(ctx, refs, k)
     ctx.close()
+
+
+def test_edits_with_fir_converter(oracle, icw):
+    """the FIR Hilbert converter on (fused KF2 while the list fits its LDS, KF + K2 otherwise):
+    list and render edits between calls, the converter's history carried; a Hilbert-type change
+    leaves the FIR converter alone (it replaces the quadrature IIR)"""
+    cfg = graph.default_config(48000)
+    nodes = graph.graph_shift_master()
+    ctx = icw.Context(cfg, nodes, 2)
+    ctx.set_fir_hilbert(254, 8.0)
+    refs = [oracle.Stream(cfg, nodes) for _ in range(2)]
+    for st in refs:
+        st.set_fir(254, 8.0)
+    r2 = abi.RenderCfg.from_buffer_copy(cfg.render)
+    r2.render_type, r2.nshape_type = abi.RENDER_RPDF, abi.NSHAPE_FLAT
+    edits = [None,
+             [lambda t: t.set_graph(graph.graph_pm_shift_mix())],
+             [lambda t: t.set_render(r2), lambda t: t.set_hilbert_filter(3)],
+             [lambda t: t.set_graph(graph.graph_leaky_feedback())],
+             [lambda t: t.set_graph(graph.graph_master_only())]]
+    n = 5000
+    raw = synth.batch_pcm(2, n * len(edits), 48000, first=700)
+    for k, e in enumerate(edits):
+        for f in (e or []):
+            for tgt in [ctx] + refs:
+                f(tgt)
+        seg = np.ascontiguousarray(raw[:, k * n * 4:(k + 1) * n * 4])
+        out, pre = ctx.process(seg, n, want_pre=True)
+        for s, st in enumerate(refs):
+            ro, rp = st.process(seg[s], n, want_pre=True)
+            assert differing(pre[s], rp).size == 0 and np.array_equal(out[s], ro), (k, s)
+        check_meters(ctx, refs, k)
+    ctx.close()
