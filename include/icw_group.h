@@ -32,6 +32,8 @@ int icw_group_destroy(icw_group *g);
 /* shard d: its first stream, stream count, device and context (for per-stream calls such as
  * icw_stream_open / icw_set_state, with stream index s - first) */
 int icw_group_shard(const icw_group *g, int d, int *first, int *count, int *device, icw_ctx **ctx);
+/* Live edits (icw_set_graph / icw_set_render / icw_set_hilbert_filter / _config, icw.h) apply per
+ * context: call them on every shard's ctx to change the whole group. */
 
 /* icw_process_batch over the whole group with HOST pointers: stream s at in + s*in_stride, out +
  * s*out_stride (dbg: double[n_streams][n_frames][2] with ICW_F_DEBUG_PRE).  Every device's thread
