@@ -255,11 +255,6 @@ __global__ __launch_bounds__(256) void icw_iir_state(IcwK1Args a)
     /* this block's start (for K2); each (stream, filter) flag is read and written by one wave */
     if (ch == 0) a.info_dup[s * 2 + f] = a.lr_equal[s * 2 + f];
     const double *xp = a.xd + (size_t)g * a.x_pitch;
-    /* the same row through a pointer the compiler cannot equate with xp: the zero-input loops of
-     * orders > 17 load each input into two registers (icw_row_step's xin2), not load + copy */
-    int zoff = 0;
-    asm volatile("" : "+s"(zoff));
-    const double *xp2 = xp + zoff;             /* still a global-memory pointer (no flat loads) */
     double *wrow = a.w + (size_t)g * a.w_pitch;
     /* history rows [0, N): row j = z_{N-1-j} = R[j] */
 #pragma unroll
@@ -408,11 +403,6 @@ __global__ __launch_bounds__(64) void icw_iir_state_fc(IcwK1Args a, int N)
 #pragma unroll 1
     for (int i = 0; i < N; ++i) R[N - 1 - i] = a.hist[(size_t)g * ICW_HIST_PITCH + i];
     const double *xp = a.xd + (size_t)g * a.x_pitch;
-    /* the same row through a pointer the compiler cannot equate with xp: the zero-input loops of
-     * orders > 17 load each input into two registers (icw_row_step's xin2), not load + copy */
-    int zoff = 0;
-    asm volatile("" : "+s"(zoff));
-    const double *xp2 = xp + zoff;             /* still a global-memory pointer (no flat loads) */
     double *wrow = a.w + (size_t)g * a.w_pitch;
 #pragma unroll 1
     for (int j = 0; j < N; ++j) wrow[j] = R[j];
