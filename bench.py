@@ -238,11 +238,24 @@ def cpu_baseline(workers, n_frames, wname):
         per = pool.map(_cpu_worker, [(s, n_frames, wname, cpus[s]) for s in range(workers)])
     wall = time.perf_counter() - t0
     samples = 2.0 * n_frames * workers
-    return {"value": samples / max(per) / 1e6, "unit": "Msamples/s", "cores": workers, "kind": "port",
-            "cpu_model": model, "per_core": 2.0 * n_frames / float(np.mean(per)) / 1e6, "topology": topo,
-            "sample": f"{workers} streams x {n_frames} frames ({wname} shape), oracle C restatement "
-                      f"(-O2 -ffp-contract=off), one process pinned per physical core, wall {wall:.1f}s; "
-                      f"the reference's own IIR/graph/render need <windows.h> and are not built here"}
+    out = {"value": samples / max(per) / 1e6, "unit": "Msamples/s", "cores": workers, "kind": "port",
+           "cpu_model": model, "per_core": 2.0 * n_frames / float(np.mean(per)) / 1e6, "topology": topo,
+           "sample": f"{workers} streams x {n_frames} frames ({wname} shape), oracle C restatement "
+                     f"(-O2 -ffp-contract=off), one process pinned per physical core, wall {wall:.1f}s; "
+                     f"the reference's own IIR/graph/render need <windows.h> and are not built here"}
+    # the restatement's speed against the reference C on one CPU type (tools/cpu_calibrate.py,
+    # against BASELINE.md's reference numbers measured on the same container CPU)
+    cal = _latest("r*_cpu_calibration.json")
+    if cal is not None:
+        try:
+            r = json.loads(cal.read_text().strip().splitlines()[-1])["workloads"].get(wname)
+            if r:
+                out["calibration"] = {"oracle_over_reference": r["oracle_over_reference"], "cpu": "container Xeon",
+                                      "reference_equivalent_value": out["value"] / r["oracle_over_reference"],
+                                      "source": f"profiles/{cal.name}"}
+        except (ValueError, KeyError):
+            pass
+    return out
 
 
 # ----------------------------------------------------------------------------- C1 leg -------
