@@ -204,6 +204,5 @@ def test_dropin_boundary_takes_cwave(oracle, icw, fmt):
             assert lib.icw_amod_process_samples(buf.ctypes.data, mc, blk.ctypes.data, k) == k
             got.append(buf)
         ro, _ = ref.process(raw, n)
-        d = np.abs(np.concatenate(got).view("<i2").astype(int) - ro.view("<i2").astype(int))
-        assert d.max() <= 1 and (d > 0).mean() < 1e-3, (track, d.max())    # Shift: sin/cos ulps
+        assert np.array_equal(np.concatenate(got), ro), track     # Shift factors glibc-identical
     lib.icw_mod_context_destroy(mc)

@@ -300,3 +300,47 @@ def test_edits_with_fir_converter(oracle, icw):
             assert differing(pre[s], rp).size == 0 and np.array_equal(out[s], ro), (k, s)
         check_meters(ctx, refs, k)
     ctx.close()
+
+
+def test_dropin_context_live_edits(oracle, icw):
+    """the drop-in boundary: icw_amod_process_samples in 576-frame blocks (playback.c:619), with
+    the GUI's edits applied between blocks through icw_mod_context_ctx -- list, render, filter"""
+    import ctypes as C
+    lib = icw.load()
+    fs = 44100
+    cfg = graph.default_config(fs)
+    nodes = graph.graph_shift_master()
+    arr = graph.node_array(nodes)
+    st = C.c_int()
+    mc = lib.icw_mod_context_create(C.byref(cfg), arr, len(nodes), 0, C.byref(st))
+    assert mc and st.value == abi.OK
+    ctx = lib.icw_mod_context_ctx(mc)
+    assert ctx
+    ref = oracle.Stream(cfg, nodes)
+    osz = lib.icw_mod_context_out_size(mc)
+    n = 576 * 12
+    raw = synth.batch_pcm(1, n, fs, first=31)[0]
+    r2 = abi.RenderCfg.from_buffer_copy(cfg.render)
+    r2.render_type, r2.nshape_type = abi.RENDER_TPDF, abi.NSHAPE_MEW44
+    pm = graph.graph_pm_shift_mix()
+    got, ro = [], []
+    for b in range(12):
+        if b == 3:
+            acc = C.c_int()
+            assert lib.icw_set_graph(ctx, graph.node_array(pm), len(pm), 0, C.byref(acc)) == abi.OK and acc.value
+            assert ref.set_graph(pm)
+        if b == 6:
+            assert lib.icw_set_render(ctx, C.byref(r2)) == abi.OK
+            ref.set_render(r2)
+        if b == 9:
+            assert lib.icw_set_hilbert_filter(ctx, 2) == abi.OK
+            ref.set_hilbert_filter(2)
+        blk = np.ascontiguousarray(raw[b * 576 * 4:(b + 1) * 576 * 4])
+        buf = np.zeros(576 * osz, np.uint8)
+        assert lib.icw_amod_process_samples(buf.ctypes.data, mc, blk.ctypes.data, 576) == 576
+        got.append(buf)
+        o, _ = ref.process(blk, 576)
+        ro.append(o)
+    for b in range(12):
+        assert np.array_equal(got[b], ro[b]), b
+    lib.icw_mod_context_destroy(mc)
