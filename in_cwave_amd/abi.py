@@ -98,7 +98,8 @@ class StateBlob(C.Structure):
     """the per-stream state blob of icw_get_state / icw_set_state"""
     _fields_ = [("magic", C.c_uint64), ("n_frame", C.c_uint64), ("pos", C.c_int64), ("n_samples", C.c_int64),
                 ("n_fade_in", C.c_int64), ("n_fade_out", C.c_int64), ("hq_phase", C.c_uint32 * 2),
-                ("nord", C.c_uint32), ("has_render", C.c_uint32), ("hist", (C.c_double * 20) * 4),
+                ("nord", C.c_uint32), ("has_render", C.c_uint32), ("fir_M", C.c_uint32), ("reserved", C.c_uint32),
+                ("hist", (C.c_double * 20) * 4),
                 ("sncnt", C.c_uint64 * 4), ("bus", (C.c_double * 4) * N_INPUTS),
                 ("mt", (C.c_uint32 * 624) * 2), ("mt_idx", C.c_int32 * 2), ("rs", (C.c_double * RSTATE) * 2)]
 
@@ -134,6 +135,7 @@ SIGNATURES = {
     "icw_set_fir_hilbert": (_i, [_vp, C.c_int32, C.c_double]),
     "icw_set_graph": (_i, [_vp, C.POINTER(Node), _i, _i, C.POINTER(_i)]),
     "icw_set_render": (_i, [_vp, C.POINTER(RenderCfg)]),
+    "icw_clear_bus_slot": (_i, [_vp, _i]),
     "icw_set_hilbert_filter": (_i, [_vp, C.c_uint32]),
     "icw_set_hilbert_config": (_i, [_vp, _i, _i]),
     "icw_fir_taps": (_i, [C.c_int32, C.c_double, _vp, C.c_int]),

@@ -767,6 +767,16 @@ bool fold_peaks(icw_ctx *c)
     return true;
 }
 
+/* mod_context_clear_all_inouts (in_cwave.c:255-261): slot `slot` of every stream's bus to zero.
+ * The context's work has been waited for (quiesce). */
+int clear_slot(icw_ctx *c, int slot)
+{
+    if (slot < 0 || slot >= ICW_N_INPUTS) return ICW_OK;
+    const size_t pitch = (size_t)ICW_N_INPUTS * 4 * sizeof(double);
+    return hipMemset2D(c->st.bus + (size_t)slot * 4, pitch, 0, 4 * sizeof(double), (size_t)c->n_streams) == hipSuccess
+               ? ICW_OK : ICW_EDEVICE;
+}
+
 }  // namespace
 
 extern "C" {
@@ -1118,11 +1128,27 @@ int icw_set_graph(icw_ctx *c, const icw_node *nodes, int n_nodes, int bypass_lis
     const bool serial = needs_serial(cfg, c->rk, P);
     if (serial && (rc = ensure_render_state(c))) return rc;
     if (hipMemcpy(c->d_prog, &P, sizeof(IcwProg), hipMemcpyHostToDevice) != hipSuccess) return ICW_EDEVICE;
+    /* replace_output_plug (adv_modulator.c:176-209) of the removed / re-plugged nodes, matched by
+     * position (include/icw.h): their old output slots read zero from now on */
+    for (size_t i = 0; i < c->nodes.size(); ++i) {
+        const icw_node &o = c->nodes[i];
+        if (o.mode != ICW_MODE_SHIFT && o.mode != ICW_MODE_PM && o.mode != ICW_MODE_MIX) continue;
+        if (i >= nv.size() || nv[i].mode != o.mode || nv[i].n_out != o.n_out)
+            if (clear_slot(c, o.n_out) != ICW_OK) return ICW_EDEVICE;
+    }
     c->cfg.bypass_list = cfg.bypass_list;
     c->nodes = nv;
     c->prog = P;
     c->serial_render = serial;
     return ICW_OK;
+}
+
+int icw_clear_bus_slot(icw_ctx *c, int slot)
+{
+    if (!c || slot < 0 || slot >= ICW_N_INPUTS) return ICW_EINVAL;
+    std::lock_guard<std::mutex> lk(c->mu);
+    if (set_dev(c) || quiesce(c) != hipSuccess) return ICW_EDEVICE;
+    return clear_slot(c, slot);
 }
 
 int icw_set_render(icw_ctx *c, const icw_render_cfg *r)
@@ -1408,12 +1434,22 @@ int icw_process_streams(icw_ctx *c, int first, int count, const void *in, size_t
         af.nt = c->fir_nt;
         af.g = c->d_fir_g;
         const size_t hrow = 2 * (size_t)c->fir_M;
-        af.hist_in = c->fir_hist[c->fir_par] + f0 * hrow;
-        af.hist_out = c->fir_hist[c->fir_par ^ 1] + f0 * hrow;
-        c->fir_par ^= 1;
+        af.hist_in = c->fir_hist[(c->fir_par + b) & 1] + f0 * hrow;
+        af.hist_out = c->fir_hist[(c->fir_par + b + 1) & 1] + f0 * hrow;
         af.xd = c->xd[b % n_sets];
         af.x_pitch = x_pitch;
         return af;
+    };
+    /* pinned host input: block b's input slice of every stream goes in on the copy stream, and the
+     * stream of the block's first reader (K0, KF or the fused KF2) waits for it */
+    auto io_in = [&](int b, hipStream_t s0) -> int {
+        if (!pipe_io) return ICW_OK;
+        const int t0 = blocks[b].first, T = blocks[b].second;
+        if (hipMemcpy2DAsync(c->d_in + (size_t)t0 * fsz, dis, (const unsigned char *)in + (size_t)t0 * fsz, in_stride,
+                             (size_t)T * fsz, S, hipMemcpyHostToDevice, sC) != hipSuccess ||
+            hipEventRecord(c->ev_io[b], sC) != hipSuccess || hipStreamWaitEvent(s0, c->ev_io[b], 0) != hipSuccess)
+            return ICW_EDEVICE;
+        return ICW_OK;
     };
     /* K0 of block b on sA: xd[p] was last read by K1 of block b-2 (and, complex input, by K2 of
      * block b-2, which precedes it on sA) */
@@ -1446,13 +1482,7 @@ int icw_process_streams(icw_ctx *c, int first, int count, const void *in, size_t
             s0 = sK;
             if (b >= n_sets && hipStreamWaitEvent(sK, c->k2done[p], 0) != hipSuccess) return ICW_EDEVICE;
         }
-        if (pipe_io) {
-            /* this block's input slice of every stream, on the copy stream */
-            if (hipMemcpy2DAsync(c->d_in + (size_t)t0 * fsz, dis, (const unsigned char *)in + (size_t)t0 * fsz, in_stride,
-                                 (size_t)T * fsz, S, hipMemcpyHostToDevice, sC) != hipSuccess ||
-                hipEventRecord(c->ev_io[b], sC) != hipSuccess || hipStreamWaitEvent(s0, c->ev_io[b], 0) != hipSuccess)
-                return ICW_EDEVICE;
-        }
+        if (io_in(b, s0) != ICW_OK) return ICW_EDEVICE;
         if (fir) {
             IcwFirArgs af = fir_args(b);
             if (timing && hipEventRecord(c->ev[4 * b], s0) != hipSuccess) return ICW_EDEVICE;
@@ -1591,6 +1621,7 @@ int icw_process_streams(icw_ctx *c, int first, int count, const void *in, size_t
         if (timing && hipEventRecord(c->ev[4 * b + 2], s2) != hipSuccess) return ICW_EDEVICE;
         if (fir_fused) {
             const IcwFirArgs af = fir_args(b);
+            if (io_in(b, s2) != ICW_OK) return ICW_EDEVICE;
             if (timing && hipEventRecord(c->ev[4 * b], s2) != hipSuccess) return ICW_EDEVICE;
             if (icw_launch_fir_graph(&af, &a2, s2) != hipSuccess) return ICW_EDEVICE;
             if (timing && hipEventRecord(c->ev[4 * b + 1], s2) != hipSuccess) return ICW_EDEVICE;
@@ -1672,6 +1703,15 @@ int icw_process_streams(icw_ctx *c, int first, int count, const void *in, size_t
     for (hipStream_t x : {sK, sA, sD, sR, sF, sC})
         if (x && x != st && (hipEventRecord(c->join, x) != hipSuccess || hipStreamWaitEvent(st, c->join, 0) != hipSuccess))
             return ICW_EDEVICE;
+    /* FIR history: the current rows of every stream stay in fir_hist[fir_par] between calls (a call on
+     * a subset of the streams must not move the others' rows); after an odd number of blocks this
+     * call's rows are in the other buffer and come back */
+    if (fir && (n_blocks & 1)) {
+        const size_t hrow = 2 * (size_t)c->fir_M;
+        if (hipMemcpyAsync(c->fir_hist[c->fir_par] + f0 * hrow, c->fir_hist[c->fir_par ^ 1] + f0 * hrow,
+                           S * hrow * sizeof(double), hipMemcpyDeviceToDevice, st) != hipSuccess)
+            return ICW_EDEVICE;
+    }
     {
         IcwAdvArgs av;
         memset(&av, 0, sizeof(av));
@@ -1810,6 +1850,7 @@ struct IcwBlob {
     uint64_t magic, n_frame;
     int64_t pos, n_samples, n_fade_in, n_fade_out;
     uint32_t hq_phase[2], nord, has_render;
+    uint32_t fir_M, reserved;         /* FIR converter order in force (0: the quadrature IIR) */
     double hist[4][ICW_HIST_PITCH];
     uint64_t sncnt[4];
     double bus[ICW_N_INPUTS][4];
@@ -1819,7 +1860,7 @@ struct IcwBlob {
     int32_t mt_idx[2];
     double rs[2][ICW_RSTATE];
 };
-constexpr uint64_t kBlobMagic = 0x32574349ull;   /* "ICW2" */
+constexpr uint64_t kBlobMagic = 0x33574349ull;   /* "ICW3" */
 
 /* with the FIR Hilbert converter on, its history (2 x k_M doubles, oldest first) follows the blob */
 size_t icw_state_size(const icw_ctx *c) { return c ? sizeof(IcwBlob) + 2 * (size_t)c->fir_M * sizeof(double) : 0; }
@@ -1834,6 +1875,7 @@ int icw_get_state(icw_ctx *c, int s, void *blob, size_t size)
     b.magic = kBlobMagic;
     b.nord = (uint32_t)c->nord;
     b.has_render = c->serial_render ? 1u : 0u;
+    b.fir_M = (uint32_t)c->fir_M;
     long long fd[3];
     bool ok = quiesce(c) == hipSuccess;
     ok &= hipMemcpy(&b.n_frame, c->st.n_frame + s, 8, hipMemcpyDeviceToHost) == hipSuccess;
@@ -1866,7 +1908,10 @@ int icw_set_state(icw_ctx *c, int s, const void *blob, size_t size)
     if (!c || !blob || size < icw_state_size(c) || s < 0 || s >= c->n_streams) return ICW_EINVAL;
     IcwBlob b;
     memcpy(&b, blob, sizeof(b));
-    if (b.magic != kBlobMagic || b.nord != (uint32_t)c->nord || b.has_render != (c->serial_render ? 1u : 0u))
+    /* a blob holds the state of the render and converter forms in force when it was saved: the
+     * serial-render words exist only with a dithered / shaped render, the FIR history only at its order */
+    if (b.magic != kBlobMagic || b.nord != (uint32_t)c->nord || b.has_render != (c->serial_render ? 1u : 0u) ||
+        b.fir_M != (uint32_t)c->fir_M)
         return ICW_EINVAL;
     std::lock_guard<std::mutex> lk(c->mu);
     if (set_dev(c)) return ICW_EDEVICE;

@@ -156,6 +156,10 @@ class Context:
         self.cfg.bypass_list = int(bool(bypass_list))
         return True
 
+    def clear_bus_slot(self, slot):
+        """mod_context_clear_all_inouts for every stream (icw_clear_bus_slot): slot 0..26 to zero"""
+        _check(self._lib.icw_clear_bus_slot(self.h, int(slot)), "icw_clear_bus_slot")
+
     def set_render(self, render):
         """srenders_set_vcfg for every stream (icw_set_render): an abi.RenderCfg"""
         _check(self._lib.icw_set_render(self.h, C.byref(render)), "icw_set_render")

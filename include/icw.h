@@ -190,7 +190,17 @@ int icw_set_input(icw_ctx *ctx, uint32_t sample_rate, uint32_t fmt, uint32_t cha
  *                    (adv_modulator.c:422-425): the whole new list, head first, normalised as
  *                    icw_create does (locks fanned out).  A list amod_init would reject (no Master
  *                    at the head, two Masters, unknown mode) returns ICW_EGRAPH with *accepted = 0
- *                    and leaves the running list in place.  The 27-slot bus keeps its values.
+ *                    and leaves the running list in place.  The 27-slot bus keeps its values,
+ *                    except the slots the reference clears: amod_del_lastdsp, amod_del_dsplist and
+ *                    amod_set_output_plug go through replace_output_plug (adv_modulator.c:176-209),
+ *                    which zeroes the removed / re-plugged node's old output slot in every context
+ *                    (mod_context_clear_all_inouts, in_cwave.c:255-261).  The new list is matched to
+ *                    the old one by position: an old Shift / PM / Mix node whose position is gone,
+ *                    now holds a node of another mode, or whose n_out changed has its old slot
+ *                    zeroed for every stream.  Edits that position matching cannot see (a re-plug to
+ *                    the same slot, delete + add of an identical node) call icw_clear_bus_slot.
+ * icw_clear_bus_slot <- mod_context_clear_all_inouts (in_cwave.c:255-261): bus slot 0..26 of
+ *                    every stream to zero (the 4 doubles L re/im, R re/im).
  * icw_set_render  <- srenders_set_vcfg (in_cwave.c:457-469) -> sound_render_setup
  *                    (sound_render.c:625-629): the new SR_VCONFIG for both renders of every
  *                    stream; sound_render_recalc restarts prev_rnd, the shaper rings and
@@ -202,6 +212,7 @@ int icw_set_input(icw_ctx *ctx, uint32_t sample_rate, uint32_t fmt, uint32_t cha
  *                    iir_rp_setcfg (hblpf.c:1117-1127): Kahan / baseline summation and the
  *                    subnormal reject; the rings stay, the de-subnorm counters restart. */
 int icw_set_graph(icw_ctx *ctx, const icw_node *nodes, int n_nodes, int bypass_list, int *accepted);
+int icw_clear_bus_slot(icw_ctx *ctx, int slot);
 int icw_set_render(icw_ctx *ctx, const icw_render_cfg *render);
 int icw_set_hilbert_filter(icw_ctx *ctx, uint32_t type);
 int icw_set_hilbert_config(icw_ctx *ctx, int kahan, int subnorm_reject);

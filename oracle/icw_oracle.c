@@ -683,14 +683,29 @@ void orc_set_input(orc_stream *s, uint32_t sample_rate, uint32_t fmt, uint32_t c
  * of amod_process_samples at block granularity.
  * The DSP list: amod_add_lastdsp / amod_del_* (adv_modulator.c:358-400) and the node-field
  * writes, as a whole new list normalised like amod_init; a list amod_init would reject is refused
- * and the running one stays.  am.is_bypass_list: amod_set_bypass_list_flag (:422-425).  The bus
- * (mc->inout) is not touched by any of them. */
+ * and the running one stays.  am.is_bypass_list: amod_set_bypass_list_flag (:422-425).
+ * Bus slots: amod_del_lastdsp / amod_del_dsplist and amod_set_output_plug go through
+ * replace_output_plug (adv_modulator.c:176-209), which zeroes the removed or re-plugged node's old
+ * output slot in every context (mod_context_clear_all_inouts, in_cwave.c:255-261).  A whole-list
+ * edit is matched to those primitives by position: an old Shift / PM / Mix node whose position is
+ * gone, holds a node of another mode, or whose n_out changed had its old slot cleared.  Any other
+ * slot keeps its value (orc_clear_inout is the primitive itself). */
+void orc_clear_inout(orc_stream *s, int slot)
+{
+    if (slot >= 0 && slot < ICW_N_INPUTS) memset(&s->bus[slot], 0, sizeof(s->bus[slot]));
+}
+
 int orc_set_graph(orc_stream *s, const icw_node *nodes, int n_nodes, int bypass)
 {
     icw_node tmp[64];
     if (n_nodes <= 0 || n_nodes > 64) return 0;
     memcpy(tmp, nodes, sizeof(icw_node) * (size_t)n_nodes);
     if (!graph_accept(tmp, n_nodes)) return 0;
+    for (int i = 0; i < s->n_nodes; ++i) {
+        const icw_node *o = &s->nodes[i];
+        if (o->mode != ICW_MODE_SHIFT && o->mode != ICW_MODE_PM && o->mode != ICW_MODE_MIX) continue;
+        if (i >= n_nodes || tmp[i].mode != o->mode || tmp[i].n_out != o->n_out) orc_clear_inout(s, o->n_out);
+    }
     memcpy(s->nodes, tmp, sizeof(icw_node) * (size_t)n_nodes);
     s->n_nodes = n_nodes;
     s->cfg.bypass_list = bypass ? 1 : 0;

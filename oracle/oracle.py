@@ -55,6 +55,7 @@ def load():
         lib.orc_set_graph.restype = C.c_int
         lib.orc_set_graph.argtypes = [vp, C.POINTER(abi.Node), C.c_int, C.c_int]
         lib.orc_set_render.argtypes = [vp, C.POINTER(abi.RenderCfg)]
+        lib.orc_clear_inout.argtypes = [vp, C.c_int]
         lib.orc_set_hilbert_filter.argtypes = [vp, C.c_uint]
         lib.orc_set_hilbert_config.argtypes = [vp, C.c_int, C.c_int]
         lib.orc_set_fir.restype = C.c_int
@@ -111,6 +112,10 @@ class Stream:
         """live DSP-list edit (amod_add_lastdsp / amod_del_* / field writes); False if refused"""
         arr = (abi.Node * max(1, len(nodes)))(*nodes) if nodes else (abi.Node * 1)()
         return bool(load().orc_set_graph(self.h, arr, len(nodes), int(bypass_list)))
+
+    def clear_bus_slot(self, slot):
+        """mod_context_clear_all_inouts (in_cwave.c:255-261): bus slot `slot` to zero"""
+        load().orc_clear_inout(self.h, int(slot))
 
     def set_render(self, render):
         """srenders_set_vcfg"""

@@ -176,3 +176,89 @@ def test_fir_off_restores_quadrature_iir(oracle, icw):
     ro, rp = oracle.process_streams(cfg, nodes, raw, 2000, want_pre=True)
     assert_parity(out, pre, ro, rp)
     ctx.close()
+
+
+def test_fir_pinned_host_buffers_many_blocks(oracle, icw):
+    """pinned host in / out buffers (icw_host_alloc) on a call of several launch blocks: each block's
+    input slice goes H2D on the copy stream before the block's converter reads it (KF or the fused
+    KF2), and three blocks leave the history in the second buffer, which the call copies back"""
+    from in_cwave_amd import lib as L
+    cfg = graph.default_config(48000)
+    nodes = graph.graph_shift_master()
+    n = 3 * 65536 - 1000
+    raw = synth.batch_pcm(2, n, 48000)
+    ctx = icw.Context(cfg, nodes, 2)
+    ctx.set_fir_hilbert(254, BETA)
+    h_in = L.host_array(raw.shape)
+    h_in[:] = raw
+    h_out = L.host_array((2, n * 4))
+    for call in range(2):          # the second call starts from the history the first one left
+        seg = raw if call == 0 else np.ascontiguousarray(raw[:, ::-1])
+        h_in[:] = seg
+        ctx.process(h_in, n, out=h_out)
+        if call == 0:
+            ro, _ = oracle.process_streams(cfg, nodes, seg, n, fir=(254, BETA))
+            assert np.array_equal(np.asarray(h_out), ro)
+    refs = [oracle.Stream(cfg, nodes) for _ in range(2)]
+    for s, st in enumerate(refs):
+        st.set_fir(254, BETA)
+        st.process(raw[s], n)
+        r2, _ = st.process(np.ascontiguousarray(raw[s, ::-1]), n)
+        assert np.array_equal(np.asarray(h_out)[s], r2), s
+    ctx.close()
+
+
+def test_fir_subset_calls_keep_other_streams_history(oracle, icw, monkeypatch):
+    """icw_process_streams on subsets with odd and even block counts: every stream's history stays
+    its own (a subset call must not move the other streams' current history buffer)"""
+    monkeypatch.setenv("ICW_BLOCK", "4096")
+    cfg = graph.default_config(48000)
+    nodes = graph.graph_pm_shift_mix()
+    S = 3
+    calls = [(0, 1, 3000), (0, 3, 2500), (1, 2, 9000), (0, 3, 4100), (2, 1, 5000), (0, 3, 700)]
+    total = [0] * S
+    for f, cnt, n in calls:
+        for s in range(f, f + cnt):
+            total[s] += n
+    raw = synth.batch_pcm(S, max(total), 48000, first=900)
+    ctx = icw.Context(cfg, nodes, S)
+    ctx.set_fir_hilbert(510, BETA)
+    refs = [oracle.Stream(cfg, nodes) for _ in range(S)]
+    for st in refs:
+        st.set_fir(510, BETA)
+    pos = [0] * S
+    for k, (f, cnt, n) in enumerate(calls):
+        seg = np.stack([raw[s, pos[s] * 4:(pos[s] + n) * 4] for s in range(f, f + cnt)])
+        out, pre = ctx.process(seg, n, first=f, count=cnt, want_pre=True)
+        for i, s in enumerate(range(f, f + cnt)):
+            ro, rp = refs[s].process(seg[i], n, want_pre=True)
+            assert np.array_equal(pre[i].view(np.uint64), rp.view(np.uint64)), (k, s)
+            assert np.array_equal(out[i], ro), (k, s)
+            pos[s] += n
+    ctx.close()
+
+
+def test_fir_state_blob_records_order(icw):
+    """the blob carries the FIR order in force; a blob of another order (or of the IIR) is refused"""
+    cfg = graph.default_config(48000)
+    nodes = graph.graph_shift_master()
+    a = icw.Context(cfg, nodes, 1)
+    a.set_fir_hilbert(254, BETA)
+    assert icw.load().icw_state_size(a.h) == C_sizeof_blob() + 2 * 254 * 8
+    blob = a.get_state(0)
+    assert abi.StateBlob.from_buffer_copy(blob).fir_M == 254
+    b = icw.Context(cfg, nodes, 1)
+    b.set_fir_hilbert(510, BETA)
+    big = blob + bytes(2 * 256 * 8)
+    with pytest.raises(Exception):
+        b.set_state(0, big)
+    b.set_fir_hilbert(0, 0.0)
+    with pytest.raises(Exception):
+        b.set_state(0, blob)
+    for c in (a, b):
+        c.close()
+
+
+def C_sizeof_blob():
+    import ctypes
+    return ctypes.sizeof(abi.StateBlob)

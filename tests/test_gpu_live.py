@@ -344,3 +344,43 @@ def test_dropin_context_live_edits(oracle, icw):
     for b in range(12):
         assert np.array_equal(got[b], ro[b]), b
     lib.icw_mod_context_destroy(mc)
+
+
+@pytest.mark.parametrize("form", ["register", "bus"])
+def test_deleted_writer_slot_reads_zero(oracle, icw, form):
+    """amod_del_lastdsp / amod_set_output_plug -> replace_output_plug (adv_modulator.c:176-209): the
+    removed or re-plugged node's old slot is zeroed in every stream (mod_context_clear_all_inouts,
+    in_cwave.c:255-261) while a Mix still reads it; icw_clear_bus_slot is the primitive itself.  The
+    bus form (a one-frame delay: the Mix reads A before the Shift writes it) reads the cleared slot
+    in the first frame of the next call."""
+    cfg = graph.default_config(48000)
+    if form == "register":
+        l1 = [graph.master(inputs=("C",)), graph.mix(inputs=("in", "A"), out="C"),
+              graph.shift(inputs=("in",), out="A", fr=3.0)]
+    else:
+        l1 = [graph.master(inputs=("C",)), graph.shift(inputs=("in",), out="A", fr=3.0),
+              graph.mix(inputs=("in", "A"), out="C")]
+    # register form: the writer deleted; bus form: a parameter edit keeps A, the explicit clear zeroes it
+    l2 = l1[:2] if form == "register" else [l1[0], graph.shift(inputs=("in",), out="A", fr=5.0), l1[2]]
+    l3 = [l2[0], l2[1], graph.mix(inputs=("in", "A"), out="D")]      # re-plugged C -> D: C cleared
+    raw = synth.batch_pcm(3, 2400, 48000, first=77)
+    ctx = icw.Context(cfg, l1, 3)
+    refs = [oracle.Stream(cfg, l1) for _ in range(3)]
+    t = 0
+    for step in ("none", "l2", "clear", "l3"):
+        if step in ("l2", "l3"):
+            nn = l2 if step == "l2" else l3
+            assert ctx.set_graph(nn)
+            for st in refs:
+                assert st.set_graph(nn)
+        elif step == "clear":
+            ctx.clear_bus_slot(graph.slot("A"))
+            for st in refs:
+                st.clear_bus_slot(graph.slot("A"))
+        seg = np.ascontiguousarray(raw[:, t * 4:(t + 600) * 4])
+        out, pre = ctx.process(seg, 600, want_pre=True)
+        for s, st in enumerate(refs):
+            ro, rp = st.process(seg[s], 600, want_pre=True)
+            assert differing(pre[s], rp).size == 0 and np.array_equal(out[s], ro), (step, s)
+        t += 600
+    ctx.close()

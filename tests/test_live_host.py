@@ -8,7 +8,8 @@ need no GPU.  The GPU parity of the same edits is tests/test_gpu_live.py.
     restarts the de-subnorm counters;
   srenders_set_vcfg -> sound_render_setup (sound_render.c:625-629): after ROUND (which draws nothing)
     the new render runs as a freshly seeded one on the same pre-render doubles;
-  amod_add_lastdsp / amod_del_* keep the bus: a list reading a slot the old list wrote sees it.
+  amod_del_* / amod_set_output_plug zero the removed / re-plugged node's old slot (replace_output_plug,
+    adv_modulator.c:176-209); every other slot keeps its value.
 """
 import numpy as np
 
@@ -85,19 +86,49 @@ def test_render_change_after_round_is_a_fresh_render(oracle):
         assert np.array_equal(got[:, ch, :].reshape(-1), ref), ch
 
 
-def test_graph_change_keeps_bus_and_rejects_bad_lists(oracle):
+def test_graph_change_clears_removed_writers_and_rejects_bad_lists(oracle):
+    """amod_del_lastdsp -> replace_output_plug (adv_modulator.c:176-209, 377-390): the deleted node's
+    output slot is zeroed in every context (mod_context_clear_all_inouts, in_cwave.c:255-261), so a
+    node still reading it reads 0 from then on"""
     cfg = graph.default_config(48000)
     writer = [graph.master(inputs=("A",)), graph.shift(inputs=("in",), out="A", fr=2.5)]
-    reader = [graph.master(inputs=("A",))]        # reads A, which nobody writes any more
+    reader = [graph.master(inputs=("A",))]        # the Shift deleted: A is cleared
     raw = synth.batch_pcm(1, 600, 48000, first=16)[0]
     a = oracle.Stream(cfg, writer)
     _, p1 = a.process(raw[:300 * 4], 300, want_pre=True)
+    assert np.any(p1 != 0.0)
     assert not a.set_graph([graph.shift(inputs=("in",), out="A"), graph.master(inputs=("A",))])
     assert not a.set_graph([graph.master(), graph.master()])
     assert a.set_graph(reader)
     _, p2 = a.process(raw[300 * 4:], 300, want_pre=True)
-    # the Master now converts the frozen last value of A every frame
-    assert np.all(p2 == p2[0]) and np.any(p2[0] != 0.0)
+    assert np.all(p2 == 0.0)
+
+
+def test_graph_change_keeps_other_slots(oracle):
+    """a parameter edit keeps every slot: a one-frame delay (Mix reads A before the Shift writes it
+    in the frame, doc 3.1) sees last call's A in the first frame of the next call; an explicit
+    mod_context_clear_all_inouts of A makes that first frame read 0 instead"""
+    cfg = graph.default_config(48000)
+    delay = [graph.master(inputs=("B",)), graph.shift(inputs=("in",), out="A", fr=2.0),
+             graph.mix(inputs=("A",), out="B")]
+    edited = [graph.master(inputs=("B",)), graph.shift(inputs=("in",), out="A", fr=3.0),
+              graph.mix(inputs=("A",), out="B", gain=0.7)]
+    raw = synth.batch_pcm(1, 600, 48000, first=17)[0]
+    a, b = oracle.Stream(cfg, delay), oracle.Stream(cfg, delay)
+    for st in (a, b):
+        st.process(raw[:300 * 4], 300)
+        assert st.set_graph(edited)
+    b.clear_bus_slot(graph.slot("A"))
+    _, pa = a.process(raw[300 * 4:], 300, want_pre=True)
+    _, pb = b.process(raw[300 * 4:], 300, want_pre=True)
+    assert np.any(pa[0] != 0.0) and np.all(pb[0] == 0.0)
+    assert np.array_equal(pa[1:], pb[1:])
+    # position matching: the Mix re-plugged to C clears B (the Master reads it, nobody writes it)
+    c = oracle.Stream(cfg, delay)
+    c.process(raw[:300 * 4], 300)
+    assert c.set_graph(edited[:2] + [graph.mix(inputs=("A",), out="C")])
+    _, pc = c.process(raw[300 * 4:], 300, want_pre=True)
+    assert np.all(pc == 0.0)
 
 
 def test_live_setters_reject_bad_arguments_without_gpu(icw):
@@ -107,3 +138,4 @@ def test_live_setters_reject_bad_arguments_without_gpu(icw):
     assert lib.icw_set_hilbert_config(None, 1, 1) == abi.EINVAL
     assert lib.icw_set_render(None, None) == abi.EINVAL
     assert lib.icw_set_graph(None, None, 0, 0, None) == abi.EINVAL
+    assert lib.icw_clear_bus_slot(None, 1) == abi.EINVAL
