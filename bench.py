@@ -54,15 +54,20 @@ FP64_PEAK_TFLOPS = 78.6        # MI355X FP64 vector (256 CU x 2.4 GHz x 128 flop
 # effective engine clock under the C2 recurrence: SQ_BUSY_CYCLES / 32 shader engines / launch time
 # of the K1 kernel in the newest committed SQ pass (profiles/r*_c2_sq.json; r01: 2.31 GHz)
 CLOCK_GHZ = 2.31
-# Issue floor of the recurrence: a lone wave issues one FP64 VALU instruction per
-# ~5.0 cycles, dependent or not (profiles/r01_fp64_bank_probe.txt).  icw_iir_state<19> issues 91
-# FP64 VALU per sample (zero-input steps included), icw_iir_row<19> 75.4 (products lane-parallel,
-# the Kahan steps through v_fmac_f64_dpp row_newbcast, t0 from a spare lane of the second row).
-# SQ counters: profiles/r02_c3_sq.json (K1), profiles/r02_c2_sq.json (K1r: 3955034 VALU per wave
-# and launch of 52429 samples per chain).
+# Issue model of the recurrence: a chain costs (VALU instructions per sample) x
+# (cycles per VALU).  Both come from the newest committed SQ pass of the workload
+# (profiles/r*_<workload>_sq.json: SQ_INSTS_VALU per wave / samples per chain, and the profiled
+# launch time x SQ_BUSY_CYCLES clock / VALU per wave); the fallbacks are the round-2 figures
+# (icw_iir_state<19> 91.1, icw_iir_row<19> 75.4 VALU per sample; 4.83 cycles per VALU).
 K1_VALU_PER_SAMPLE = {0: 91.1, 3: 75.4}        # by ICW_K1_* (icw_last_k1_kernel)
 K1_KERNEL_NAME = {0: "icw_iir_state", 3: "icw_iir_row", 4: "icw_iir_state_fc"}
-CYC_PER_FP64_VALU = 5.0
+CYC_PER_FP64_VALU = 4.83
+# the path's algorithmic FP64 work per frame is the whole Kahan IIR of
+# iir_rp_process_kahan (hblpf.c:1017-1056): 15N - 4 flops per filter-sample (N = 19: 281), over the
+# 4 filters of a stereo frame (1 124) or the 2 of a mono frame under the dedup (562) -- the
+# loop-back sum (K1, 5N per sample) plus the output sum (K2)
+def chain_flops_per_frame(ch):
+    return (2 if ch == 1 else 4) * (15 * IIR_ORDER - 4)
 
 
 def _latest(pattern):
@@ -125,6 +130,8 @@ def parse():
                     help="c2 at N=1: skip the short C1/C3/C4/C5 runs reported under other_workloads")
     ap.add_argument("--cpu-workers", type=int, default=0, help="0: one per physical core available here")
     ap.add_argument("--cpu-frames", type=int, default=1 << 25)
+    ap.add_argument("--other-frames", type=int, default=None,
+                    help="frames per stream of the other_workloads legs (default: each workload's)")
     ap.add_argument("--block", type=int, default=576, help="c1: frames per boundary call (NS_PERTIME)")
     ap.add_argument("--e2e-steps", type=int, default=2,
                     help="extra steps with host buffers (H2D + D2H included), reported beside `value`")
@@ -342,29 +349,60 @@ def measure_c1(steps, warmup, block, with_cpu):
 
 
 # ----------------------------------------------------------------------------- GPU leg ------
-def fir_roofline(W, S, T, kf_ms, kf_n, k2_ms, k2_n):
-    """roofline of the FIR converter KF (icw_fir_hilbert) per launch, from its HIP events: per
-    channel-sample nt taps x (1 subtract + 1 FMA = 3 flops) and 2 LDS reads of 8 B; its HBM bytes
-    are the raw input (read) and the I/Q rows it hands to K2 (4 x 8 B per frame, written)"""
+def pmc_traffic(wname, kernel, frames_per_launch):
+    """HBM bytes per launch of `kernel` in the newest committed PMC pass of this workload
+    (profiles/r*_<workload>_pmc.json, 2 x FETCH_SIZE + WRITE_SIZE, MI355X_MICROARCH.md's gfx950
+    correction), scaled to this run's frames per launch; (bytes, file name) or (None, None)"""
+    f = _latest(f"r*_{wname}_pmc.json")
+    if f is None:
+        return None, None
+    try:
+        pmc = json.loads(f.read_text())
+        for k, v in pmc["kernels"].items():
+            if k.split("<")[0].split("(")[0].split()[-1] == kernel:
+                return v["hbm_bytes_corrected"] * frames_per_launch / float(pmc["frames_per_launch"]), f.name
+    except (ValueError, KeyError, OSError):
+        pass
+    return None, None
+
+
+def sq_model(wname, kernel):
+    """(VALU per wave, cycles per VALU, clock GHz, launch ns, file) of `kernel` in the newest SQ pass"""
+    f = _latest(f"r*_{wname}_sq.json")
+    if f is None:
+        return None
+    try:
+        for k, v in json.loads(f.read_text())["kernels"].items():
+            if kernel in k:
+                cpv = v["avg_launch_ns_trace"] * v["effective_clock_ghz"] / v["valu_per_wave"]
+                return v["valu_per_wave"], cpv, v["effective_clock_ghz"], v["avg_launch_ns_trace"], f.name
+    except (ValueError, KeyError, OSError, ZeroDivisionError):
+        pass
+    return None
+
+
+def fir_roofline(wname, W, S, T, kf_ms, kf_n, k2_ms, k2_n, fused):
+    """roofline of the FIR converter per launch, from its HIP events: per channel-sample nt odd
+    taps x (1 subtract + 1 FMA = 3 flops); HBM traffic from the workload's committed PMC pass"""
     M = W["fir"]
     nt = (M // 2 + 1) // 2
     chans = 1 if W["ch"] == 1 else 2
     frames_per_launch = float(S) * T / max(1, kf_n)
     avg_s = kf_ms / 1e3 / max(1, kf_n)
     flops_per_frame = chans * nt * 3
-    in_b = {"i16": 2, "f32": 4}[W["fmt"]] * W["ch"]
-    kbytes = in_b + 32
+    kname = "icw_fir_graph" if fused else "icw_fir_hilbert"
+    traffic, src = pmc_traffic(wname, kname, frames_per_launch)
     tf = flops_per_frame * frames_per_launch / avg_s / 1e12 if avg_s > 0 else None
-    gbs = kbytes * frames_per_launch / avg_s / 1e9 if avg_s > 0 else None
-    lds_tbs = chans * nt * 16 * frames_per_launch / avg_s / 1e12 if avg_s > 0 else None
+    alg_b = W["bytes"] * frames_per_launch
+    gbs = (traffic if traffic else alg_b) / avg_s / 1e9 if avg_s > 0 else None
     return {"bound": "fp64", "achieved": tf, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
-            "frac": (tf / FP64_PEAK_TFLOPS) if tf else None, "traffic": None, "kernel": "icw_fir_hilbert",
+            "frac": (tf / FP64_PEAK_TFLOPS) if tf else None, "traffic": traffic, "kernel": kname,
             "fir_order": M, "taps_odd": nt, "flops_per_frame": flops_per_frame, "frames_per_launch": frames_per_launch,
             "avg_launch_ms": avg_s * 1e3, "output_kernel_avg_launch_ms": k2_ms / max(1, k2_n),
             "hbm": {"achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": (gbs / HBM_PEAK_GBS) if gbs else None,
-                    "kernel_bytes_per_frame": kbytes},
-            "lds_read_tbs": lds_tbs,
-            "note": "FIR Hilbert converter KF: per channel-sample nt odd taps, each 2 LDS reads + subtract + FMA; "
+                    "bytes_per_frame": (traffic if traffic else alg_b) / frames_per_launch,
+                    "source": f"profiles/{src} (PMC)" if traffic else "algorithmic in + out bytes (no PMC pass)"},
+            "note": "FIR Hilbert converter: per channel-sample nt odd taps, each a subtract + FMA; "
                     "frame-parallel (no recurrence), so it fills the chip"}
 
 
@@ -450,7 +488,7 @@ def measure_gpu(wname, streams, frames, steps, warmup, e2e_steps, dev, local_dev
                        "beside the other blocks' kernels; one GPU"}
 
     if W.get("fir"):
-        roof = fir_roofline(W, S, T, k1_ms, k1_n, k2_ms, k2_n)
+        roof = fir_roofline(wname, W, S, T, k1_ms, k1_n, k2_ms, k2_n, os.environ.get("ICW_FIR_FUSED", "1") != "0")
         ctx.close()
         return {"value": value, "ms_per_step": ms_per_step, "roofline": roof, "e2e": e2e, "W": W, "S": S, "T": T,
                 "fs": fs}
@@ -466,26 +504,25 @@ def measure_gpu(wname, streams, frames, steps, warmup, e2e_steps, dev, local_dev
     flops_per_frame = chains_per_stream * 5 * IIR_ORDER   # loop-back Kahan sum: N x (1 mul + 4 add)
     achieved_tf = flops_per_frame * frames_per_launch / k1_avg_s / 1e12 if k1_avg_s > 0 else None
     hbm_gbs = W["bytes"] * frames_per_launch / k1_avg_s / 1e9 if k1_avg_s > 0 else None
-    traffic = None
-    pmc_file = _latest("r*_c2_pmc.json")
-    try:   # HBM bytes per launch of the same kernel/config from the committed PMC passes
-        pmc = json.loads(pmc_file.read_text())
-        if int(pmc["frames_per_launch"]) == int(frames_per_launch) and wname == "c2":
-            traffic = next(v["hbm_bytes_corrected"] for k, v in pmc["kernels"].items()
-                           if k.split("<")[0].split("(")[0].split()[-1] == k1_name)
-    except Exception:
-        traffic = None
-    valu = K1_VALU_PER_SAMPLE.get(k1_kind)
-    clock_ghz, clock_src = CLOCK_GHZ, "r01_c2_sq_counters.json"
-    sq_file = _latest("r*_c2_sq.json")
-    try:
-        sq = json.loads(sq_file.read_text())["kernels"]
-        clock_ghz = next(v["effective_clock_ghz"] for k, v in sq.items() if k1_name in k)
-        clock_src = sq_file.name
-    except Exception:
-        pass
+    traffic, pmc_src = pmc_traffic(wname, k1_name, frames_per_launch)
     samples_per_chain = frames_per_launch / S
-    floor_ms = (samples_per_chain * valu * CYC_PER_FP64_VALU / (clock_ghz * 1e6)) if valu else None
+    sq = sq_model(wname, k1_name)
+    if sq is not None:
+        valu_wave, cpv, clock_ghz, sq_ns, sq_src = sq
+        # the SQ pass's launches cover its own samples per chain: VALU per sample from its frames
+        pmc_f = _latest(f"r*_{wname}_pmc.json")
+        sq_frames = None
+        try:
+            sq_frames = float(json.loads(pmc_f.read_text())["frames_per_launch"]) if pmc_f else None
+        except (ValueError, KeyError, OSError):
+            pass
+        valu = valu_wave / (sq_frames / S) if sq_frames else K1_VALU_PER_SAMPLE.get(k1_kind)
+    else:
+        valu, cpv, clock_ghz, sq_src = K1_VALU_PER_SAMPLE.get(k1_kind), CYC_PER_FP64_VALU, 2.32, None
+    floor_ms = (samples_per_chain * valu * cpv / (clock_ghz * 1e6)) if valu else None
+    # the whole path's FP64 work over the step: every filter's Kahan IIR, per GPU
+    chain_fpf = chain_flops_per_frame(W["ch"])
+    chain_tf = chain_fpf * float(S) * T / (ms_per_step / 1e3) / 1e12
     roof = {
         "bound": "fp64", "achieved": achieved_tf, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
         "frac": (achieved_tf / FP64_PEAK_TFLOPS) if achieved_tf else None, "traffic": traffic,
@@ -493,16 +530,23 @@ def measure_gpu(wname, streams, frames, steps, warmup, e2e_steps, dev, local_dev
         "avg_launch_ms": k1_avg_s * 1e3, "output_kernel_avg_launch_ms": k2_avg_s * 1e3,
         "hbm": {"achieved": hbm_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": (hbm_gbs / HBM_PEAK_GBS) if hbm_gbs else None,
-                "alg_bytes_per_frame": W["bytes"], "traffic_source": pmc_file.name if (traffic and pmc_file) else None},
-        "issue_bound": {"valu_per_sample": valu, "cycles_per_valu": CYC_PER_FP64_VALU, "clock_ghz": clock_ghz,
-                        "clock_source": clock_src,
+                "alg_bytes_per_frame": W["bytes"], "traffic_source": f"profiles/{pmc_src}" if traffic else None},
+        "chain_fp64": {"flops_per_frame": chain_fpf, "achieved": chain_tf, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+                       "frac": chain_tf / FP64_PEAK_TFLOPS,
+                       "note": "SURVEY 8(d): the Kahan IIR of every filter (15N - 4 flops per filter-sample, "
+                               "hblpf.c:1017-1056), per GPU, over ms_per_step"},
+        "issue_bound": {"kind": "model", "valu_per_sample": valu, "cycles_per_valu": cpv, "clock_ghz": clock_ghz,
+                        "source": f"profiles/{sq_src}" if sq_src else "round-2 constants",
                         "floor_ms_per_launch": floor_ms,
-                        "frac": (floor_ms / (k1_avg_s * 1e3)) if (k1_avg_s and floor_ms) else None},
+                        "frac": (floor_ms / (k1_avg_s * 1e3)) if (k1_avg_s and floor_ms) else None,
+                        "note": "VALU per sample x cycles per VALU at the clock of the committed SQ pass of this "
+                                "kernel; frac = that time / this run's launch time (~1: the recurrence runs at "
+                                "the issue rate it was profiled at; boxes differ by a few %)"},
         "note": f"serial IIR recurrence: {chains_per_stream * S} DF-II chains per GPU, each a dependent "
                 f"chain of ~{4 * IIR_ORDER} FP64 ops per sample ({'one 16-lane DPP row' if k1_kind == 3 else 'one lane'}"
                 f" per chain); `frac` is the algorithmic FP64 rate (5N = {5 * IIR_ORDER} flops per chain-sample) "
                 f"against the FP64 vector peak, small because {chains_per_stream * S} chains cannot fill "
-                f"1024 SIMDs; issue_bound.frac ~1 = at the per-wave issue floor (DESIGN.md 5)",
+                f"1024 SIMDs (DESIGN.md 5)",
     }
 
     ctx.close()
@@ -543,43 +587,57 @@ def main():
     W, S, T, fs = r["W"], r["S"], r["T"], r["fs"]
     value, ms_per_step, roof, e2e = r["value"], r["ms_per_step"], r["roofline"], r["e2e"]
 
-    # ---- the other BASELINE configs, measured in the same run (N=1 only): short runs of the same
-    # harness, reported beside the headline, never in `value`
+    # ---- the other BASELINE configs, measured in the same run: short runs of the same harness,
+    # reported beside the headline, never in `value`.  N = 1: C3 / C4 / C5 and their FIR forms, and
+    # the C1 drop-in.  N > 1: the configs BASELINE.json quotes "sharded across 8xMI355X" -- C4 and
+    # C5 (and their 255 / 1023-tap FIR forms) at their per-GPU shard sizes (2 048 / 256 streams per
+    # rank: 16 384 / 2 048 at N = 8), timed like the headline (barriers, max over ranks), whole-job
     others = None
-    if (world == 1 and a.workload == "c2" and not a.no_other_workloads and not a.no_cpu_baseline
-            and a.streams is None and a.frames is None):
+    want_others = a.workload == "c2" and not a.no_other_workloads and (
+        world > 1 or (not a.no_cpu_baseline and a.streams is None and a.frames is None))
+    if want_others:
         others = {}
         import gc
-        import torch
-        for w in os.environ.get("ICW_BENCH_OTHERS", "c3,c4,c5,c2fir,c3fir,c4fir,c5fir").split(","):
+        default = "c4,c5,c4fir,c5fir" if world > 1 else "c3,c4,c5,c2fir,c3fir,c4fir,c5fir"
+        for w in os.environ.get("ICW_BENCH_OTHERS_MULTI" if world > 1 else "ICW_BENCH_OTHERS", default).split(","):
             gc.collect()
             torch.cuda.empty_cache()
-            o = measure_gpu(w, None, None, 2, 1, 0, dev, local_dev, None, 0, 1)
+            o = measure_gpu(w, None, a.other_frames, 2, 1, 0, dev, local_dev, dist, rank, world)
             ro = o["roofline"]
             others[w] = {"value": o["value"], "unit": "Msamples/s", "ms_per_step": o["ms_per_step"], "steps": 2,
-                         "warmup": 1, "workload": o["W"]["desc"], "streams_per_gpu": o["S"],
-                         "frames_per_stream_per_step": o["T"], "k1_kernel": ro["kernel"],
-                         "k1_avg_launch_ms": ro["avg_launch_ms"], "k2_avg_launch_ms": ro["output_kernel_avg_launch_ms"],
-                         "fp64_frac": ro["frac"]}
+                         "warmup": 1, "n_gpus": world, "workload": o["W"]["desc"], "streams_per_gpu": o["S"],
+                         "streams_total": o["S"] * world, "frames_per_stream_per_step": o["T"],
+                         "k1_kernel": ro["kernel"], "k1_avg_launch_ms": ro["avg_launch_ms"],
+                         "k2_avg_launch_ms": ro["output_kernel_avg_launch_ms"], "fp64_frac": ro["frac"]}
+            if "chain_fp64" in ro:
+                others[w]["chain_fp64_frac"] = ro["chain_fp64"]["frac"]
             if o["W"].get("fir"):
                 others[w].update({"fir_kernel_avg_launch_ms": ro["avg_launch_ms"], "fir_tflops": ro["achieved"],
-                                  "fir_hbm_gbs": ro["hbm"]["achieved"]})
+                                  "fir_hbm_gbs": ro["hbm"]["achieved"], "fir_hbm_source": ro["hbm"]["source"]})
                 for k in ("k1_kernel", "k1_avg_launch_ms"):
                     others[w].pop(k)
-        try:
-            c1 = measure_c1(1, 1, 576, True)
-            others["c1"] = {k: c1[k] for k in ("value", "unit", "ms_per_step", "block_latency_us", "realtime_x",
-                                               "parity_vs_oracle", "cpu_baseline")}
-            others["c1"]["workload"] = c1["config"]["workload"]
-        except (SystemExit, Exception) as e:      # reported, never silently replaced
-            others["c1"] = {"error": repr(e)}
+        if world == 1:
+            try:
+                c1 = measure_c1(1, 1, 576, True)
+                others["c1"] = {k: c1[k] for k in ("value", "unit", "ms_per_step", "block_latency_us", "realtime_x",
+                                                   "parity_vs_oracle", "cpu_baseline")}
+                others["c1"]["workload"] = c1["config"]["workload"]
+            except (SystemExit, Exception) as e:      # reported, never silently replaced
+                others["c1"] = {"error": repr(e)}
 
+    # ---- the CPU baseline: rank 0, after the last GPU barrier (never beside GPU timing); the other
+    # ranks wait for it at a final barrier
+    if dist:
+        torch.cuda.synchronize()
+        dist.barrier()
     cpu = None
-    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+    if rank == 0 and not a.no_cpu_baseline:
         try:
             cpu = cpu_baseline(a.cpu_workers, a.cpu_frames, a.workload)
         except Exception as e:  # reported, never silently replaced
             cpu = {"error": repr(e)}
+    if dist:
+        dist.barrier()
 
     if rank == 0:
         line = {

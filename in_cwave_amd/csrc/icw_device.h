@@ -279,4 +279,13 @@ __device__ __forceinline__ void icw_fes_flush(const IcwFes &f, uint32_t *dst)
 }
 #endif
 
+/* K5 icw_stream1: the four kernels of a one-stream, one-block call in one workgroup */
+#define ICW_S1_MAX 4096   /* frames: the output phase runs T / 256 tiles in turn */
+struct IcwS1Args {
+    IcwK0Args k0;
+    IcwK1Args k1;
+    IcwK2Args k2;
+    IcwAdvArgs adv;
+};
+
 #endif

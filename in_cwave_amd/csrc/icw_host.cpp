@@ -35,6 +35,7 @@ extern "C" hipError_t icw_launch_output(const IcwK2Args *a, int nord, int kahan,
 extern "C" hipError_t icw_launch_trig_table(const IcwTrigArgs *a, hipStream_t st);
 extern "C" hipError_t icw_launch_graph_serial(const IcwK4Args *a, hipStream_t st);
 extern "C" hipError_t icw_launch_advance(const IcwAdvArgs *a, hipStream_t st);
+extern "C" hipError_t icw_launch_stream1(const IcwS1Args *a, int nord, hipStream_t st);
 extern "C" hipError_t icw_launch_fir(const IcwFirArgs *a, hipStream_t st);
 extern "C" hipError_t icw_launch_fir_graph(const IcwFirArgs *f, const IcwK2Args *a, hipStream_t st);
 extern "C" size_t icw_fir_graph_lds(int M, int nt, int nch, int n_regs);
@@ -190,6 +191,7 @@ struct icw_ctx {
     double *fir_hist[2] = {};
     int fir_par = 0;
     bool fir_fuse = true;                 /* ICW_FIR_FUSED=0: KF + K2 as two kernels (A/B) */
+    bool stream1 = true;                  /* ICW_STREAM1=0: one-stream calls keep the four kernels (A/B) */
     std::mutex mu;
 };
 
@@ -910,6 +912,8 @@ int icw_create(const icw_config *cfg, const icw_node *nodes, int n_nodes, int n_
         if (fd && !strcmp(fd, "0")) c->fill_drain = false;
         const char *ff = getenv("ICW_FIR_FUSED");
         if (ff && !strcmp(ff, "0")) c->fir_fuse = false;
+        const char *s1e = getenv("ICW_STREAM1");
+        if (s1e && !strcmp(s1e, "0")) c->stream1 = false;
         const char *kl = getenv("ICW_K1_LDS");
         c->k1_lds = kl && !strcmp(kl, "1");
         {
@@ -1276,6 +1280,9 @@ int icw_process_streams(icw_ctx *c, int first, int count, const void *in, size_t
     const std::vector<std::pair<int, int>> blocks =
         plan_blocks(n_frames, Tb, fir_fused ? 0 : c->first_block, taper, c->taper_min);
     const int n_blocks = (int)blocks.size();
+    /* K5 (icw_stream1): one stream, one block, the row recurrence, register-form graph, ROUND / flat */
+    const bool s1 = c->stream1 && count == 1 && n_blocks == 1 && !cw && !fcm && k1_mode == 3 && !c->serial_render &&
+                    !bus && n_frames <= ICW_S1_MAX;
 
     const unsigned char *d_in;
     unsigned char *d_out;
@@ -1453,8 +1460,7 @@ int icw_process_streams(icw_ctx *c, int first, int count, const void *in, size_t
     };
     /* K0 of block b on sA: xd[p] was last read by K1 of block b-2 (and, complex input, by K2 of
      * block b-2, which precedes it on sA) */
-    auto launch_k0 = [&](int b) -> int {
-        if (fir_fused) return ICW_OK;                   /* KF2 converts inside the block's kernel */
+    auto k0_args = [&](int b) {
         const int t0 = blocks[b].first, T = blocks[b].second, p = b % n_sets;
         IcwK0Args a0;
         memset(&a0, 0, sizeof(a0));
@@ -1474,6 +1480,12 @@ int icw_process_streams(icw_ctx *c, int first, int count, const void *in, size_t
         a0.xd = c->xd[p];
         a0.x_pitch = x_pitch;
         a0.dedup = dedup ? 1 : 0;
+        return a0;
+    };
+    auto launch_k0 = [&](int b) -> int {
+        if (fir_fused) return ICW_OK;                   /* KF2 converts inside the block's kernel */
+        const int p = b % n_sets;
+        const IcwK0Args a0 = k0_args(b);
         if (b >= n_sets && !cw && sK != sA && hipStreamWaitEvent(sA, c->k1done[p], 0) != hipSuccess) return ICW_EDEVICE;
         hipStream_t s0 = (b == 0 && sF) ? sF : sA;         /* the fill: nothing else runs yet */
         /* the FIR converter runs on the caller's stream (K1's, idle without the IIR), so KF of the
@@ -1495,67 +1507,34 @@ int icw_process_streams(icw_ctx *c, int first, int count, const void *in, size_t
         return ICW_OK;
     };
 
-    /* n_sets scratch sets (2 by default, ICW_SETS=3): K0 of the first n_sets blocks is queued up
-     * front, K0(b + n_sets) as soon as its xd set is free (below); K1(b + n_sets) reuses the w /
-     * info_dup set that K2(b) read and waits for it.  Three sets measured slower for large
-     * batches (C3: K1 3.96 vs 3.16 ms per launch, DESIGN §6), so two is the default. */
-    int rc0 = ICW_OK;
-    for (int b = 0; b < n_sets; ++b)
-        if ((rc0 = launch_k0(b)) != ICW_OK) return rc0;
-    for (int b = 0; b < n_blocks; ++b) {
-        const int t0 = blocks[b].first;
-        const int T = blocks[b].second;
+    auto k1_args = [&](int b) {
         const int p = b % n_sets;
-
-        if (!cw) {
-            IcwK1Args a1;
-            memset(&a1, 0, sizeof(a1));
-            a1.xd = c->xd[p];
-            a1.x_pitch = x_pitch;
-            a1.nch = nch;
-            a1.n_streams = count;
-            a1.n_chains = count * 4;
-            a1.T = T;
-            a1.hist = ds.hist + f0 * 4 * ICW_HIST_PITCH;
-            a1.sncnt = ds.sncnt + f0 * 4;
-            a1.err = ds.err;
-            a1.w = c->w[p];
-            a1.w_pitch = w_pitch;
-            a1.lr_equal = ds.lr_equal + f0 * 2;
-            a1.hq_phase = ds.hq_phase + f0 * 2;
-            a1.t0 = t0;
-            a1.info_dup = c->info_dup[p];
-            memcpy(a1.pc, c->pc, sizeof(a1.pc));
-            a1.wg_waves = c->k1_lds ? 4 : c->k1_wg;
-            a1.lds_hold = c->k1_lds ? c->lds_cu : 0;
-            a1.dedup = dedup ? 1 : 0;
-            a1.fes = fcm ? ds.fes + f0 * 4 * ICW_FES_PITCH : nullptr;
-            /* K0(b) done, and K2(b-2), the last reader of w[p] / info_dup[p] */
-            if (sK != sA && hipStreamWaitEvent(sK, c->k0done[p], 0) != hipSuccess) return ICW_EDEVICE;
-            if (b >= n_sets && sK != sA && hipStreamWaitEvent(sK, c->k2done[p], 0) != hipSuccess) return ICW_EDEVICE;
-            if (timing && hipEventRecord(c->ev[4 * b], sK) != hipSuccess) return ICW_EDEVICE;
-            const hipError_t e1 = k1_mode == ICW_K1_FC ? icw_launch_iir_fc(&a1, N, cfg.iir_kahan, cfg.iir_subnorm_reject, sK)
-                                : k1_mode == 3 ? icw_launch_iir_row(&a1, N, cfg.iir_kahan, cfg.iir_subnorm_reject, sK)
-                                               : icw_launch_iir_state(&a1, N, cfg.iir_kahan, cfg.iir_subnorm_reject, sK);
-            if (e1 != hipSuccess) return ICW_EDEVICE;
-            if (timing && hipEventRecord(c->ev[4 * b + 1], sK) != hipSuccess) return ICW_EDEVICE;
-            if (hipEventRecord(c->k1done[p], sK) != hipSuccess) return ICW_EDEVICE;
-            if (sK != sA && hipStreamWaitEvent(sA, c->k1done[p], 0) != hipSuccess) return ICW_EDEVICE;
-            /* real input: K0(b + n_sets) reuses xd[p], which K1(b) read; queued before K2(b) it
-             * runs beside K1(b+1) instead of between two recurrences */
-            if (b + n_sets < n_blocks && (rc0 = launch_k0(b + n_sets)) != ICW_OK) return rc0;
-        } else if (timing && !fir) {
-            if (hipEventRecord(c->ev[4 * b], sA) != hipSuccess || hipEventRecord(c->ev[4 * b + 1], sA) != hipSuccess)
-                return ICW_EDEVICE;
-        }
-
-        /* the drain: K2 of the last block on the unmasked stream, after K1 of the block and K2 of
-         * the one before it (the rotation table and the block order of the meters' owners) */
-        const bool drain = sF && b == n_blocks - 1;
-        hipStream_t s2 = drain ? sF : sA;
-        if (drain && (hipStreamWaitEvent(sF, c->k1done[p], 0) != hipSuccess ||
-                      (b >= 1 && hipStreamWaitEvent(sF, c->k2done[(b - 1) % n_sets], 0) != hipSuccess)))
-            return ICW_EDEVICE;
+        IcwK1Args a1;
+        memset(&a1, 0, sizeof(a1));
+        a1.xd = c->xd[p];
+        a1.x_pitch = x_pitch;
+        a1.nch = nch;
+        a1.n_streams = count;
+        a1.n_chains = count * 4;
+        a1.T = blocks[b].second;
+        a1.hist = ds.hist + f0 * 4 * ICW_HIST_PITCH;
+        a1.sncnt = ds.sncnt + f0 * 4;
+        a1.err = ds.err;
+        a1.w = c->w[p];
+        a1.w_pitch = w_pitch;
+        a1.lr_equal = ds.lr_equal + f0 * 2;
+        a1.hq_phase = ds.hq_phase + f0 * 2;
+        a1.t0 = blocks[b].first;
+        a1.info_dup = c->info_dup[p];
+        memcpy(a1.pc, c->pc, sizeof(a1.pc));
+        a1.wg_waves = c->k1_lds ? 4 : c->k1_wg;
+        a1.lds_hold = c->k1_lds ? c->lds_cu : 0;
+        a1.dedup = dedup ? 1 : 0;
+        a1.fes = fcm ? ds.fes + f0 * 4 * ICW_FES_PITCH : nullptr;
+        return a1;
+    };
+    auto k2_args = [&](int b) {
+        const int t0 = blocks[b].first, T = blocks[b].second, p = b % n_sets;
         IcwK2Args a2;
         memset(&a2, 0, sizeof(a2));
         a2.w = c->w[p];
@@ -1597,6 +1576,83 @@ int icw_process_streams(icw_ctx *c, int first, int count, const void *in, size_t
         a2.trig = c->prog.needs_omega;
         a2.sncnt = (!cw && cfg.iir_subnorm_reject) ? ds.sncnt + f0 * 4 : nullptr;
         a2.fes = fcm ? ds.fes + f0 * 4 * ICW_FES_PITCH : nullptr;
+        return a2;
+    };
+    auto adv_args = [&]() {
+        IcwAdvArgs av;
+        memset(&av, 0, sizeof(av));
+        av.lds_guard = c->k1_lds ? 256u : 0u;
+        av.n_streams = count;
+        av.cw = cw ? 1 : 0;
+        av.n = n_frames;
+        av.hq_phase = ds.hq_phase + f0 * 2;
+        av.pos = ds.pos + f0;
+        av.n_frame = ds.n_frame + f0;
+        av.ssr = ssr;
+        av.scaled = cfg.frmod_scaled;
+        if (pinned) {
+            av.err = ds.err;
+            av.err_copy = (int *)(d_out + dos * S);        /* the output buffer has 16 spare bytes */
+        }
+        return av;
+    };
+    /* K5: a one-stream call of one block (the drop-in's 576-frame calls, playback.c:619) runs its four
+     * kernels as phases of one workgroup (icw_stream1): no launch gaps, one launch per call */
+    if (s1) {
+        IcwS1Args a5;
+        memset(&a5, 0, sizeof(a5));
+        a5.k0 = k0_args(0);
+        a5.k1 = k1_args(0);
+        a5.k2 = k2_args(0);
+        a5.adv = adv_args();
+        if (timing && hipEventRecord(c->ev[0], st) != hipSuccess) return ICW_EDEVICE;
+        if (icw_launch_stream1(&a5, N, st) != hipSuccess) return ICW_EDEVICE;
+        if (timing && (hipEventRecord(c->ev[1], st) != hipSuccess || hipEventRecord(c->ev[2], st) != hipSuccess ||
+                       hipEventRecord(c->ev[3], st) != hipSuccess))
+            return ICW_EDEVICE;
+        if (!cw && nch > 1) c->lr_known[first] = 0;
+    } else {
+    /* n_sets scratch sets (2 by default, ICW_SETS=3): K0 of the first n_sets blocks is queued up
+     * front, K0(b + n_sets) as soon as its xd set is free (below); K1(b + n_sets) reuses the w /
+     * info_dup set that K2(b) read and waits for it.  Three sets measured slower for large
+     * batches (C3: K1 3.96 vs 3.16 ms per launch, DESIGN §6), so two is the default. */
+    int rc0 = ICW_OK;
+    for (int b = 0; b < n_sets; ++b)
+        if ((rc0 = launch_k0(b)) != ICW_OK) return rc0;
+    for (int b = 0; b < n_blocks; ++b) {
+        const int t0 = blocks[b].first;
+        const int T = blocks[b].second;
+        const int p = b % n_sets;
+
+        if (!cw) {
+            const IcwK1Args a1 = k1_args(b);
+            /* K0(b) done, and K2(b-2), the last reader of w[p] / info_dup[p] */
+            if (sK != sA && hipStreamWaitEvent(sK, c->k0done[p], 0) != hipSuccess) return ICW_EDEVICE;
+            if (b >= n_sets && sK != sA && hipStreamWaitEvent(sK, c->k2done[p], 0) != hipSuccess) return ICW_EDEVICE;
+            if (timing && hipEventRecord(c->ev[4 * b], sK) != hipSuccess) return ICW_EDEVICE;
+            const hipError_t e1 = k1_mode == ICW_K1_FC ? icw_launch_iir_fc(&a1, N, cfg.iir_kahan, cfg.iir_subnorm_reject, sK)
+                                : k1_mode == 3 ? icw_launch_iir_row(&a1, N, cfg.iir_kahan, cfg.iir_subnorm_reject, sK)
+                                               : icw_launch_iir_state(&a1, N, cfg.iir_kahan, cfg.iir_subnorm_reject, sK);
+            if (e1 != hipSuccess) return ICW_EDEVICE;
+            if (timing && hipEventRecord(c->ev[4 * b + 1], sK) != hipSuccess) return ICW_EDEVICE;
+            if (hipEventRecord(c->k1done[p], sK) != hipSuccess) return ICW_EDEVICE;
+            if (sK != sA && hipStreamWaitEvent(sA, c->k1done[p], 0) != hipSuccess) return ICW_EDEVICE;
+            /* real input: K0(b + n_sets) reuses xd[p], which K1(b) read; queued before K2(b) it
+             * runs beside K1(b+1) instead of between two recurrences */
+            if (b + n_sets < n_blocks && (rc0 = launch_k0(b + n_sets)) != ICW_OK) return rc0;
+        } else if (timing && !fir) {
+            if (hipEventRecord(c->ev[4 * b], sA) != hipSuccess || hipEventRecord(c->ev[4 * b + 1], sA) != hipSuccess)
+                return ICW_EDEVICE;
+        }
+
+        /* the drain: K2 of the last block on the unmasked stream, after K1 of the block and K2 of
+         * the one before it (the rotation table and the block order of the meters' owners) */
+        const bool drain = sF && b == n_blocks - 1;
+        hipStream_t s2 = drain ? sF : sA;
+        if (drain && (hipStreamWaitEvent(sF, c->k1done[p], 0) != hipSuccess ||
+                      (b >= 1 && hipStreamWaitEvent(sF, c->k2done[(b - 1) % n_sets], 0) != hipSuccess)))
+            return ICW_EDEVICE;
+        IcwK2Args a2 = k2_args(b);
         if (table) {
             IcwTrigArgs at;
             memset(&at, 0, sizeof(at));
@@ -1712,24 +1768,9 @@ int icw_process_streams(icw_ctx *c, int first, int count, const void *in, size_t
                            S * hrow * sizeof(double), hipMemcpyDeviceToDevice, st) != hipSuccess)
             return ICW_EDEVICE;
     }
-    {
-        IcwAdvArgs av;
-        memset(&av, 0, sizeof(av));
-        av.lds_guard = c->k1_lds ? 256u : 0u;
-        av.n_streams = count;
-        av.cw = cw ? 1 : 0;
-        av.n = n_frames;
-        av.hq_phase = ds.hq_phase + f0 * 2;
-        av.pos = ds.pos + f0;
-        av.n_frame = ds.n_frame + f0;
-        av.ssr = ssr;
-        av.scaled = cfg.frmod_scaled;
-        if (pinned) {
-            av.err = ds.err;
-            av.err_copy = (int *)(d_out + dos * S);        /* the output buffer has 16 spare bytes */
-        }
+        const IcwAdvArgs av = adv_args();
         if (icw_launch_advance(&av, st) != hipSuccess) return ICW_EDEVICE;
-    }
+    }   /* !s1 */
     if (legacy && hipStreamSynchronize(st) != hipSuccess) return ICW_EDEVICE;
     if (!dev) {
         unsigned char *h_out = pinned ? c->h_stage + stage_in : nullptr;

@@ -20,6 +20,7 @@
 
 #include "../../include/icw.h"
 #include "icw_device.h"
+#include "icw_iir_dev.h"
 #include "icw_libm.h"
 
 #pragma clang fp contract(off)
@@ -107,11 +108,8 @@ __device__ __forceinline__ double icw_filter_in(double x, unsigned kq)
  * (lpf_hilbert_quad.c:129-156) feeds the I filter {x, +0, -x, +0} and the Q filter {+0, -x, +0, x}
  * by sample phase.  Mono input feeds the right converter with the left value, exactly the
  * reference's reuse of `val` (xwave_reader.c:988).  Row g = s*4 + ch*2 + {0:I, 1:Q}. */
-__global__ __launch_bounds__(256) void icw_unpack_frames(IcwK0Args a)
+__device__ __forceinline__ void icw_unpack_frame(const IcwK0Args &a, int t, int s)
 {
-    const int t = blockIdx.x * 256 + threadIdx.x;
-    const int s = blockIdx.y;
-    if (t >= a.T) return;
     const unsigned char *fp = a.in + (size_t)s * a.in_stride + (size_t)t * a.fsz;
     const long long ix = a.pos[s] + a.t0 + t;
     const double fd = icw_fade(ix, a.fade[s * 3 + 0], a.fade[s * 3 + 1], a.fade[s * 3 + 2]);
@@ -150,6 +148,12 @@ __global__ __launch_bounds__(256) void icw_unpack_frames(IcwK0Args a)
             xs[(size_t)(ch * 2 + 1) * a.x_pitch] = icw_filter_in(v[ch], (k + 1u) & 3u);
         }
     }
+}
+
+__global__ __launch_bounds__(256) void icw_unpack_frames(IcwK0Args a)
+{
+    const int t = blockIdx.x * 256 + threadIdx.x;
+    if (t < a.T) icw_unpack_frame(a, t, blockIdx.y);
 }
 
 /* FIR Hilbert converter: real PCM -> the analytic signal a CWAVE file holds (cwave.h:40,56-58:
@@ -706,18 +710,17 @@ __device__ __forceinline__ void icw_meters_wg(const IcwK2Args &a, int s, unsigne
 #define ICW_K2_MINWG 1
 #endif
 template <int N, bool KAHAN, bool TRIG, bool FCK = false>
-__global__ __launch_bounds__(ICW_K2_TILE, ICW_K2_MINWG) void icw_output(IcwK2Args a)
+__device__ __forceinline__ void icw_output_body(const IcwK2Args &a, int bx, int s, double *lregs)
 {
     constexpr int TILE = ICW_K2_TILE;
     constexpr int NR = N + 1;                        /* window rows past the tile (row N+t: w[t]) */
     __shared__ double lw[2][4][TILE + 24];
-    extern __shared__ __attribute__((aligned(16))) double lregs[];   /* [n_regs][4][TILE] */
+    /* lregs: the DSP register file [n_regs][4][TILE] in dynamic LDS */
     __shared__ unsigned red_clip[2][TILE / 64];
     __shared__ double red_pk[2][TILE / 64];
-    const int s = blockIdx.y;
     const int tl = threadIdx.x;
     const int T = a.T;
-    const int tw0 = blockIdx.x * TILE * a.tpw;
+    const int tw0 = bx * TILE * a.tpw;
     const int ntile = min(a.tpw, (T - tw0 + TILE - 1) / TILE);
 
     /* mono input, converters bit-identical at block start (K1's flag) and in phase: the right
@@ -859,6 +862,13 @@ __global__ __launch_bounds__(ICW_K2_TILE, ICW_K2_MINWG) void icw_output(IcwK2Arg
         }
     }
     if (a.do_render) icw_meters_wg(a, s, clip_l, clip_r, pk_l, pk_r, red_clip, red_pk);
+}
+
+template <int N, bool KAHAN, bool TRIG, bool FCK = false>
+__global__ __launch_bounds__(ICW_K2_TILE, ICW_K2_MINWG) void icw_output(IcwK2Args a)
+{
+    extern __shared__ __attribute__((aligned(16))) double lregs[];   /* [n_regs][4][TILE] */
+    icw_output_body<N, KAHAN, TRIG, FCK>(a, blockIdx.x, blockIdx.y, lregs);
 }
 
 /* Fused FIR converter + graph + render (KF2): one workgroup per stream and 1024-frame tile (2048
@@ -1016,10 +1026,8 @@ __global__ __launch_bounds__(64) void icw_graph_serial(IcwK4Args a)
 
 /* Call-end bookkeeping: the reader position, the Hilbert phases (not for complex input -- the
  * converters were not called) and the modulator frame counter advance by the call's frames. */
-__global__ __launch_bounds__(64) void icw_advance(IcwAdvArgs a)
+__device__ __forceinline__ void icw_advance_stream(const IcwAdvArgs &a, int s)
 {
-    const int s = blockIdx.x * 64 + threadIdx.x;
-    if (s >= a.n_streams) return;
     a.pos[s] += a.n;
     if (!a.cw) {
         a.hq_phase[s * 2 + 0] = (a.hq_phase[s * 2 + 0] + (unsigned)a.n) & 3u;
@@ -1028,6 +1036,36 @@ __global__ __launch_bounds__(64) void icw_advance(IcwAdvArgs a)
     const unsigned long long n0 = a.n_frame[s];
     a.n_frame[s] = a.scaled ? (n0 + (unsigned long long)a.n) % a.ssr : n0 + (unsigned long long)a.n;
     if (s == 0 && a.err_copy) *a.err_copy = *a.err;
+}
+
+__global__ __launch_bounds__(64) void icw_advance(IcwAdvArgs a)
+{
+    const int s = blockIdx.x * 64 + threadIdx.x;
+    if (s < a.n_streams) icw_advance_stream(a, s);
+}
+
+/* K5 icw_stream1: one stream's whole launch block in ONE workgroup -- the per-call form of the
+ * drop-in boundary (icw_amod_process_samples: playback.c:619 renders 576-frame blocks, NS_PERTIME,
+ * in_cwave.h:133).  The pipeline's four launches (K0, K1r, K2, icw_advance) and their ~6 us gaps
+ * become phases of one kernel, separated by workgroup barriers; each phase runs the same device
+ * code as its kernel, so the results are the pipeline's bit for bit:
+ *   1. all 256 threads: unpack + fade + quadrature mix of the block (K0) into the xd rows;
+ *   2. waves 0-1: the row-broadcast recurrence (K1r: filter f = wave, one 16-lane row per channel);
+ *   3. all threads: output sums, un-mix, DSP list, ROUND render, meters (K2, a.tpw tiles of 256);
+ *   4. thread 0: reader position, Hilbert phases, frame counter (icw_advance).
+ * The stores of one phase reach the next one's loads through the barrier's workgroup-scope
+ * release / acquire (one CU, one vector L1). */
+template <int N, bool TRIG>
+__global__ __launch_bounds__(ICW_K2_TILE) void icw_stream1(IcwS1Args a)
+{
+    extern __shared__ __attribute__((aligned(16))) double lregs[];   /* K2's register file */
+    for (int t = threadIdx.x; t < a.k0.T; t += ICW_K2_TILE) icw_unpack_frame(a.k0, t, 0);
+    __syncthreads();
+    if (threadIdx.x < 128) icw_iir_row_body<N>(a.k1, threadIdx.x);
+    __syncthreads();
+    icw_output_body<N, true, TRIG>(a.k2, 0, 0, lregs);
+    __syncthreads();
+    if (threadIdx.x == 0) icw_advance_stream(a.adv, 0);
 }
 
 /* ------------------------------------------------------ serial render kernel (K3) ------ */
@@ -2051,6 +2089,32 @@ extern "C" hipError_t icw_launch_graph_serial(const IcwK4Args *a, hipStream_t st
 {
     hipLaunchKernelGGL(icw_graph_serial, dim3((a->n_streams + 63) / 64), dim3(64), a->lds_guard, st, *a);
     return hipGetLastError();
+}
+
+template <int N>
+static hipError_t launch_s1_t(IcwS1Args a, hipStream_t st)
+{
+    a.k2.tpw = (a.k2.T + ICW_K2_TILE - 1) / ICW_K2_TILE;
+    const size_t lds = (size_t)a.k2.n_regs * 4 * ICW_K2_TILE * sizeof(double);
+    if (a.k2.trig) hipLaunchKernelGGL((icw_stream1<N, true>), dim3(1), dim3(ICW_K2_TILE), lds, st, a);
+    else hipLaunchKernelGGL((icw_stream1<N, false>), dim3(1), dim3(ICW_K2_TILE), lds, st, a);
+    return hipGetLastError();
+}
+
+/* K5: one stream, one launch block of at most ICW_S1_MAX frames, real input, Kahan + reject (the
+ * row recurrence), register-form graph, ROUND / flat render, no FP_CHECK -- the host checks */
+extern "C" hipError_t icw_launch_stream1(const IcwS1Args *a, int nord, hipStream_t st)
+{
+    if (a->k0.T != a->k2.T || a->k1.T != a->k2.T || a->k2.T <= 0 || a->k2.T > ICW_S1_MAX || a->k2.n_streams != 1 ||
+        a->k2.cw || a->k2.fes || a->k2.iq_out || !a->k2.do_render)
+        return hipErrorInvalidValue;
+    switch (nord) {
+    case 15: return launch_s1_t<15>(*a, st);
+    case 18: return launch_s1_t<18>(*a, st);
+    case 19: return launch_s1_t<19>(*a, st);
+    case 20: return launch_s1_t<20>(*a, st);
+    }
+    return hipErrorInvalidValue;
 }
 
 extern "C" hipError_t icw_launch_advance(const IcwAdvArgs *a, hipStream_t st)
