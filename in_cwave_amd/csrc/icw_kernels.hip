@@ -880,8 +880,12 @@ __global__ __launch_bounds__(ICW_K2_TILE, ICW_K2_MINWG) void icw_output(IcwK2Arg
  * analytic signal never leaves the registers (KF + K2 move 32 B per frame through HBM twice); the
  * sums are KF's, in the same order, so the results are KF + K2's bit for bit.  Dynamic LDS: the
  * padded inputs of each computed channel, the taps, the DSP register file. */
+/* Occupancy: 4 workgroups (4 waves per SIMD, <= 128 VGPRs) without a Shift / PM node; 3 with one
+ * (<= 168 VGPRs): at 128 the per-stream fallback call (icw_trig_call) left values live across it that
+ * the allocator spilled to scratch -- 44 B per thread written to HBM, which was most of the kernel's
+ * 2.95x write traffic (profiles/r02_c2fir_pmc.json: 198 MB per launch against 67 MB of output) */
 template <bool TRIG>
-__global__ __launch_bounds__(256, 4) void icw_fir_graph(IcwFirArgs f, IcwK2Args a)
+__global__ __launch_bounds__(256, TRIG ? 3 : 4) void icw_fir_graph(IcwFirArgs f, IcwK2Args a)
 {
     extern __shared__ double lds[];
     __shared__ unsigned red_clip[2][ICW_K2_TILE / 64];
