@@ -70,14 +70,16 @@ __device__ __forceinline__ void icw_iir_step(double (&R)[N], double xin, const d
 
 
 
+/* generic steps (every input read, the zero ones supplied by icw_chain_x; qodd: the block starts
+ * on an odd (phi + t), see icw_chain_x) */
 template <int N, int J0, bool KAHAN, bool SUBN>
 __device__ __forceinline__ void icw_block_steps(double (&R)[N], const double (&xv)[N],
-                                                const double (&pc)[20], unsigned &cnt, int lim)
+                                                const double (&pc)[20], unsigned &cnt, int lim, bool qodd)
 {
     if constexpr (J0 < N) {
         if (J0 < lim) {
-            icw_iir_step<N, KAHAN, SUBN, J0>(R, xv[J0], pc, cnt);
-            icw_block_steps<N, J0 + 1, KAHAN, SUBN>(R, xv, pc, cnt, lim);
+            icw_iir_step<N, KAHAN, SUBN, J0>(R, icw_chain_x<J0>(xv[J0], qodd), pc, cnt);
+            icw_block_steps<N, J0 + 1, KAHAN, SUBN>(R, xv, pc, cnt, lim, qodd);
         }
     }
 }
@@ -85,12 +87,13 @@ __device__ __forceinline__ void icw_block_steps(double (&R)[N], const double (&x
 
 template <int N, int J0, bool KAHAN, bool SUBN, bool SPEC = false>
 __device__ __forceinline__ void icw_block_steps_pf(double (&R)[N], double (&xv)[N], const double *xnext,
-                                                   const double (&pc)[20], unsigned &cnt, double *mn = nullptr)
+                                                   const double (&pc)[20], unsigned &cnt, bool qodd,
+                                                   double *mn = nullptr)
 {
     if constexpr (J0 < N) {
-        icw_iir_step<N, KAHAN, SUBN, J0, SPEC>(R, xv[J0], pc, cnt, mn);
+        icw_iir_step<N, KAHAN, SUBN, J0, SPEC>(R, icw_chain_x<J0>(xv[J0], qodd), pc, cnt, mn);
         xv[J0] = xnext[J0];
-        icw_block_steps_pf<N, J0 + 1, KAHAN, SUBN, SPEC>(R, xv, xnext, pc, cnt, mn);
+        icw_block_steps_pf<N, J0 + 1, KAHAN, SUBN, SPEC>(R, xv, xnext, pc, cnt, qodd, mn);
     }
 }
 
@@ -184,8 +187,11 @@ __global__ __launch_bounds__(256) void icw_iir_state(IcwK1Args a)
 
     /* this block's start (for K2); each (stream, filter) flag is read and written by one wave */
     if (ch == 0) a.info_dup[s * 2 + f] = a.lr_equal[s * 2 + f];
-    const double *xp = a.xd + (size_t)g * a.x_pitch;
+    const double *xp = a.xd + (size_t)(s * 2 + ch) * a.x_pitch;     /* the channel's signed row (K0) */
     double *wrow = a.w + (size_t)g * a.w_pitch;
+    /* block-relative sample n has a zero input iff (phi + n) is odd (I: k = hq + t0 + n odd;
+     * Q: k + 1 odd) */
+    const unsigned phi = (a.hq_phase[s * 2 + ch] + (unsigned)a.t0 + (unsigned)f) & 1u;
     /* history rows [0, N): row j = z_{N-1-j} = R[j] */
 #pragma unroll
     for (int j = 0; j < N; ++j) wrow[j] = R[j];
@@ -202,9 +208,7 @@ __global__ __launch_bounds__(256) void icw_iir_state(IcwK1Args a)
         bool zfast = false;
         unsigned phi0 = 0;
         if constexpr (KAHAN && SUBN && (N & 1)) {
-            /* block-relative sample n has a zero input iff (phi + n) is odd (I: k = hq + t0 + n odd;
-             * Q: k + 1 odd); the fast path needs one parity across the wave */
-            const unsigned phi = (a.hq_phase[s * 2 + ch] + (unsigned)a.t0 + (unsigned)f) & 1u;
+            /* the fast path needs one zero-input parity across the wave */
             phi0 = __builtin_amdgcn_readfirstlane(phi);
             zfast = __all(phi == phi0) && T >= 3 * N;
         }
@@ -213,7 +217,7 @@ __global__ __launch_bounds__(256) void icw_iir_state(IcwK1Args a)
                 /* speculative pairs of blocks ("Speculative blocks") that start on a nonzero sample; a
                  * failed block ends them and the exact loops below take over at its start */
                 if ((phi0 + (unsigned)t) & 1u) {
-                    icw_block_steps_pf<N, 0, KAHAN, SUBN>(R, xv, xp + t + N, pc, cnt);
+                    icw_block_steps_pf<N, 0, KAHAN, SUBN>(R, xv, xp + t + N, pc, cnt, true);
                     icw_store_block<N>(R, wrow + N + t);
                     t += N;
                 }
@@ -240,7 +244,7 @@ __global__ __launch_bounds__(256) void icw_iir_state(IcwK1Args a)
                     /* exact from here: the same zero-input pairs with the reject */
                     ICW_DRAIN_VMEM();
                     if (((phi0 + (unsigned)t) & 1u) && t + N <= T) {
-                        icw_block_steps_pf<N, 0, KAHAN, SUBN>(R, xv, xp + t + N, pc, cnt);
+                        icw_block_steps_pf<N, 0, KAHAN, SUBN>(R, xv, xp + t + N, pc, cnt, true);
                         icw_store_block<N>(R, wrow + N + t);
                         t += N;
                     }
@@ -255,7 +259,7 @@ __global__ __launch_bounds__(256) void icw_iir_state(IcwK1Args a)
             }
         }
         for (; t + N <= T; t += N) {
-            icw_block_steps_pf<N, 0, KAHAN, SUBN>(R, xv, xp + t + N, pc, cnt);
+            icw_block_steps_pf<N, 0, KAHAN, SUBN>(R, xv, xp + t + N, pc, cnt, ((phi + (unsigned)t) & 1u) != 0u);
             icw_store_block<N>(R, wrow + N + t);
         }
     }
@@ -264,7 +268,7 @@ __global__ __launch_bounds__(256) void icw_iir_state(IcwK1Args a)
         double xv[N];
 #pragma unroll
         for (int j = 0; j < N; ++j) xv[j] = (j < rem) ? xp[t + j] : 0.0;
-        icw_block_steps<N, 0, KAHAN, SUBN>(R, xv, pc, cnt, rem);
+        icw_block_steps<N, 0, KAHAN, SUBN>(R, xv, pc, cnt, rem, ((phi + (unsigned)t) & 1u) != 0u);
         double *wo = wrow + N + t;
 #pragma unroll
         for (int j = 0; j < N; ++j)
@@ -332,14 +336,18 @@ __global__ __launch_bounds__(64) void icw_iir_state_fc(IcwK1Args a, int N)
     for (int i = 0; i < 20; ++i) pc[i] = a.pc[i];
 #pragma unroll 1
     for (int i = 0; i < N; ++i) R[N - 1 - i] = a.hist[(size_t)g * ICW_HIST_PITCH + i];
-    const double *xp = a.xd + (size_t)g * a.x_pitch;
+    const double *xp = a.xd + (size_t)(s * 2 + ch) * a.x_pitch;     /* the channel's signed row (K0) */
+    const unsigned phi = (a.hq_phase[s * 2 + ch] + (unsigned)a.t0 + (unsigned)f) & 1u;
     double *wrow = a.w + (size_t)g * a.w_pitch;
 #pragma unroll 1
     for (int j = 0; j < N; ++j) wrow[j] = R[j];
     IcwFes fe = {};
     const int T = a.T;
 #pragma unroll 1
-    for (int t = 0; t < T; ++t) wrow[N + t] = icw_iir_step_fc<KAHAN, SUBN>(R, N, t, xp[t], pc, fe);
+    for (int t = 0; t < T; ++t) {
+        const double x = ((phi + (unsigned)t) & 1u) ? 0.0 : xp[t];     /* hq_rp_process's literal +0.0 */
+        wrow[N + t] = icw_iir_step_fc<KAHAN, SUBN>(R, N, t, x, pc, fe);
+    }
     /* after T steps logical z_i = R[(T - 1 - i) mod N] */
 #pragma unroll 1
     for (int i = 0; i < N; ++i) a.hist[(size_t)g * ICW_HIST_PITCH + i] = R[((T - 1 - i) % N + N) % N];

@@ -10,6 +10,18 @@
 
 #pragma clang fp contract(off)
 
+/* Filter input of a chain at step J of a block (K0 writes one signed row per channel, holding the I
+ * filter's nonzero inputs at the even Hilbert phases and the Q filter's at the odd ones): the row's
+ * value, or the literal +0.0 that hq_rp_process feeds the filter at the other phases
+ * (lpf_hilbert_quad.c:133-151).  Block-relative sample n is a zero input iff (phi + n) is odd; qodd
+ * says (phi + t) is odd for the block at t, so step J is a zero input iff (J odd) != qodd.  Only the
+ * generic loops call this: the zero-input loops never read a zero step's input. */
+template <int J>
+__device__ __forceinline__ double icw_chain_x(double v, bool qodd)
+{
+    return (((J & 1) != 0) != qodd) ? 0.0 : v;
+}
+
 /* ------------------------------------------------------------ IIR state kernel (K1) ----- */
 /* mn = min(mn, |s|) in one instruction: v_min_f64 with the abs modifier (the fmin builtin adds a
  * NaN-quieting v_max_f64 per operand in IEEE mode).  A NaN s leaves mn unchanged, as it leaves the

@@ -97,17 +97,15 @@ __device__ __forceinline__ double icw_fade(long long ix, long long ns, long long
 }
 
 /* input of the I (f=0) / Q (f=1) filter for Hilbert phase k (lpf_hilbert_quad.c:133-151):
- *   I: {x, +0, -x, +0}   Q: {+0, -x, +0, x}   ==  k' = (k+f)&3: {x, +0, -x, +0}[k'] */
-__device__ __forceinline__ double icw_filter_in(double x, unsigned kq)
-{
-    return kq == 0 ? x : (kq == 2 ? -x : 0.0);
-}
+ *   I: {x, +0, -x, +0}   Q: {+0, -x, +0, x}.  K0 writes the nonzero values of both into one row per
+ * channel; the recurrences supply the +0.0 (icw_iir_dev.h: icw_chain_x). */
 
 /* Input prep (K0): unpack + fade each frame once (xwave_unpack_csample, xwave_reader.c:908-1001)
- * and lay out every DF-II chain's own input sequence: the quadrature mix of hq_rp_process
- * (lpf_hilbert_quad.c:129-156) feeds the I filter {x, +0, -x, +0} and the Q filter {+0, -x, +0, x}
- * by sample phase.  Mono input feeds the right converter with the left value, exactly the
- * reference's reuse of `val` (xwave_reader.c:988).  Row g = s*4 + ch*2 + {0:I, 1:Q}. */
+ * and lay out the filter inputs of the quadrature mix of hq_rp_process (lpf_hilbert_quad.c:129-156):
+ * the I filter {x, +0, -x, +0} and the Q filter {+0, -x, +0, x} by sample phase, both in one row
+ * s*2 + ch of signed samples (below).  Mono input feeds the right converter with the left value,
+ * exactly the reference's reuse of `val` (xwave_reader.c:988).  Complex input: four rows
+ * s*4 + ch*2 + {I, Q}. */
 __device__ __forceinline__ void icw_unpack_frame(const IcwK0Args &a, int t, int s)
 {
     const unsigned char *fp = a.in + (size_t)s * a.in_stride + (size_t)t * a.fsz;
@@ -138,14 +136,17 @@ __device__ __forceinline__ void icw_unpack_frame(const IcwK0Args &a, int t, int 
     } else {
         v[1] = v[0];
     }
-    double *xs = a.xd + (size_t)s * 4 * a.x_pitch + t;
-    const int nchw = a.dedup ? 1 : 2;          /* mono dedup: K1 reads the left rows only */
+    /* one row per channel, s*2 + ch: the I filter's nonzero inputs sit at the even phases, the Q
+     * filter's at the odd ones, so the channel's signed sample {x, -x, -x, x}[k] serves both -- the
+     * I filter reads it where k is even (x, -x), the Q filter where k is odd (-x, x), and each takes
+     * the literal +0.0 at the other phases itself (icw_chain_x): 16 B per stereo frame, not 32 */
+    double *xs = a.xd + (size_t)s * 2 * a.x_pitch + t;
+    const int nchw = a.dedup ? 1 : 2;          /* mono dedup: K1 reads the left row only */
 #pragma unroll
     for (int ch = 0; ch < 2; ++ch) {
         if (ch < nchw) {
             const unsigned k = (a.hq_phase[s * 2 + ch] + (unsigned)(a.t0 + t)) & 3u;
-            xs[(size_t)(ch * 2 + 0) * a.x_pitch] = icw_filter_in(v[ch], k);
-            xs[(size_t)(ch * 2 + 1) * a.x_pitch] = icw_filter_in(v[ch], (k + 1u) & 3u);
+            xs[(size_t)ch * a.x_pitch] = (k == 0u || k == 3u) ? v[ch] : -v[ch];
         }
     }
 }
@@ -190,10 +191,25 @@ __device__ __forceinline__ void icw_fir_stage(const IcwFirArgs &f, int s, int ch
     const bool mono = f.nch == 1;
     const int nl = sh + M + nout + 24;               /* logical extent: pad, history, tile, margin */
     const int nf = min(nout, T - tt);
+    /* no fade anywhere in the frames this tile stages (uniform): icw_fade returns "none" for
+     * fi <= ix <= ns - fo and for ix >= ns */
+    const long long ja = max(tt - M, 0), jb = (long long)tt + nf - 1;
+    const bool nofade = p0 + ja >= fi && (p0 + jb <= ns - fo || p0 + ja >= ns);
     /* 8 consecutive inputs per thread and pass, their loads issued together (clamped in range,
      * selected after): the staging is load-latency bound otherwise */
     constexpr int V = 8;
     for (int i0 = tid * V; i0 < nl; i0 += nthr * V) {
+        /* the interior of the block (the common case): 8 inputs from the file, no history, no fade,
+         * no history write-back -- loads, conversions and stores only */
+        const int j0 = tt - M + i0 - sh;
+        if (nofade && i0 >= sh && j0 >= 0 && j0 + V - 1 < tt + nf && j0 + V - 1 < T - M) {
+            double raw[V];
+#pragma unroll
+            for (int e = 0; e < V; ++e) raw[e] = icw_unpack(src + (size_t)(j0 + e) * f.fsz, f.fmt);
+#pragma unroll
+            for (int e = 0; e < V; ++e) xs[icw_fir_phys(i0 + e)] = raw[e];
+            continue;
+        }
         double raw[V], his[V];
 #pragma unroll
         for (int e = 0; e < V; ++e) {

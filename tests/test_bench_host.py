@@ -34,3 +34,26 @@ def test_host_cores_census():
     assert set(cpus) <= set(os.sched_getaffinity(0))
     assert isinstance(model, str) and model
     assert topo["physical_in_affinity"] >= n
+
+
+def test_roofline_inputs_from_committed_profiles():
+    """the roofline fields recompute from profiles/: HBM bytes per launch from the newest PMC pass
+    of the workload (scaled by frames per launch), the issue model from its SQ pass (VALU per wave,
+    cycles per VALU = profiled launch time x SQ clock / VALU per wave), and the whole-chain FP64
+    work per frame of SURVEY 8(d) (4 filters x (15N - 4) for stereo)"""
+    import json
+    import bench
+    assert bench.chain_flops_per_frame(2) == 1124 and bench.chain_flops_per_frame(1) == 562
+    f = bench._latest("r*_c2_pmc.json")
+    pmc = json.loads(f.read_text())
+    fpl = float(pmc["frames_per_launch"])
+    t, src = bench.pmc_traffic("c2", "icw_iir_row", fpl)
+    k = next(v for kk, v in pmc["kernels"].items() if "icw_iir_row" in kk)
+    assert src == f.name and abs(t - k["hbm_bytes_corrected"]) < 1e-6 * t
+    t2, _ = bench.pmc_traffic("c2", "icw_iir_row", fpl / 2)
+    assert abs(t2 - t / 2) < 1e-6 * t
+    m = bench.sq_model("c2", "icw_iir_row")
+    valu, cpv, clk, ns, name = m
+    assert 3.0 < cpv < 6.0 and 1.5 < clk < 2.5 and valu > 0
+    assert abs(cpv - ns * clk / valu) < 1e-9
+    assert bench.pmc_traffic("c2", "no_such_kernel", fpl) == (None, None)
