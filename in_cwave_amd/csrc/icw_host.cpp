@@ -37,7 +37,7 @@ extern "C" hipError_t icw_launch_graph_serial(const IcwK4Args *a, hipStream_t st
 extern "C" hipError_t icw_launch_advance(const IcwAdvArgs *a, hipStream_t st);
 extern "C" hipError_t icw_launch_stream1(const IcwS1Args *a, int nord, hipStream_t st);
 extern "C" hipError_t icw_launch_fir(const IcwFirArgs *a, hipStream_t st);
-extern "C" hipError_t icw_launch_fir_graph(const IcwFirArgs *f, const IcwK2Args *a, hipStream_t st);
+extern "C" hipError_t icw_launch_fir_graph(const IcwFirArgs *f, const IcwK2Args *a, int in_step, hipStream_t st);
 extern "C" size_t icw_fir_graph_lds(int M, int nt, int nch, int n_regs);
 
 #define ICW_PI_H (3.1415926535897932384626433832795029)
@@ -169,6 +169,11 @@ struct icw_ctx {
      * state, or a set_state with equal halves, and no stereo block since) -- mono calls over such
      * streams run K1 on the left chains only */
     std::vector<char> lr_known;
+    /* host mirror of every stream's modulator frame counter (the device's n_frame, advanced by the same
+     * arithmetic as icw_advance): a call whose streams are all in step has every Shift / PM factor in
+     * the shared rotation table, so the fused FIR kernel takes its variant without the per-stream
+     * fallback (whose out-of-line call cost it scratch spills) */
+    std::vector<unsigned long long> nf_host;
     bool serial_render = false;
     uint32_t mt_seed_state[2][624];       /* seeded MT19937 states for L / R (mtrnd_init_seed) */
     hipStream_t stream = nullptr;
@@ -876,6 +881,7 @@ int icw_create(const icw_config *cfg, const icw_node *nodes, int n_nodes, int n_
     }
     c->peak_db.assign(S * 2, ICW_SR_ZERO_SIGNAL_DB);
     c->lr_known.assign(S, 1);
+    c->nf_host.assign(S, 0ull);
     {
         hipDeviceProp_t prop;
         if (hipGetDeviceProperties(&prop, c->device) == hipSuccess) c->n_cu = prop.multiProcessorCount;
@@ -963,6 +969,7 @@ int icw_stream_init(icw_ctx *c, int first, int count)
     for (size_t i = 0; i < n; ++i) c->lr_known[f + i] = 1;
     ok &= hipMemsetAsync(s.pos + f, 0, n * sizeof(long long), st) == hipSuccess;
     ok &= hipMemsetAsync(s.n_frame + f, 0, n * sizeof(unsigned long long), st) == hipSuccess;
+    for (size_t i = 0; i < n; ++i) c->nf_host[f + i] = 0;
     ok &= hipMemsetAsync(s.bus + f * ICW_N_INPUTS * 4, 0, n * ICW_N_INPUTS * 4 * sizeof(double), st) == hipSuccess;
     ok &= hipMemsetAsync(s.clips + f * 2, 0, n * 2 * sizeof(uint32_t), st) == hipSuccess;
     ok &= hipMemsetAsync(s.peak_bits + f * 2, 0, n * 2 * sizeof(unsigned long long), st) == hipSuccess;
@@ -1000,7 +1007,10 @@ int icw_stream_open(icw_ctx *c, int s, int64_t n_samples, uint32_t fade_in, uint
     bool ok = quiesce(c) == hipSuccess;
     ok &= hipMemcpy(c->st.fade + (size_t)s * 3, fd, sizeof(fd), hipMemcpyHostToDevice) == hipSuccess;
     ok &= hipMemset(c->st.pos + s, 0, sizeof(long long)) == hipSuccess;
-    if (clr_nframe) ok &= hipMemset(c->st.n_frame + s, 0, sizeof(unsigned long long)) == hipSuccess;
+    if (clr_nframe) {
+        ok &= hipMemset(c->st.n_frame + s, 0, sizeof(unsigned long long)) == hipSuccess;
+        c->nf_host[s] = 0;
+    }
     if (clr_hilb) {
         ok &= hipMemset(c->st.hist + (size_t)s * 4 * ICW_HIST_PITCH, 0, 4 * ICW_HIST_PITCH * sizeof(double)) == hipSuccess;
         ok &= hipMemset(c->st.sncnt + (size_t)s * 4, 0, 4 * sizeof(unsigned long long)) == hipSuccess;
@@ -1087,6 +1097,7 @@ int icw_stream_reset_framecnt(icw_ctx *c, int s)
     std::lock_guard<std::mutex> lk(c->mu);
     if (set_dev(c)) return ICW_EDEVICE;
     if (quiesce(c) != hipSuccess) return ICW_EDEVICE;
+    c->nf_host[s] = 0;
     return hipMemset(c->st.n_frame + s, 0, sizeof(unsigned long long)) == hipSuccess ? ICW_OK : ICW_EDEVICE;
 }
 
@@ -1355,6 +1366,8 @@ int icw_process_streams(icw_ctx *c, int first, int count, const void *in, size_t
             if (grow((void **)&c->rpre[p], &c->rpre_bytes[p], S * (size_t)Tb * 2 * sizeof(double))) return ICW_ENOMEM;
     /* the shared rotation table pays from two streams on; one stream computes its factors inline */
     const bool table = c->prog.needs_omega && !bus && c->prog.n_trig > 0 && count > 1;
+    bool in_step = table;
+    for (int i = 1; in_step && i < count; ++i) in_step = c->nf_host[first + i] == c->nf_host[first];
     if (table && grow((void **)&c->trig, &c->trig_bytes, (size_t)Tb * 2 * c->prog.n_trig * sizeof(double)))
         return ICW_ENOMEM;
     if (bus)
@@ -1679,7 +1692,7 @@ int icw_process_streams(icw_ctx *c, int first, int count, const void *in, size_t
             const IcwFirArgs af = fir_args(b);
             if (io_in(b, s2) != ICW_OK) return ICW_EDEVICE;
             if (timing && hipEventRecord(c->ev[4 * b], s2) != hipSuccess) return ICW_EDEVICE;
-            if (icw_launch_fir_graph(&af, &a2, s2) != hipSuccess) return ICW_EDEVICE;
+            if (icw_launch_fir_graph(&af, &a2, in_step, s2) != hipSuccess) return ICW_EDEVICE;
             if (timing && hipEventRecord(c->ev[4 * b + 1], s2) != hipSuccess) return ICW_EDEVICE;
         } else {
             if (fir_async && hipStreamWaitEvent(s2, c->k0done[p], 0) != hipSuccess) return ICW_EDEVICE;
@@ -1771,6 +1784,10 @@ int icw_process_streams(icw_ctx *c, int first, int count, const void *in, size_t
         const IcwAdvArgs av = adv_args();
         if (icw_launch_advance(&av, st) != hipSuccess) return ICW_EDEVICE;
     }   /* !s1 */
+    for (int i = 0; i < count; ++i) {   /* icw_advance's arithmetic */
+        unsigned long long &v = c->nf_host[first + i];
+        v = cfg.frmod_scaled ? (v + (unsigned long long)n_frames) % ssr : v + (unsigned long long)n_frames;
+    }
     if (legacy && hipStreamSynchronize(st) != hipSuccess) return ICW_EDEVICE;
     if (!dev) {
         unsigned char *h_out = pinned ? c->h_stage + stage_in : nullptr;
@@ -1959,6 +1976,7 @@ int icw_set_state(icw_ctx *c, int s, const void *blob, size_t size)
     long long fd[3] = {b.n_samples, b.n_fade_in, b.n_fade_out};
     bool ok = quiesce(c) == hipSuccess;
     ok &= hipMemcpy(c->st.n_frame + s, &b.n_frame, 8, hipMemcpyHostToDevice) == hipSuccess;
+    c->nf_host[s] = b.n_frame;
     ok &= hipMemcpy(c->st.pos + s, &b.pos, 8, hipMemcpyHostToDevice) == hipSuccess;
     ok &= hipMemcpy(c->st.fade + (size_t)s * 3, fd, sizeof(fd), hipMemcpyHostToDevice) == hipSuccess;
     ok &= hipMemcpy(c->st.hq_phase + (size_t)s * 2, b.hq_phase, 8, hipMemcpyHostToDevice) == hipSuccess;

@@ -128,22 +128,48 @@ __device__ __forceinline__ void icw_iir_step_z(double (&R)[N], const double (&pc
     R[J] = S;
 }
 
-/* A block of N steps whose input is zero at the steps J with (J & 1) == Z.  The next block's
- * zero steps are the other parity (N is odd), so the look-ahead refill of xv[J] is needed exactly
- * where this block's step J had a zero input. */
-template <int N, int J0, int Z, bool SUBN, bool SPEC = false>
+/* A block of N steps whose input is zero at the steps J with (J & 1) == Z; the look-ahead refill
+ * of xv[J] happens where the NEXT block's step J consumes an input (its zero parity ZN: the other
+ * one for odd N, the same one for even N) */
+template <int N, int J0, int Z, bool SUBN, bool SPEC = false, int ZN = 1 - Z>
 __device__ __forceinline__ void icw_block_steps_zpf(double (&R)[N], double (&xv)[N], const double *xnext,
                                                     const double (&pc)[20], unsigned &cnt, double *mn = nullptr)
 {
     if constexpr (J0 < N) {
-        if constexpr ((J0 & 1) == Z) {
-            icw_iir_step_z<N, J0, SPEC>(R, pc, cnt, mn);
-            xv[J0] = xnext[J0];
-        } else {
-            icw_iir_step<N, true, SUBN, J0, SPEC>(R, xv[J0], pc, cnt, mn);
-        }
-        icw_block_steps_zpf<N, J0 + 1, Z, SUBN, SPEC>(R, xv, xnext, pc, cnt, mn);
+        if constexpr ((J0 & 1) == Z) icw_iir_step_z<N, J0, SPEC>(R, pc, cnt, mn);
+        else icw_iir_step<N, true, SUBN, J0, SPEC>(R, xv[J0], pc, cnt, mn);
+        if constexpr ((J0 & 1) != ZN) xv[J0] = xnext[J0];
+        icw_block_steps_zpf<N, J0 + 1, Z, SUBN, SPEC, ZN>(R, xv, xnext, pc, cnt, mn);
     }
+}
+
+/* even orders: every block of N (even) steps has the same zero steps, (J & 1) == Z; speculative
+ * blocks first, then (after a block whose smallest |sum| fell below 1) the exact ones from its start */
+template <int N, int Z, bool SUBN>
+__device__ __forceinline__ void icw_even_blocks(double (&R)[N], double (&xv)[N], const double *xp, double *wrow,
+                                                const double (&pc)[20], unsigned &cnt, int &t, int T)
+{
+    double mn = __builtin_inf();
+    bool fail = false;
+    ICW_DRAIN_VMEM();
+    while (!fail && t + N <= T) {
+        icw_block_steps_zpf<N, 0, Z, SUBN, true, Z>(R, xv, xp + t + N, pc, cnt, &mn);
+        icw_store_block<N>(R, wrow + N + t);
+        fail = __any(mn < 1.0);
+        if (!fail) t += N;
+    }
+    if (fail) {
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+#pragma unroll
+        for (int j = 0; j < N; ++j) R[j] = wrow[t + j];
+        icw_load_x<N>(xv, xp + t);
+        ICW_DRAIN_VMEM();
+        for (; t + N <= T; t += N) {
+            icw_block_steps_zpf<N, 0, Z, SUBN, false, Z>(R, xv, xp + t + N, pc, cnt);
+            icw_store_block<N>(R, wrow + N + t);
+        }
+    }
+    icw_load_x<N>(xv, xp + t);   /* the zero steps left part of xv unloaded */
 }
 
 
@@ -207,10 +233,18 @@ __global__ __launch_bounds__(256) void icw_iir_state(IcwK1Args a)
         icw_load_x<N>(xv, xp);
         bool zfast = false;
         unsigned phi0 = 0;
-        if constexpr (KAHAN && SUBN && (N & 1)) {
+        if constexpr (KAHAN && SUBN) {
             /* the fast path needs one zero-input parity across the wave */
             phi0 = __builtin_amdgcn_readfirstlane(phi);
             zfast = __all(phi == phi0) && T >= 3 * N;
+        }
+        if constexpr (KAHAN && SUBN && !(N & 1)) {
+            /* even order: block-relative step J of every block (t a multiple of N) is a zero input
+             * iff (phi0 + J) is odd */
+            if (zfast) {
+                if (phi0) icw_even_blocks<N, 0, SUBN>(R, xv, xp, wrow, pc, cnt, t, T);
+                else icw_even_blocks<N, 1, SUBN>(R, xv, xp, wrow, pc, cnt, t, T);
+            }
         }
         if constexpr (KAHAN && SUBN && (N & 1)) {
             if (zfast) {

@@ -163,8 +163,9 @@ constexpr int icw_row_c0_lane() { return N - 17; }
  * twice), which the I0 = 0 chain turns into T in place. */
 template <int N, int J, int Z, bool SPEC>
 __device__ __forceinline__ void icw_row_step(double (&W)[N], double (&P)[N], double (&P2)[N], double xin,
-                                             double xin2, const IcwRowC &c, double &mn)
+                                             double xin2, const IcwRowC &c, double &mn, bool qodd = false)
 {
+    if constexpr (Z == 2) xin = icw_chain_x<J>(xin, qodd);   /* generic steps: the zero inputs supplied */
     constexpr bool ZS = Z != 2 && (J & 1) == Z;
     constexpr bool C0P = icw_row_c0p<N>() && Z != 2 && !ZS;
     double S;
@@ -201,27 +202,27 @@ __device__ __forceinline__ void icw_row_step(double (&W)[N], double (&P)[N], dou
 template <int N, int J, int Z, int ZN, bool SPEC>
 __device__ __forceinline__ void icw_row_block(double (&W)[N], double (&P)[N], double (&P2)[N], double (&xv)[N],
                                               double (&xv2)[N], const double *xnext, const double *xnext2,
-                                              const IcwRowC &c, double &mn)
+                                              const IcwRowC &c, double &mn, bool qodd = false)
 {
     if constexpr (J < N) {
-        icw_row_step<N, J, Z, SPEC>(W, P, P2, xv[J], xv2[J], c, mn);
+        icw_row_step<N, J, Z, SPEC>(W, P, P2, xv[J], xv2[J], c, mn, qodd);
         if constexpr (!(ZN != 2 && (J & 1) == ZN)) {
             xv[J] = xnext[J];
             if constexpr (icw_row_c0p<N>() && ZN != 2) xv2[J] = xnext2[J];
         }
-        icw_row_block<N, J + 1, Z, ZN, SPEC>(W, P, P2, xv, xv2, xnext, xnext2, c, mn);
+        icw_row_block<N, J + 1, Z, ZN, SPEC>(W, P, P2, xv, xv2, xnext, xnext2, c, mn, qodd);
     }
 }
 
 template <int N, int J>
 __device__ __forceinline__ void icw_row_block_lim(double (&W)[N], double (&P)[N], double (&P2)[N],
-                                                  const double (&xv)[N], const IcwRowC &c, int lim)
+                                                  const double (&xv)[N], const IcwRowC &c, int lim, bool qodd)
 {
     if constexpr (J < N) {
         if (J < lim) {
             double mn;
-            icw_row_step<N, J, 2, false>(W, P, P2, xv[J], 0.0, c, mn);
-            icw_row_block_lim<N, J + 1>(W, P, P2, xv, c, lim);
+            icw_row_step<N, J, 2, false>(W, P, P2, xv[J], 0.0, c, mn, qodd);
+            icw_row_block_lim<N, J + 1>(W, P, P2, xv, c, lim, qodd);
         }
     }
 }
@@ -293,7 +294,9 @@ __device__ __forceinline__ void icw_iir_row_body(const IcwK1Args &a, int gl)
     icw_row_products<N>(W, P, P2, c);
 
     if (writer && ch == 0) a.info_dup[s * 2 + f] = a.lr_equal[s * 2 + f];
-    const double *xp = a.xd + (size_t)g * a.x_pitch;
+    const double *xp = a.xd + (size_t)(s * 2 + ch) * a.x_pitch;     /* the channel's signed row (K0) */
+    /* block-relative sample n has a zero input iff (phi + n) is odd (see icw_iir_state) */
+    const unsigned phi = (a.hq_phase[s * 2 + ch] + (unsigned)a.t0 + (unsigned)f) & 1u;
     /* the same row through a pointer the compiler cannot equate with xp: the zero-input loops of
      * orders > 17 load each input into two registers (icw_row_step's xin2), not load + copy */
     int zoff = 0;
@@ -308,8 +311,6 @@ __device__ __forceinline__ void icw_iir_row_body(const IcwK1Args &a, int gl)
         double xv[N], xv2[N];
         icw_load_x<N>(xv, xp);
         if constexpr (icw_row_c0p<N>()) icw_load_x<N>(xv2, xp2);
-        /* block-relative sample n has a zero input iff (phi + n) is odd (see icw_iir_state) */
-        const unsigned phi = (a.hq_phase[s * 2 + ch] + (unsigned)a.t0 + (unsigned)f) & 1u;
         const unsigned phi0 = __builtin_amdgcn_readfirstlane(phi);
         const bool zfast = __all(phi == phi0) && T >= 3 * N;
         double mn = __builtin_inf();               /* smallest |sum| of the speculative block */
@@ -381,7 +382,8 @@ __device__ __forceinline__ void icw_iir_row_body(const IcwK1Args &a, int gl)
             icw_load_x<N>(xv, xp + t);
         }
         for (; t + N <= T; t += N) {
-            icw_row_block<N, 0, 2, 2, false>(W, P, P2, xv, xv2, xp + t + N, xp2 + t + N, c, mn);
+            icw_row_block<N, 0, 2, 2, false>(W, P, P2, xv, xv2, xp + t + N, xp2 + t + N, c, mn,
+                                             ((phi + (unsigned)t) & 1u) != 0u);
             icw_row_store<N>(W, wrow + N + t, writer);
         }
     }
@@ -390,7 +392,7 @@ __device__ __forceinline__ void icw_iir_row_body(const IcwK1Args &a, int gl)
         double xv[N];
 #pragma unroll
         for (int j = 0; j < N; ++j) xv[j] = (j < rem) ? xp[t + j] : 0.0;
-        icw_row_block_lim<N, 0>(W, P, P2, xv, c, rem);
+        icw_row_block_lim<N, 0>(W, P, P2, xv, c, rem, ((phi + (unsigned)t) & 1u) != 0u);
         if (writer) {
             double *wo = wrow + N + t;
 #pragma unroll

@@ -176,6 +176,10 @@ __global__ __launch_bounds__(256) void icw_unpack_frames(IcwK0Args a)
 
 __device__ __forceinline__ int icw_fir_phys(int i) { return i + (i >> 3); }
 
+#ifndef ICW_FIR_STAGE_FAST
+#define ICW_FIR_STAGE_FAST 1          /* 0: every staged input through the general path (A/B builds) */
+#endif
+
 /* inputs of channel ch for the outputs [tt, tt + nout) of a launch block, at logical index
  * i <-> frame j = tt - M + i - sh (zero outside [-M, T)); the history after the block is written by
  * the tile that owns each of its frames */
@@ -202,7 +206,7 @@ __device__ __forceinline__ void icw_fir_stage(const IcwFirArgs &f, int s, int ch
         /* the interior of the block (the common case): 8 inputs from the file, no history, no fade,
          * no history write-back -- loads, conversions and stores only */
         const int j0 = tt - M + i0 - sh;
-        if (nofade && i0 >= sh && j0 >= 0 && j0 + V - 1 < tt + nf && j0 + V - 1 < T - M) {
+        if (ICW_FIR_STAGE_FAST && nofade && i0 >= sh && j0 >= 0 && j0 + V - 1 < tt + nf && j0 + V - 1 < T - M) {
             double raw[V];
 #pragma unroll
             for (int e = 0; e < V; ++e) raw[e] = icw_unpack(src + (size_t)(j0 + e) * f.fsz, f.fmt);
@@ -574,7 +578,7 @@ __device__ __noinline__ double2 icw_trig_call(const IcwOp &op, int c, double ome
 /* One DSP node on its mixed input d (adv_modulator.c:669-751): channel exchange, I/Q swap,
  * gains, then Master (-> lOut/rOut) or Shift / PM / Mix (-> o, returns true).  trow: this frame's
  * row of the rotation table (nullable: compute the factors inline). */
-template <bool TRIG = true>
+template <bool TRIG = true, bool TAB = false>
 __device__ __forceinline__ bool icw_exec_op(const IcwOp &op, IcwLR d, double omega, IcwLR &o, double &lOut,
                                             double &rOut, const double *trow = nullptr)
 {
@@ -606,12 +610,12 @@ __device__ __forceinline__ bool icw_exec_op(const IcwOp &op, IcwLR d, double ome
         if constexpr (!TRIG) { o = d; return true; }   /* no active Shift/PM in the program */
         double cs, sn;
         if (op.act[0]) {
-            if (trow) { cs = trow[op.tslot[0] * 2]; sn = trow[op.tslot[0] * 2 + 1]; }
+            if (TAB || trow) { cs = trow[op.tslot[0] * 2]; sn = trow[op.tslot[0] * 2 + 1]; }
             else { const double2 f = icw_trig_call(op, 0, omega); cs = f.x; sn = f.y; }
             icw_rot(d.lre, d.lim, cs, sn, o.lre, o.lim);
         } else { o.lre = d.lre; o.lim = d.lim; }
         if (op.act[1]) {
-            if (trow) { cs = trow[op.tslot[1] * 2]; sn = trow[op.tslot[1] * 2 + 1]; }
+            if (TAB || trow) { cs = trow[op.tslot[1] * 2]; sn = trow[op.tslot[1] * 2 + 1]; }
             else { const double2 f = icw_trig_call(op, 1, omega); cs = f.x; sn = f.y; }
             icw_rot(d.rre, d.rim, cs, sn, o.rre, o.rim);
         } else { o.rre = d.rre; o.rim = d.rim; }
@@ -626,7 +630,7 @@ __device__ __forceinline__ bool icw_exec_op(const IcwOp &op, IcwLR d, double ome
 /* One frame's `in` through the rest of the block (K2 and the fused converter KF2): the bus-form
  * hand-off, or the DSP list (adv_modulator.c:637-751) on the LDS register file, the pre-render
  * doubles and the elementwise ROUND render with the meters' per-thread parts. */
-template <bool TRIG>
+template <bool TRIG, bool TAB = false>
 __device__ __forceinline__ void icw_frame_graph(const IcwK2Args &a, const IcwProg *P, const IcwRegFile &R, int s,
                                                 int t, const IcwLR &in, bool use_tab, unsigned &clip_l,
                                                 unsigned &clip_r, double &pk_l, double &pk_r)
@@ -662,7 +666,7 @@ __device__ __forceinline__ void icw_frame_graph(const IcwK2Args &a, const IcwPro
                 }
             }
             IcwLR o;
-            if (icw_exec_op<TRIG>(op, d, omega, o, lOut, rOut, trow)) {
+            if (icw_exec_op<TRIG, TAB>(op, d, omega, o, lOut, rOut, trow)) {
                 R.set(op.out_reg, o);
                 if (last && op.wb_slot >= 0) {
                     double *b = bus_s + op.wb_slot * 4;
@@ -896,12 +900,14 @@ __global__ __launch_bounds__(ICW_K2_TILE, ICW_K2_MINWG) void icw_output(IcwK2Arg
  * analytic signal never leaves the registers (KF + K2 move 32 B per frame through HBM twice); the
  * sums are KF's, in the same order, so the results are KF + K2's bit for bit.  Dynamic LDS: the
  * padded inputs of each computed channel, the taps, the DSP register file. */
-/* Occupancy: 4 workgroups (4 waves per SIMD, <= 128 VGPRs) without a Shift / PM node; 3 with one
- * (<= 168 VGPRs): at 128 the per-stream fallback call (icw_trig_call) left values live across it that
- * the allocator spilled to scratch -- 44 B per thread written to HBM, which was most of the kernel's
- * 2.95x write traffic (profiles/r02_c2fir_pmc.json: 198 MB per launch against 67 MB of output) */
-template <bool TRIG>
-__global__ __launch_bounds__(256, TRIG ? 3 : 4) void icw_fir_graph(IcwFirArgs f, IcwK2Args a)
+/* Occupancy: 4 workgroups per CU (4 waves per SIMD, <= 128 VGPRs).  TAB: every stream of the launch
+ * is in step with the rotation table (the host's frame-counter mirror says so), so the per-stream
+ * fallback (icw_trig_call) is compiled out.  With the call in the kernel the allocator kept values
+ * live across it in scratch -- 44 B per thread written to HBM, most of the kernel's 2.95x write
+ * traffic (profiles/r02_c2fir_pmc.json: 198 MB per launch against 67 MB of output); giving that
+ * variant 168 VGPRs instead (3 workgroups per CU) removed the spills but cost c2fir 22 %. */
+template <bool TRIG, bool TAB>
+__global__ __launch_bounds__(256, 4) void icw_fir_graph(IcwFirArgs f, IcwK2Args a)
 {
     extern __shared__ double lds[];
     __shared__ unsigned red_clip[2][ICW_K2_TILE / 64];
@@ -936,7 +942,7 @@ __global__ __launch_bounds__(256, TRIG ? 3 : 4) void icw_fir_graph(IcwFirArgs f,
         IcwLR v; v.lre = b[0]; v.lim = b[1]; v.rre = b[2]; v.rim = b[3];
         Rf.set(P->persist_reg[r], v);
     }
-    const bool use_tab = TRIG && a.trig_tab && a.n_frame[s] == a.n_frame[0];
+    const bool use_tab = TAB || (TRIG && a.trig_tab && a.n_frame[s] == a.n_frame[0]);
     unsigned clip_l = 0, clip_r = 0;
     double pk_l = 0.0, pk_r = 0.0;
     if (nchc == 2) {
@@ -951,7 +957,7 @@ __global__ __launch_bounds__(256, TRIG ? 3 : 4) void icw_fir_graph(IcwFirArgs f,
                 IcwLR in;
                 if (ch) { in.lre = oi; in.lim = oq; in.rre = vi[r + 4]; in.rim = q[r + 4]; }
                 else { in.lre = vi[r]; in.lim = q[r]; in.rre = oi; in.rim = oq; }
-                icw_frame_graph<TRIG>(a, P, Rf, s, tt + fr, in, use_tab, clip_l, clip_r, pk_l, pk_r);
+                icw_frame_graph<TRIG, TAB>(a, P, Rf, s, tt + fr, in, use_tab, clip_l, clip_r, pk_l, pk_r);
             }
         }
     } else {
@@ -962,7 +968,7 @@ __global__ __launch_bounds__(256, TRIG ? 3 : 4) void icw_fir_graph(IcwFirArgs f,
                 IcwLR in;
                 in.lre = in.rre = vi[r];
                 in.lim = in.rim = q[r];
-                icw_frame_graph<TRIG>(a, P, Rf, s, tt + fr, in, use_tab, clip_l, clip_r, pk_l, pk_r);
+                icw_frame_graph<TRIG, TAB>(a, P, Rf, s, tt + fr, in, use_tab, clip_l, clip_r, pk_l, pk_r);
             }
         }
     }
@@ -1983,17 +1989,21 @@ extern "C" size_t icw_fir_graph_lds(int M, int nt, int nch, int n_regs)
     return lds <= 96 * 1024 ? lds : 0;
 }
 
-extern "C" hipError_t icw_launch_fir_graph(const IcwFirArgs *f, const IcwK2Args *a, hipStream_t st)
+/* in_step: every stream of the launch is in step with the rotation table (a->trig_tab) */
+extern "C" hipError_t icw_launch_fir_graph(const IcwFirArgs *f, const IcwK2Args *a, int in_step, hipStream_t st)
 {
     if (!fir_ok(f->M, f->nt)) return hipErrorInvalidValue;
     const size_t lds = icw_fir_graph_lds(f->M, f->nt, f->nch, a->n_regs);
     if (!lds) return hipErrorInvalidValue;
+    if (in_step && !(a->trig && a->trig_tab)) return hipErrorInvalidValue;
     const int TF = 256 * ICW_FIR_R / (f->nch > 1 ? 2 : 1);
     dim3 grid((f->T + TF - 1) / TF, f->n_streams);
-    const void *fn = a->trig ? (const void *)icw_fir_graph<true> : (const void *)icw_fir_graph<false>;
+    const void *fn = !a->trig ? (const void *)icw_fir_graph<false, false>
+                   : in_step ? (const void *)icw_fir_graph<true, true> : (const void *)icw_fir_graph<true, false>;
     if (fir_lds_attr(fn, lds) != hipSuccess) return hipErrorInvalidValue;
-    if (a->trig) hipLaunchKernelGGL(icw_fir_graph<true>, grid, dim3(256), lds, st, *f, *a);
-    else hipLaunchKernelGGL(icw_fir_graph<false>, grid, dim3(256), lds, st, *f, *a);
+    if (!a->trig) hipLaunchKernelGGL((icw_fir_graph<false, false>), grid, dim3(256), lds, st, *f, *a);
+    else if (in_step) hipLaunchKernelGGL((icw_fir_graph<true, true>), grid, dim3(256), lds, st, *f, *a);
+    else hipLaunchKernelGGL((icw_fir_graph<true, false>), grid, dim3(256), lds, st, *f, *a);
     return hipGetLastError();
 }
 
