@@ -62,6 +62,18 @@ CLOCK_GHZ = 2.31
 K1_VALU_PER_SAMPLE = {0: 91.1, 3: 75.4}        # by ICW_K1_* (icw_last_k1_kernel)
 K1_KERNEL_NAME = {0: "icw_iir_state", 3: "icw_iir_row", 4: "icw_iir_state_fc"}
 CYC_PER_FP64_VALU = 4.83
+
+
+def fp64_issue_floor():
+    """cycles per dependent FP64 add on gfx950: a chain of v_add_f64, each reading the previous
+    result, on one wave with 64 active lanes (tools/lat_probe.hip, profiles/r01_fp64_latency_probe.txt)"""
+    import re
+    f = ROOT / "profiles" / "r01_fp64_latency_probe.txt"
+    try:
+        m = re.search(r"active lanes 64: dep_add ([0-9.]+) cyc/op", f.read_text())
+        return float(m.group(1)), f.name
+    except (OSError, AttributeError, ValueError):
+        return 4.62, None
 # SURVEY 8(d): the path's algorithmic FP64 work per frame is the whole Kahan IIR of
 # iir_rp_process_kahan (hblpf.c:1017-1056): 15N - 4 flops per filter-sample (N = 19: 281), over the
 # 4 filters of a stereo frame (1 124) or the 2 of a mono frame under the dedup (562) -- the
@@ -519,7 +531,12 @@ def measure_gpu(wname, streams, frames, steps, warmup, e2e_steps, dev, local_dev
         valu = valu_wave / (sq_frames / S) if sq_frames else K1_VALU_PER_SAMPLE.get(k1_kind)
     else:
         valu, cpv, clock_ghz, sq_src = K1_VALU_PER_SAMPLE.get(k1_kind), CYC_PER_FP64_VALU, 2.32, None
-    floor_ms = (samples_per_chain * valu * cpv / (clock_ghz * 1e6)) if valu else None
+    # the issue floor: the kernel's VALU per sample, each at the dependent FP64 add rate (the
+    # recurrence is one dependent chain: ~74 of its ~75 VALU per sample are on it), at
+    # the clock of the SQ pass; the SQ pass's own cycles per VALU is the kernel as profiled (frac ~1)
+    cfl, cfl_src = fp64_issue_floor()
+    floor_ms = (samples_per_chain * valu * cfl / (clock_ghz * 1e6)) if valu else None
+    model_ms = (samples_per_chain * valu * cpv / (clock_ghz * 1e6)) if valu else None
     # the whole path's FP64 work over the step: every filter's Kahan IIR, per GPU
     chain_fpf = chain_flops_per_frame(W["ch"])
     chain_tf = chain_fpf * float(S) * T / (ms_per_step / 1e3) / 1e12
@@ -535,13 +552,16 @@ def measure_gpu(wname, streams, frames, steps, warmup, e2e_steps, dev, local_dev
                        "frac": chain_tf / FP64_PEAK_TFLOPS,
                        "note": "SURVEY 8(d): the Kahan IIR of every filter (15N - 4 flops per filter-sample, "
                                "hblpf.c:1017-1056), per GPU, over ms_per_step"},
-        "issue_bound": {"kind": "model", "valu_per_sample": valu, "cycles_per_valu": cpv, "clock_ghz": clock_ghz,
-                        "source": f"profiles/{sq_src}" if sq_src else "round-2 constants",
+        "issue_bound": {"valu_per_sample": valu, "cycles_per_valu_floor": cfl, "clock_ghz": clock_ghz,
                         "floor_ms_per_launch": floor_ms,
                         "frac": (floor_ms / (k1_avg_s * 1e3)) if (k1_avg_s and floor_ms) else None,
-                        "note": "VALU per sample x cycles per VALU at the clock of the committed SQ pass of this "
-                                "kernel; frac = that time / this run's launch time (~1: the recurrence runs at "
-                                "the issue rate it was profiled at; boxes differ by a few %)"},
+                        "floor_source": f"profiles/{cfl_src}" if cfl_src else "constant",
+                        "sq_source": f"profiles/{sq_src}" if sq_src else "round-2 constants",
+                        "sq_cycles_per_valu": cpv, "sq_model_ms_per_launch": model_ms,
+                        "note": "floor = VALU per sample (SQ pass) x cycles per dependent FP64 add (a v_add_f64 "
+                                "chain on one wave, latency probe) / the SQ pass's clock; frac = floor / this "
+                                "run's launch time.  sq_model = the same VALU at the SQ pass's own cycles per "
+                                "VALU (the kernel as profiled: ~1 x the launch time)"},
         "note": f"serial IIR recurrence: {chains_per_stream * S} DF-II chains per GPU, each a dependent "
                 f"chain of ~{4 * IIR_ORDER} FP64 ops per sample ({'one 16-lane DPP row' if k1_kind == 3 else 'one lane'}"
                 f" per chain); `frac` is the algorithmic FP64 rate (5N = {5 * IIR_ORDER} flops per chain-sample) "

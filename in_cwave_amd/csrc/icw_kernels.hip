@@ -176,9 +176,6 @@ __global__ __launch_bounds__(256) void icw_unpack_frames(IcwK0Args a)
 
 __device__ __forceinline__ int icw_fir_phys(int i) { return i + (i >> 3); }
 
-#ifndef ICW_FIR_STAGE_FAST
-#define ICW_FIR_STAGE_FAST 1          /* 0: every staged input through the general path (A/B builds) */
-#endif
 
 /* inputs of channel ch for the outputs [tt, tt + nout) of a launch block, at logical index
  * i <-> frame j = tt - M + i - sh (zero outside [-M, T)); the history after the block is written by
@@ -195,25 +192,10 @@ __device__ __forceinline__ void icw_fir_stage(const IcwFirArgs &f, int s, int ch
     const bool mono = f.nch == 1;
     const int nl = sh + M + nout + 24;               /* logical extent: pad, history, tile, margin */
     const int nf = min(nout, T - tt);
-    /* no fade anywhere in the frames this tile stages (uniform): icw_fade returns "none" for
-     * fi <= ix <= ns - fo and for ix >= ns */
-    const long long ja = max(tt - M, 0), jb = (long long)tt + nf - 1;
-    const bool nofade = p0 + ja >= fi && (p0 + jb <= ns - fo || p0 + ja >= ns);
     /* 8 consecutive inputs per thread and pass, their loads issued together (clamped in range,
      * selected after): the staging is load-latency bound otherwise */
     constexpr int V = 8;
     for (int i0 = tid * V; i0 < nl; i0 += nthr * V) {
-        /* the interior of the block (the common case): 8 inputs from the file, no history, no fade,
-         * no history write-back -- loads, conversions and stores only */
-        const int j0 = tt - M + i0 - sh;
-        if (ICW_FIR_STAGE_FAST && nofade && i0 >= sh && j0 >= 0 && j0 + V - 1 < tt + nf && j0 + V - 1 < T - M) {
-            double raw[V];
-#pragma unroll
-            for (int e = 0; e < V; ++e) raw[e] = icw_unpack(src + (size_t)(j0 + e) * f.fsz, f.fmt);
-#pragma unroll
-            for (int e = 0; e < V; ++e) xs[icw_fir_phys(i0 + e)] = raw[e];
-            continue;
-        }
         double raw[V], his[V];
 #pragma unroll
         for (int e = 0; e < V; ++e) {
@@ -630,10 +612,11 @@ __device__ __forceinline__ bool icw_exec_op(const IcwOp &op, IcwLR d, double ome
 /* One frame's `in` through the rest of the block (K2 and the fused converter KF2): the bus-form
  * hand-off, or the DSP list (adv_modulator.c:637-751) on the LDS register file, the pre-render
  * doubles and the elementwise ROUND render with the meters' per-thread parts. */
-template <bool TRIG, bool TAB = false>
+/* DEFER: the rendered integers go to dv[0..1] instead of the output row (KF2 stores 4 frames at once) */
+template <bool TRIG, bool TAB = false, bool DEFER = false>
 __device__ __forceinline__ void icw_frame_graph(const IcwK2Args &a, const IcwProg *P, const IcwRegFile &R, int s,
                                                 int t, const IcwLR &in, bool use_tab, unsigned &clip_l,
-                                                unsigned &clip_r, double &pk_l, double &pk_r)
+                                                unsigned &clip_r, double &pk_l, double &pk_r, int *dv = nullptr)
 {
     const int T = a.T;
     if (a.iq_out) {
@@ -682,6 +665,11 @@ __device__ __forceinline__ void icw_frame_graph(const IcwK2Args &a, const IcwPro
         if (a.do_render) {
             const int vl = icw_render_round(lOut, a.rk, clip_l, pk_l);
             const int vr = icw_render_round(rOut, a.rk, clip_r, pk_r);
+            if constexpr (DEFER) {
+                dv[0] = vl;
+                dv[1] = vr;
+                return;
+            }
             unsigned char *o = a.out + (size_t)s * a.out_stride;
             if (a.rk.is24) {
                 unsigned char *q = o + (size_t)t * 6;
@@ -946,18 +934,70 @@ __global__ __launch_bounds__(256, 4) void icw_fir_graph(IcwFirArgs f, IcwK2Args 
     unsigned clip_l = 0, clip_r = 0;
     double pk_l = 0.0, pk_r = 0.0;
     if (nchc == 2) {
-        /* lane l (L) keeps frames 0-3 and gets R's values of them; lane l + 32 (R) frames 4-7 */
+        /* lane l (L) keeps frames 0-3 and gets R's values of them; lane l + 32 (R) frames 4-7.  Their
+         * rendered frames are stored together: lane l's four at byte 32 ll, lane l + 32's at 32 ll + 16
+         * (16-bit output), so one 16-byte store per lane covers the wave's 1 KB contiguously.  One
+         * 4-byte store per frame instead put 2 of every 32 bytes in each store instruction, and the L2
+         * wrote the partial sectors out 2.3x over (r03_c2fir_pmc.json before this change: WRITE_SIZE
+         * 153 MB per launch against 67 MB of output). */
         const int h = ch ? 4 : 0;
+        int dv[4][2];
+        const int fr0 = ICW_FIR_R * ll + h;
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
             const double oi = __shfl_xor(ch ? vi[r] : vi[r + 4], 32);
             const double oq = __shfl_xor(ch ? q[r] : q[r + 4], 32);
-            const int fr = ICW_FIR_R * ll + h + r;
+            const int fr = fr0 + r;
+            dv[r][0] = dv[r][1] = 0;
             if (fr < nf) {
                 IcwLR in;
                 if (ch) { in.lre = oi; in.lim = oq; in.rre = vi[r + 4]; in.rim = q[r + 4]; }
                 else { in.lre = vi[r]; in.lim = q[r]; in.rre = oi; in.rim = oq; }
-                icw_frame_graph<TRIG, TAB>(a, P, Rf, s, tt + fr, in, use_tab, clip_l, clip_r, pk_l, pk_r);
+                icw_frame_graph<TRIG, TAB, true>(a, P, Rf, s, tt + fr, in, use_tab, clip_l, clip_r, pk_l, pk_r, dv[r]);
+            }
+        }
+        if (a.do_render && !a.iq_out) {
+            unsigned char *o = a.out + (size_t)s * a.out_stride;
+            const int nv = min(4, nf - fr0);
+            if (a.rk.is24) {
+                /* 6 bytes per frame: 24 contiguous bytes per lane */
+                unsigned char *p = o + (size_t)(tt + fr0) * 6;
+                if (nv == 4 && !((uintptr_t)p & 7)) {
+                    unsigned w[6];
+#pragma unroll
+                    for (int r = 0; r < 4; r += 2) {
+                        const unsigned l0 = (unsigned)dv[r][0] & 0xffffffu, r0 = (unsigned)dv[r][1] & 0xffffffu;
+                        const unsigned l1 = (unsigned)dv[r + 1][0] & 0xffffffu, r1 = (unsigned)dv[r + 1][1] & 0xffffffu;
+                        w[r / 2 * 3 + 0] = l0 | (r0 << 24);
+                        w[r / 2 * 3 + 1] = (r0 >> 8) | (l1 << 16);
+                        w[r / 2 * 3 + 2] = (l1 >> 16) | (r1 << 8);
+                    }
+                    uint2 *q2 = (uint2 *)p;
+                    q2[0] = make_uint2(w[0], w[1]);
+                    q2[1] = make_uint2(w[2], w[3]);
+                    q2[2] = make_uint2(w[4], w[5]);
+                } else {
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        if (r >= nv) break;
+                        unsigned char *b = p + r * 6;
+                        const int vl = dv[r][0], vr = dv[r][1];
+                        b[0] = (unsigned char)vl; b[1] = (unsigned char)(vl >> 8); b[2] = (unsigned char)(vl >> 16);
+                        b[3] = (unsigned char)vr; b[4] = (unsigned char)(vr >> 8); b[5] = (unsigned char)(vr >> 16);
+                    }
+                }
+            } else {
+                unsigned pk[4];
+#pragma unroll
+                for (int r = 0; r < 4; ++r) pk[r] = ((unsigned)dv[r][0] & 0xffffu) | ((unsigned)dv[r][1] << 16);
+                unsigned *p = (unsigned *)(o + (size_t)(tt + fr0) * 4);
+                if (nv == 4 && !((uintptr_t)p & 15)) {
+                    *(uint4 *)p = make_uint4(pk[0], pk[1], pk[2], pk[3]);
+                } else {
+#pragma unroll
+                    for (int r = 0; r < 4; ++r)
+                        if (r < nv) p[r] = pk[r];
+                }
             }
         }
     } else {

@@ -57,3 +57,6 @@ def test_roofline_inputs_from_committed_profiles():
     assert 3.0 < cpv < 6.0 and 1.5 < clk < 2.5 and valu > 0
     assert abs(cpv - ns * clk / valu) < 1e-9
     assert bench.pmc_traffic("c2", "no_such_kernel", fpl) == (None, None)
+    # the issue floor's cycles per VALU: the Kahan add chain of the committed latency probe
+    cfl, src = bench.fp64_issue_floor()
+    assert src == "r01_fp64_latency_probe.txt" and 3.5 < cfl < cpv

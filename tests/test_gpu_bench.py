@@ -88,7 +88,8 @@ def test_bench_line_fields():
     assert rf["bound"] == "fp64" and rf["unit"] == "TFLOP/s" and 0 < rf["frac"] < 1
     assert abs(rf["achieved"] - rf["flops_per_frame"] * rf["frames_per_launch"] / rf["avg_launch_ms"] / 1e9) \
         < 1e-9 * rf["achieved"]
-    assert rf["hbm"]["unit"] == "GB/s" and rf["issue_bound"]["frac"] > 0
+    assert rf["hbm"]["unit"] == "GB/s" and 0 < rf["issue_bound"]["frac"] <= 1.0
+    assert 0 < rf["chain_fp64"]["frac"] < 1
     assert d["e2e_host_buffers"]["value"] > 0
 
 

@@ -1,7 +1,9 @@
 #!/usr/bin/env python3
-"""Timeline of a rocprofv3 kernel trace (tools/trace_wl.sh): per bench step, the K1 launches' busy
-time, the gaps between consecutive K1s, the fill (first kernel -> first K1) and the drain (last K1
-end -> last kernel end)."""
+"""Timeline of a rocprofv3 kernel trace of one bench workload (tools/trace_wl.sh): the call of each
+bench step is one K1 (icw_iir_*) sequence, steps are split at K1 gaps > 0.5 ms.  Per step: the K1
+launches' busy time (sum K1), the gaps between consecutive K1s, the fill (the step's first kernel ->
+its first K1), the drain (its last K1 end -> its last kernel end) and the span (first kernel -> last
+kernel); ratio = span / sum K1.  -v lists every K1."""
 import csv
 import glob
 import sys
@@ -14,33 +16,40 @@ def main(d):
         for r in csv.DictReader(fh):
             rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"]))
     rows.sort()
-    # steps: split where the K1 sequence has a gap of > 5 ms (host work between steps)
     k1 = [r for r in rows if "icw_iir_" in r[2]]
-    groups, cur = [], [k1[0]]
+    steps, cur = [], [k1[0]]
     for r in k1[1:]:
-        if r[0] - cur[-1][1] > 5_000_000:
-            groups.append(cur)
+        if r[0] - cur[-1][1] > 500_000:
+            steps.append(cur)
             cur = []
         cur.append(r)
-    groups.append(cur)
-    for g in groups:
+    steps.append(cur)
+    bounds = [s[0][0] for s in steps] + [rows[-1][1] + 1]
+    prev_end = rows[0][0] - 1
+    for i, g in enumerate(steps):
         t0, t1 = g[0][0], g[-1][1]
-        ks = [r for r in rows if t0 - 20_000_000 < r[0] and r[1] < t1 + 20_000_000]
-        # the step's kernels: between the previous K1 group and the next one
+        # the step's kernels: after the previous step's last K1, before the next step's first K1
+        lo = steps[i - 1][-1][1] if i else rows[0][0] - 1
+        ks = [r for r in rows if r[0] > lo and r[0] < bounds[i + 1]]
+        ks_before = [r for r in ks if r[0] < t0 and r[0] > prev_end]
+        first = min([r[0] for r in ks if r[0] >= (ks_before[0][0] if ks_before else t0)] + [t0])
+        # drain: kernels that start after the last K1 began and before the next step's first kernel
+        nxt = bounds[i + 1]
+        after = [r for r in rows if r[0] >= g[-1][0] and r[0] < nxt and "icw_unpack" not in r[2] or
+                 (r[0] >= t1 and r[0] < nxt and "icw_advance" in r[2])]
+        last = max([r[1] for r in after if r[0] < nxt] + [t1])
         busy = sum(r[1] - r[0] for r in g)
-        gaps = [g[i + 1][0] - g[i][1] for i in range(len(g) - 1)]
-        pre = [r for r in ks if r[1] <= t0 and r[0] > t0 - 5_000_000]
-        post = [r for r in ks if r[0] >= t1 - 1 and r[0] < t1 + 5_000_000]
-        fill = (t0 - min(r[0] for r in pre)) / 1e6 if pre else 0.0
-        drain = (max(r[1] for r in post) - t1) / 1e6 if post else 0.0
-        print(f"K1 x{len(g)}: span {(t1 - t0) / 1e6:.3f} ms, busy {busy / 1e6:.3f}, gaps sum {sum(gaps) / 1e6:.3f} "
-              f"max {max(gaps or [0]) / 1e6:.3f}; fill {fill:.3f} ms; drain {drain:.3f} ms")
+        gaps = [g[j + 1][0] - g[j][1] for j in range(len(g) - 1)]
+        fill = (t0 - first) / 1e6
+        drain = (last - t1) / 1e6
+        span = (last - first) / 1e6
+        prev_end = last
+        print(f"step {i}: K1 x{len(g)} sum {busy / 1e6:.3f} ms, gaps {sum(gaps) / 1e6:.3f} ms "
+              f"(mean {sum(gaps) / max(1, len(gaps)) / 1e3:.1f} us), fill {fill:.3f} ms, drain {drain:.3f} ms, "
+              f"span {span:.3f} ms, span / sum K1 = {span / (busy / 1e6):.4f}")
         if "-v" in sys.argv:
-            for i, r in enumerate(g):
-                print(f"   K1[{i}] {(r[0] - t0) / 1e6:8.3f} .. {(r[1] - t0) / 1e6:8.3f}  ({(r[1] - r[0]) / 1e6:.3f})")
-            for r in ks:
-                if "icw_iir_" not in r[2]:
-                    print(f"   {r[2][:40]:40s} {(r[0] - t0) / 1e6:8.3f} .. {(r[1] - t0) / 1e6:8.3f}")
+            for j, r in enumerate(g):
+                print(f"   K1[{j}] {(r[0] - t0) / 1e6:8.3f} .. {(r[1] - t0) / 1e6:8.3f}  ({(r[1] - r[0]) / 1e6:.3f})")
 
 
 if __name__ == "__main__":
