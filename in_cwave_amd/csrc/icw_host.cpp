@@ -117,7 +117,12 @@ struct icw_ctx {
      * SIMD) made K1 +21 % slower even alone (C3, 4-wave workgroups), 3 per CU +27 % beside K2, and 1
      * per CU leaves the frame-parallel kernels too few CUs (C4 K2 2.57 -> 3.70 ms) */
     int k1_wpc = 2;
-    int k1_wg = 1;                        /* ICW_K1_WG: K1 waves per workgroup */
+    /* ICW_K1_WG: K1 waves per workgroup.  Default 1 for the lane kernel, 2 for the row kernel: its I and
+     * Q filter waves of the same streams then share a CU, so the second one reads the channel rows
+     * (one per channel since round 3) from the L2 / L1 the first one filled (C2 +0.7 %, C5 +0.4 %; the
+     * lane kernel loses 2-2.5 % on C3 / C4 with 2) */
+    int k1_wg = 1;
+    bool k1_wg_env = false;
     bool k1_lds = false;                  /* ICW_K1_LDS=1: K1 workgroups hold the CU's LDS (A/B) */
     bool fill_drain = true;               /* ICW_FILL_DRAIN=0: first K0 / last K2 stay partitioned (A/B) */
     uint32_t lds_cu = 0;                  /* LDS bytes per CU a workgroup may hold */
@@ -932,7 +937,7 @@ int icw_create(const icw_config *cfg, const icw_node *nodes, int n_nodes, int n_
             }
         }
         const char *wg = getenv("ICW_K1_WG");
-        if (wg && atoi(wg) >= 1 && atoi(wg) <= 4) c->k1_wg = atoi(wg);
+        if (wg && atoi(wg) >= 1 && atoi(wg) <= 4) { c->k1_wg = atoi(wg); c->k1_wg_env = true; }
     }
     rc = icw_stream_init(c, 0, n_streams);
     if (rc) { free_all(c); delete c; return rc; }
@@ -1540,7 +1545,7 @@ int icw_process_streams(icw_ctx *c, int first, int count, const void *in, size_t
         a1.t0 = blocks[b].first;
         a1.info_dup = c->info_dup[p];
         memcpy(a1.pc, c->pc, sizeof(a1.pc));
-        a1.wg_waves = c->k1_lds ? 4 : c->k1_wg;
+        a1.wg_waves = c->k1_lds ? 4 : (c->k1_wg_env || k1_mode != 3) ? c->k1_wg : 2;
         a1.lds_hold = c->k1_lds ? c->lds_cu : 0;
         a1.dedup = dedup ? 1 : 0;
         a1.fes = fcm ? ds.fes + f0 * 4 * ICW_FES_PITCH : nullptr;
