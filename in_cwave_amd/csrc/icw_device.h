@@ -286,6 +286,7 @@ struct IcwS1Args {
     IcwK1Args k1;
     IcwK2Args k2;
     IcwAdvArgs adv;
+    unsigned long long *stamps;    /* diagnostic: [4][2] phase-boundary stamps (null: none) */
 };
 
 #endif

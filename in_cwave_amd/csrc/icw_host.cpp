@@ -202,6 +202,7 @@ struct icw_ctx {
     int fir_par = 0;
     bool fir_fuse = true;                 /* ICW_FIR_FUSED=0: KF + K2 as two kernels (A/B) */
     bool stream1 = true;                  /* ICW_STREAM1=0: one-stream calls keep the four kernels (A/B) */
+    unsigned long long *s1_stamps = nullptr;   /* ICW_S1_STAMPS=1: K5 phase stamps, printed per call */
     std::mutex mu;
 };
 
@@ -681,7 +682,7 @@ bool fir_clear(icw_ctx *c, size_t f, size_t n, hipStream_t st)
 void free_all(icw_ctx *c)
 {
     DevState &s = c->st;
-    void *ptrs[] = {s.mt, s.mt_idx, s.rs, s.lr_equal, s.fes, s.err, s.hist, s.sncnt, s.hq_phase, s.pos, s.fade,
+    void *ptrs[] = {c->s1_stamps, s.mt, s.mt_idx, s.rs, s.lr_equal, s.fes, s.err, s.hist, s.sncnt, s.hq_phase, s.pos, s.fade,
                     s.n_frame, s.bus, s.clips, s.peak_bits, c->d_prog, c->trig, c->d_in, c->d_out, c->d_pre,
                     c->d_fir_g, c->fir_hist[0], c->fir_hist[1]};
     for (void *p : ptrs)
@@ -925,6 +926,8 @@ int icw_create(const icw_config *cfg, const icw_node *nodes, int n_nodes, int n_
         if (ff && !strcmp(ff, "0")) c->fir_fuse = false;
         const char *s1e = getenv("ICW_STREAM1");
         if (s1e && !strcmp(s1e, "0")) c->stream1 = false;
+        const char *s1s = getenv("ICW_S1_STAMPS");
+        if (s1s && !strcmp(s1s, "1") && dalloc(&c->s1_stamps, 8) != ICW_OK) c->s1_stamps = nullptr;
         const char *kl = getenv("ICW_K1_LDS");
         c->k1_lds = kl && !strcmp(kl, "1");
         {
@@ -1623,6 +1626,7 @@ int icw_process_streams(icw_ctx *c, int first, int count, const void *in, size_t
         a5.k1 = k1_args(0);
         a5.k2 = k2_args(0);
         a5.adv = adv_args();
+        a5.stamps = c->s1_stamps;
         if (timing && hipEventRecord(c->ev[0], st) != hipSuccess) return ICW_EDEVICE;
         if (icw_launch_stream1(&a5, N, st) != hipSuccess) return ICW_EDEVICE;
         if (timing && (hipEventRecord(c->ev[1], st) != hipSuccess || hipEventRecord(c->ev[2], st) != hipSuccess ||
@@ -1811,6 +1815,12 @@ int icw_process_streams(icw_ctx *c, int first, int count, const void *in, size_t
             if (hipMemcpy(&e, ds.err, sizeof(int), hipMemcpyDeviceToHost) != hipSuccess) return ICW_EDEVICE;
         }
         if (e) return ICW_EDEVICE;
+    }
+    if (s1 && c->s1_stamps) {
+        unsigned long long sp[8];
+        if (hipStreamSynchronize(st) == hipSuccess && hipMemcpy(sp, c->s1_stamps, sizeof(sp), hipMemcpyDeviceToHost) == hipSuccess)
+            fprintf(stderr, "icw_s1 %d %llu %llu %llu %llu %llu %llu\n", n_frames, sp[2] - sp[0], sp[3] - sp[1],
+                    sp[4] - sp[2], sp[5] - sp[3], sp[6] - sp[4], sp[7] - sp[5]);
     }
     if (timing) {
         if (hipStreamSynchronize(st) != hipSuccess) return ICW_EDEVICE;

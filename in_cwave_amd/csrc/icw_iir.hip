@@ -196,11 +196,28 @@ __device__ __forceinline__ bool icw_k1_chain(int gi, int count, bool dedup, int 
     return s < count;
 }
 
+/* XCD-aware order of one-wave workgroups: workgroup b goes to XCD b mod 8 (the dispatcher's round
+ * robin on MI355X), so the I and Q waves of a 128-lane group -- which read the same channel rows
+ * since K0 writes one row per channel -- are made workgroups 16c + j and 16c + j + 8: same XCD,
+ * and the second wave's reads hit the L2 the first one filled instead of fetching the rows again.
+ * Blocks past the last full 16 keep their order. */
+#ifndef ICW_K1_XCD_REMAP
+#define ICW_K1_XCD_REMAP 1              /* 0: blocks in order (A/B builds) */
+#endif
+__device__ __forceinline__ int icw_k1_block(int b, int nb, int tpb)
+{
+    if (!ICW_K1_XCD_REMAP || tpb != 64 || b >= (nb & ~15)) return b;
+    const int c = b >> 4, j = b & 15;
+    return ((c * 8 + (j & 7)) << 1) | (j >> 3);
+}
+
 template <int N, bool KAHAN, bool SUBN>
 __global__ __launch_bounds__(256) void icw_iir_state(IcwK1Args a)
 {
     int s, ch, f;
-    if (!icw_k1_chain(blockIdx.x * blockDim.x + threadIdx.x, a.n_streams, a.dedup != 0, s, ch, f)) return;
+    if (!icw_k1_chain(icw_k1_block(blockIdx.x, gridDim.x, blockDim.x) * blockDim.x + threadIdx.x, a.n_streams,
+                      a.dedup != 0, s, ch, f))
+        return;
     const int g = s * 4 + ch * 2 + f;
     const int n_chains = a.n_chains;
     double pc[20];

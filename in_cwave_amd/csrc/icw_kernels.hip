@@ -1125,12 +1125,25 @@ template <int N, bool TRIG>
 __global__ __launch_bounds__(ICW_K2_TILE) void icw_stream1(IcwS1Args a)
 {
     extern __shared__ __attribute__((aligned(16))) double lregs[];   /* K2's register file */
+    /* diagnostic build only (ICW_S1_STAMPS, tools/s1_phases.py): shader-clock and 100 MHz stamps at
+     * the phase boundaries */
+    unsigned long long *stp = a.stamps;
+    auto stamp = [&](int k) {
+        if (stp && threadIdx.x == 0) {
+            stp[2 * k] = __builtin_amdgcn_s_memtime();
+            stp[2 * k + 1] = __builtin_amdgcn_s_memrealtime();
+        }
+    };
+    stamp(0);
     for (int t = threadIdx.x; t < a.k0.T; t += ICW_K2_TILE) icw_unpack_frame(a.k0, t, 0);
     __syncthreads();
+    stamp(1);
     if (threadIdx.x < 128) icw_iir_row_body<N>(a.k1, threadIdx.x);
     __syncthreads();
+    stamp(2);
     icw_output_body<N, true, TRIG>(a.k2, 0, 0, lregs);
     __syncthreads();
+    stamp(3);
     if (threadIdx.x == 0) icw_advance_stream(a.adv, 0);
 }
 
