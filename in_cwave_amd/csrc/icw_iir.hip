@@ -196,13 +196,15 @@ __device__ __forceinline__ bool icw_k1_chain(int gi, int count, bool dedup, int 
     return s < count;
 }
 
-/* XCD-aware order of one-wave workgroups: workgroup b goes to XCD b mod 8 (the dispatcher's round
- * robin on MI355X), so the I and Q waves of a 128-lane group -- which read the same channel rows
- * since K0 writes one row per channel -- are made workgroups 16c + j and 16c + j + 8: same XCD,
- * and the second wave's reads hit the L2 the first one filled instead of fetching the rows again.
- * Blocks past the last full 16 keep their order. */
+/* XCD-aware order of one-wave workgroups (A/B build only: -DICW_K1_XCD_REMAP=1).  Workgroup b goes
+ * to XCD b mod 8 (the dispatcher's round robin on MI355X), so making the I and Q waves of a 128-lane
+ * group -- which read the same channel rows since K0 writes one row per channel -- workgroups
+ * 16c + j and 16c + j + 8 puts them on one XCD, and the second wave's reads hit the L2 the first one
+ * filled: C4's K1 fetch halves (FETCH_SIZE 16.1 -> 8.05 B/frame, the pipeline 121.6 -> 105.5 B/frame).
+ * It does not pay: K1 2.91 -> 2.99 ms per launch, C3 -1.6 %, C4 -2.3 % (two runs each, one box),
+ * the same direction as two-wave K1 workgroups (-2 to -2.5 %).  So the lane kernel keeps its order. */
 #ifndef ICW_K1_XCD_REMAP
-#define ICW_K1_XCD_REMAP 1              /* 0: blocks in order (A/B builds) */
+#define ICW_K1_XCD_REMAP 0
 #endif
 __device__ __forceinline__ int icw_k1_block(int b, int nb, int tpb)
 {
