@@ -136,6 +136,7 @@ struct IcwOp {
     int32_t tslot[2];              /* Shift / PM channel: column of the per-frame rotation table */
     int32_t wb_slot;               /* register form: the slot whose final value this op writes (its
                                       output goes to the persistent bus at a block's last frame), -1 */
+    int32_t chain_in;              /* chain program: bit 0 reads `in`, bit 1 the previous op's output */
 };
 
 /* A compiled DSP list.  Register form (frame-parallel output kernel): every slot read resolves at
@@ -150,6 +151,8 @@ struct IcwProg {
     int32_t needs_omega;           /* some Shift / PM node is active: the frame's norm_omega is used */
     int32_t n_trig;                /* active Shift / PM channels = columns of the rotation table */
     int32_t n_persist;             /* slots read before any write in the frame and never written */
+    int32_t chain;                 /* register form where every op reads only `in` and / or the op just
+                                      before it: values stay in registers (no LDS register file) */
     int32_t persist_reg[ICW_MAX_REGS], persist_slot[ICW_MAX_REGS];
     IcwOp ops[ICW_MAX_OPS];
 };
@@ -286,6 +289,8 @@ struct IcwS1Args {
     IcwK1Args k1;
     IcwK2Args k2;
     IcwAdvArgs adv;
+    IcwTrigArgs trig;              /* the block's rotation table (has_trig), computed beside the recurrence */
+    int32_t has_trig;
     unsigned long long *stamps;    /* diagnostic: [4][2] phase-boundary stamps (null: none) */
 };
 

@@ -202,6 +202,7 @@ struct icw_ctx {
     int fir_par = 0;
     bool fir_fuse = true;                 /* ICW_FIR_FUSED=0: KF + K2 as two kernels (A/B) */
     bool stream1 = true;                  /* ICW_STREAM1=0: one-stream calls keep the four kernels (A/B) */
+    bool chain_ok = true;                 /* ICW_CHAIN=0: chain programs keep the LDS register file (A/B) */
     unsigned long long *s1_stamps = nullptr;   /* ICW_S1_STAMPS=1: K5 phase stamps, printed per call */
     std::mutex mu;
 };
@@ -465,6 +466,19 @@ int compile_graph(const std::vector<icw_node> &nodes, int bypass, IcwProg &P)
         P.persist_slot[q] = persist_slot[q];
     }
     P.n_persist = (int)persist_val.size();
+    /* chain program (C2's Shift -> Master, C4's PM -> Shift -> Mix(in + B) -> Master): every op reads
+     * only `in` and / or the output of the op just before it.  Reads are in slot order and `in` is
+     * slot 0, so the sum is 0.0 + in + prev in the reference's order (adv_modulator.c:655-665) */
+    P.chain = P.n_persist == 0 ? 1 : 0;
+    for (int oi = 0; oi < n_ops && P.chain; ++oi) {
+        int bits = 0;
+        for (int v : reads[oi]) {
+            if (v == 0 && !(bits & 1) && !(bits & 2)) bits |= 1;
+            else if (oi > 0 && v == out_val[oi - 1] && v >= 0 && !(bits & 2)) bits |= 2;
+            else P.chain = 0;
+        }
+        P.ops[oi].chain_in = bits;
+    }
     set_needs_omega(P);
     return ICW_OK;
 }
@@ -924,6 +938,16 @@ int icw_create(const icw_config *cfg, const icw_node *nodes, int n_nodes, int n_
         if (fd && !strcmp(fd, "0")) c->fill_drain = false;
         const char *ff = getenv("ICW_FIR_FUSED");
         if (ff && !strcmp(ff, "0")) c->fir_fuse = false;
+        const char *che = getenv("ICW_CHAIN");
+        if (che && !strcmp(che, "0")) {
+            c->chain_ok = false;
+            c->prog.chain = 0;
+            if (hipMemcpy(c->d_prog, &c->prog, sizeof(IcwProg), hipMemcpyHostToDevice) != hipSuccess) {
+                free_all(c);
+                delete c;
+                return ICW_EDEVICE;
+            }
+        }
         const char *s1e = getenv("ICW_STREAM1");
         if (s1e && !strcmp(s1e, "0")) c->stream1 = false;
         const char *s1s = getenv("ICW_S1_STAMPS");
@@ -1148,6 +1172,7 @@ int icw_set_graph(icw_ctx *c, const icw_node *nodes, int n_nodes, int bypass_lis
     IcwProg P;
     int rc = build_prog(cfg, nv, P);
     if (rc) return rc;
+    if (!c->chain_ok) P.chain = 0;
     const bool serial = needs_serial(cfg, c->rk, P);
     if (serial && (rc = ensure_render_state(c))) return rc;
     if (hipMemcpy(c->d_prog, &P, sizeof(IcwProg), hipMemcpyHostToDevice) != hipSuccess) return ICW_EDEVICE;
@@ -1287,7 +1312,8 @@ int icw_process_streams(icw_ctx *c, int first, int count, const void *in, size_t
      * block scratch and has no recurrence to pipeline against, so its blocks are as long as the
      * scratch bound allows (fewer launches, fewer partly filled waves of workgroups at their ends) */
     const bool fir_fused = fir && c->fir_fuse &&
-                           icw_fir_graph_lds(c->fir_M, c->fir_nt, (int)nch, c->prog.n_regs) > 0 && !c->prog.is_bus;
+                           icw_fir_graph_lds(c->fir_M, c->fir_nt, (int)nch, c->prog.chain ? 0 : c->prog.n_regs) > 0 &&
+                           !c->prog.is_bus;
     /* The row kernel without a serial render (C2) has K2 at ~0.16 of K1r's time per frame: 65 536-frame
      * blocks (a quarter of the launches, of their gaps and prologues) ending in a steep tail
      * (65 536 -> 16 384 -> 4 096 -> 1 024: the drain stays one short K2) measured +0.8 % on C2
@@ -1582,7 +1608,7 @@ int icw_process_streams(icw_ctx *c, int first, int count, const void *in, size_t
             a2.pre_stride = (size_t)T * 2;
         }
         a2.do_render = c->serial_render ? 0 : 1;
-        a2.n_regs = c->prog.n_regs;
+        a2.n_regs = c->prog.chain ? 0 : c->prog.n_regs;    /* a chain program keeps its values in VGPRs */
         a2.clips = ds.clips + f0 * 2;
         a2.peak_bits = ds.peak_bits + f0 * 2;
         a2.rk = c->rk;
@@ -1627,6 +1653,25 @@ int icw_process_streams(icw_ctx *c, int first, int count, const void *in, size_t
         a5.k2 = k2_args(0);
         a5.adv = adv_args();
         a5.stamps = c->s1_stamps;
+        if (c->prog.needs_omega && c->prog.n_trig > 0 && !bus) {
+            /* the one stream's rotation factors, computed by the kernel's idle waves beside the
+             * recurrence: the output phase reads them instead of evaluating sin / cos per frame */
+            if (grow((void **)&c->trig, &c->trig_bytes, (size_t)n_frames * 2 * c->prog.n_trig * sizeof(double)))
+                return ICW_ENOMEM;
+            IcwTrigArgs &at = a5.trig;
+            at.prog = c->d_prog;
+            at.n_frame = ds.n_frame + f0;
+            at.t0 = 0;
+            at.T = n_frames;
+            at.scaled = cfg.frmod_scaled;
+            at.trig_pitch = 2 * c->prog.n_trig;
+            at.ssr = ssr;
+            at.sample_rate = cfg.sample_rate;
+            at.tab = c->trig;
+            a5.has_trig = 1;
+            a5.k2.trig_tab = c->trig;
+            a5.k2.trig_pitch = at.trig_pitch;
+        }
         if (timing && hipEventRecord(c->ev[0], st) != hipSuccess) return ICW_EDEVICE;
         if (icw_launch_stream1(&a5, N, st) != hipSuccess) return ICW_EDEVICE;
         if (timing && (hipEventRecord(c->ev[1], st) != hipSuccess || hipEventRecord(c->ev[2], st) != hipSuccess ||

@@ -100,6 +100,30 @@ __device__ __forceinline__ double icw_fade(long long ix, long long ns, long long
  *   I: {x, +0, -x, +0}   Q: {+0, -x, +0, x}.  K0 writes the nonzero values of both into one row per
  * channel; the recurrences supply the +0.0 (icw_iir_dev.h: icw_chain_x). */
 
+/* the fade and the signed filter-input row of one real frame (v: the unpacked L, R samples) */
+__device__ __forceinline__ void icw_store_frame(const IcwK0Args &a, int t, int s, double (&v)[2])
+{
+    const long long ix = a.pos[s] + a.t0 + t;
+    const double fd = icw_fade(ix, a.fade[s * 3 + 0], a.fade[s * 3 + 1], a.fade[s * 3 + 2]);
+    if (fd >= 0.0) {
+        v[0] *= fd;
+        v[1] *= fd;
+    }
+    /* one row per channel, s*2 + ch: the I filter's nonzero inputs sit at the even phases, the Q
+     * filter's at the odd ones, so the channel's signed sample {x, -x, -x, x}[k] serves both -- the
+     * I filter reads it where k is even (x, -x), the Q filter where k is odd (-x, x), and each takes
+     * the literal +0.0 at the other phases itself (icw_chain_x): 16 B per stereo frame, not 32 */
+    double *xs = a.xd + (size_t)s * 2 * a.x_pitch + t;
+    const int nchw = a.dedup ? 1 : 2;          /* mono dedup: K1 reads the left row only */
+#pragma unroll
+    for (int ch = 0; ch < 2; ++ch) {
+        if (ch < nchw) {
+            const unsigned k = (a.hq_phase[s * 2 + ch] + (unsigned)(a.t0 + t)) & 3u;
+            xs[(size_t)ch * a.x_pitch] = (k == 0u || k == 3u) ? v[ch] : -v[ch];
+        }
+    }
+}
+
 /* Input prep (K0): unpack + fade each frame once (xwave_unpack_csample, xwave_reader.c:908-1001)
  * and lay out the filter inputs of the quadrature mix of hq_rp_process (lpf_hilbert_quad.c:129-156):
  * the I filter {x, +0, -x, +0} and the Q filter {+0, -x, +0, x} by sample phase, both in one row
@@ -129,26 +153,8 @@ __device__ __forceinline__ void icw_unpack_frame(const IcwK0Args &a, int t, int 
     }
     double v[2];
     v[0] = icw_unpack(fp, a.fmt);
-    if (fd >= 0.0) v[0] *= fd;
-    if (a.nch > 1) {
-        v[1] = icw_unpack(fp + a.csz, a.fmt);
-        if (fd >= 0.0) v[1] *= fd;
-    } else {
-        v[1] = v[0];
-    }
-    /* one row per channel, s*2 + ch: the I filter's nonzero inputs sit at the even phases, the Q
-     * filter's at the odd ones, so the channel's signed sample {x, -x, -x, x}[k] serves both -- the
-     * I filter reads it where k is even (x, -x), the Q filter where k is odd (-x, x), and each takes
-     * the literal +0.0 at the other phases itself (icw_chain_x): 16 B per stereo frame, not 32 */
-    double *xs = a.xd + (size_t)s * 2 * a.x_pitch + t;
-    const int nchw = a.dedup ? 1 : 2;          /* mono dedup: K1 reads the left row only */
-#pragma unroll
-    for (int ch = 0; ch < 2; ++ch) {
-        if (ch < nchw) {
-            const unsigned k = (a.hq_phase[s * 2 + ch] + (unsigned)(a.t0 + t)) & 3u;
-            xs[(size_t)ch * a.x_pitch] = (k == 0u || k == 3u) ? v[ch] : -v[ch];
-        }
-    }
+    v[1] = a.nch > 1 ? icw_unpack(fp + a.csz, a.fmt) : v[0];
+    icw_store_frame(a, t, s, v);
 }
 
 __global__ __launch_bounds__(256) void icw_unpack_frames(IcwK0Args a)
@@ -628,13 +634,36 @@ __device__ __forceinline__ void icw_frame_graph(const IcwK2Args &a, const IcwPro
         const double omega = (TRIG && !use_tab) ? icw_omega(a.n_frame[s], a.t0 + t, a.scaled, a.ssr, a.sample_rate)
                                                 : 0.0;
         /* DSP list (adv_modulator.c:637-751) */
-        R.set(0, in);
         /* persistent bus at the block's last frame: slot 0 = in, then each written slot's
          * final value from the op that writes it (compile_graph: op.wb_slot) */
         const bool last = t == T - 1;
         double *bus_s = a.bus + (size_t)s * ICW_N_INPUTS * 4;
         if (last) { bus_s[0] = in.lre; bus_s[1] = in.lim; bus_s[2] = in.rre; bus_s[3] = in.rim; }
         double lOut = 0.0, rOut = 0.0;
+        if (P->chain) {
+            /* chain program: `in` and the previous op's output in registers, no register file */
+            IcwLR prev = in;
+            for (int oi = 0; oi < P->n_ops; ++oi) {
+                const IcwOp &op = P->ops[oi];
+                IcwLR d;
+                if (P->bypass) {
+                    d = in;
+                } else {
+                    d.lre = d.lim = d.rre = d.rim = 0.0;
+                    if (op.chain_in & 1) { d.lre += in.lre; d.lim += in.lim; d.rre += in.rre; d.rim += in.rim; }
+                    if (op.chain_in & 2) { d.lre += prev.lre; d.lim += prev.lim; d.rre += prev.rre; d.rim += prev.rim; }
+                }
+                IcwLR o;
+                if (icw_exec_op<TRIG, TAB>(op, d, omega, o, lOut, rOut, trow)) {
+                    prev = o;
+                    if (last && op.wb_slot >= 0) {
+                        double *b = bus_s + op.wb_slot * 4;
+                        b[0] = o.lre; b[1] = o.lim; b[2] = o.rre; b[3] = o.rim;
+                    }
+                }
+            }
+        } else {
+        R.set(0, in);
         for (int oi = 0; oi < P->n_ops; ++oi) {
             const IcwOp &op = P->ops[oi];
             IcwLR d;
@@ -657,6 +686,7 @@ __device__ __forceinline__ void icw_frame_graph(const IcwK2Args &a, const IcwPro
                 }
             }
         }
+        }   /* register file */
 
         if (a.pre) {
             double *p = a.pre + (size_t)s * a.pre_stride + (size_t)t * 2;
@@ -1019,10 +1049,8 @@ __global__ __launch_bounds__(256, 4) void icw_fir_graph(IcwFirArgs f, IcwK2Args 
  * counter, which all streams of a batch share while they are in step (same call-start counter).
  * One thread per frame evaluates each active channel's factor once (icw_trig, the same code as
  * the inline path); K2 reads the row instead of running fmod / sin / sincos per stream. */
-__global__ __launch_bounds__(256) void icw_trig_table(IcwTrigArgs a)
+__device__ __forceinline__ void icw_trig_row(const IcwTrigArgs &a, int t)
 {
-    const int t = blockIdx.x * 256 + threadIdx.x;
-    if (t >= a.T) return;
     const IcwProg *P = a.prog;
     const double omega = icw_omega(a.n_frame[0], a.t0 + t, a.scaled, a.ssr, a.sample_rate);
     double *row = a.tab + (size_t)t * a.trig_pitch;
@@ -1037,6 +1065,12 @@ __global__ __launch_bounds__(256) void icw_trig_table(IcwTrigArgs a)
             row[op.tslot[c] * 2 + 1] = sn;
         }
     }
+}
+
+__global__ __launch_bounds__(256) void icw_trig_table(IcwTrigArgs a)
+{
+    const int t = blockIdx.x * 256 + threadIdx.x;
+    if (t < a.T) icw_trig_row(a, t);
 }
 
 /* ------------------------------------------------------- serial graph kernel (K4) ------ */
@@ -1135,10 +1169,35 @@ __global__ __launch_bounds__(ICW_K2_TILE) void icw_stream1(IcwS1Args a)
         }
     };
     stamp(0);
-    for (int t = threadIdx.x; t < a.k0.T; t += ICW_K2_TILE) icw_unpack_frame(a.k0, t, 0);
+    /* K0: all the block's loads first (the zero-copy input is read across PCIe: one round trip per
+     * pass instead of one per frame -- a frame's stores could alias the next frame's loads), then the
+     * fades and the stores */
+    const IcwK0Args &a0 = a.k0;
+    const bool mono = a0.nch == 1;
+    for (int t0 = 0; t0 < a0.T; t0 += 4 * ICW_K2_TILE) {
+        double v[4][2];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int t = t0 + k * ICW_K2_TILE + (int)threadIdx.x;
+            if (t < a0.T) {
+                const unsigned char *fp = a0.in + (size_t)t * a0.fsz;
+                v[k][0] = icw_unpack(fp, a0.fmt);
+                v[k][1] = mono ? v[k][0] : icw_unpack(fp + a0.csz, a0.fmt);
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int t = t0 + k * ICW_K2_TILE + (int)threadIdx.x;
+            if (t < a0.T) icw_store_frame(a0, t, 0, v[k]);
+        }
+    }
     __syncthreads();
     stamp(1);
+    /* waves 0-1 (SIMDs 0, 1): the recurrence; waves 2-3 (SIMDs 2, 3), idle otherwise: the block's
+     * Shift / PM rotation factors, which depend only on the frame counter, for the output phase */
     if (threadIdx.x < 128) icw_iir_row_body<N>(a.k1, threadIdx.x);
+    else if (a.has_trig)
+        for (int t = (int)threadIdx.x - 128; t < a.trig.T; t += 128) icw_trig_row(a.trig, t);
     __syncthreads();
     stamp(2);
     icw_output_body<N, true, TRIG>(a.k2, 0, 0, lregs);
