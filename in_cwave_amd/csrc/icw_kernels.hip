@@ -198,6 +198,13 @@ __device__ __forceinline__ void icw_fir_stage(const IcwFirArgs &f, int s, int ch
     const bool mono = f.nch == 1;
     const int nl = sh + M + nout + 24;               /* logical extent: pad, history, tile, margin */
     const int nf = min(nout, T - tt);
+    /* uniform over the tile: no fade anywhere in the frames it stages (icw_fade returns "none" for
+     * fi <= ix <= ns - fo and for ix >= ns), and whether any staged frame precedes the block (the
+     * history).  The fade's two FP64 divisions and the history loads were computed for every input
+     * and made the staging ~half of the kernel's VALU instructions (r03_c2fir_sq.json). */
+    const long long ja = max(tt - M, 0), jb = (long long)tt + nf - 1;
+    const bool nofade = p0 + ja >= fi && (p0 + jb <= ns - fo || p0 + ja >= ns);
+    const bool need_hist = tt < M + sh;
     /* 8 consecutive inputs per thread and pass, their loads issued together (clamped in range,
      * selected after): the staging is load-latency bound otherwise */
     constexpr int V = 8;
@@ -208,7 +215,11 @@ __device__ __forceinline__ void icw_fir_stage(const IcwFirArgs &f, int s, int ch
             const int j = tt - M + i0 + e - sh;
             const int jr = min(max(j, 0), T - 1);
             raw[e] = icw_unpack(src + (size_t)jr * f.fsz, f.fmt);
-            his[e] = hin[min(max(M + j, 0), M - 1)];
+            his[e] = 0.0;
+        }
+        if (need_hist) {
+#pragma unroll
+            for (int e = 0; e < V; ++e) his[e] = hin[min(max(M + tt - M + i0 + e - sh, 0), M - 1)];
         }
 #pragma unroll
         for (int e = 0; e < V; ++e) {
@@ -220,8 +231,10 @@ __device__ __forceinline__ void icw_fir_stage(const IcwFirArgs &f, int s, int ch
                     v = his[e];
                 } else {
                     v = raw[e];
-                    const double fd = icw_fade(p0 + j, ns, fi, fo);
-                    if (fd >= 0.0) v *= fd;
+                    if (!nofade) {
+                        const double fd = icw_fade(p0 + j, ns, fi, fo);
+                        if (fd >= 0.0) v *= fd;
+                    }
                 }
                 if (j >= T - M && (j >= tt || tt == 0)) {
                     hout[j - (T - M)] = v;
