@@ -85,6 +85,43 @@ __device__ __forceinline__ void icw_unpack_iq(const unsigned char *p, uint32_t f
     }
 }
 
+/* one sample of format FMT; AL: the address is aligned to the sample's size, so one typed load
+ * replaces the byte loads and their shifts */
+template <int FMT, bool AL>
+__device__ __forceinline__ double icw_unpack_f(const unsigned char *p)
+{
+    if constexpr (AL && FMT == ICW_FMT_I16) return (double)*(const short *)p;
+    else if constexpr (AL && FMT == ICW_FMT_I32) return ((double)*(const int *)p) / 65536.0;
+    else if constexpr (AL && FMT == ICW_FMT_F32) return 32768.0 * (double)*(const float *)p;
+    else return icw_unpack(p, FMT);
+}
+
+template <int V> struct icw_ic { static constexpr int value = V; };
+
+/* calls f(icw_ic<FMT>, icw_ic<AL>) for a uniform real format: the unpack specialised once per
+ * workgroup instead of a format switch per sample.  al: the OR of the base address and the strides
+ * the samples are read at (aligned when its low bits below the sample size are clear) */
+template <typename F>
+__device__ __forceinline__ void icw_fmt_dispatch(uint32_t fmt, uintptr_t al, F &&f)
+{
+    switch (fmt) {
+    case ICW_FMT_I16:
+        if (al & 1) f(icw_ic<ICW_FMT_I16>(), icw_ic<0>());
+        else f(icw_ic<ICW_FMT_I16>(), icw_ic<1>());
+        break;
+    case ICW_FMT_U8: f(icw_ic<ICW_FMT_U8>(), icw_ic<0>()); break;
+    case ICW_FMT_I24: f(icw_ic<ICW_FMT_I24>(), icw_ic<0>()); break;
+    case ICW_FMT_I32:
+        if (al & 3) f(icw_ic<ICW_FMT_I32>(), icw_ic<0>());
+        else f(icw_ic<ICW_FMT_I32>(), icw_ic<1>());
+        break;
+    default:
+        if (al & 3) f(icw_ic<ICW_FMT_F32>(), icw_ic<0>());
+        else f(icw_ic<ICW_FMT_F32>(), icw_ic<1>());
+        break;
+    }
+}
+
 /* fade factor of xwave_unpack_csample (xwave_reader.c:918-936); < 0 means "no fade" */
 __device__ __forceinline__ double icw_fade(long long ix, long long ns, long long fi, long long fo)
 {
@@ -151,10 +188,15 @@ __device__ __forceinline__ void icw_unpack_frame(const IcwK0Args &a, int t, int 
         for (int i = 0; i < 4; ++i) xs[(size_t)i * a.x_pitch] = q[i];
         return;
     }
-    double v[2];
-    v[0] = icw_unpack(fp, a.fmt);
-    v[1] = a.nch > 1 ? icw_unpack(fp + a.csz, a.fmt) : v[0];
-    icw_store_frame(a, t, s, v);
+    const uintptr_t al = (uintptr_t)(a.in + (size_t)s * a.in_stride) | (uintptr_t)a.fsz;
+    icw_fmt_dispatch(a.fmt, al, [&](auto fc, auto ac) {
+        constexpr int F = decltype(fc)::value;
+        constexpr bool AL = decltype(ac)::value != 0;
+        double v[2];
+        v[0] = icw_unpack_f<F, AL>(fp);
+        v[1] = a.nch > 1 ? icw_unpack_f<F, AL>(fp + a.csz) : v[0];
+        icw_store_frame(a, t, s, v);
+    });
 }
 
 __global__ __launch_bounds__(256) void icw_unpack_frames(IcwK0Args a)
@@ -183,18 +225,20 @@ __global__ __launch_bounds__(256) void icw_unpack_frames(IcwK0Args a)
 __device__ __forceinline__ int icw_fir_phys(int i) { return i + (i >> 3); }
 
 
-/* inputs of channel ch for the outputs [tt, tt + nout) of a launch block, at logical index
- * i <-> frame j = tt - M + i - sh (zero outside [-M, T)); the history after the block is written by
- * the tile that owns each of its frames */
-__device__ __forceinline__ void icw_fir_stage(const IcwFirArgs &f, int s, int ch, double *xs, int tt, int nout,
-                                              int sh, int tid, int nthr)
+/* inputs of NC channels from ch0 for the outputs [tt, tt + nout) of a launch block, at logical
+ * index i <-> frame j = tt - M + i - sh (zero outside [-M, T)), channel k at xs + k * px; the
+ * history after the block is written by the tile that owns each of its frames.  The stereo form
+ * computes a frame's address, validity and fade once for both channels. */
+template <int FMT, bool AL, int NC>
+__device__ __forceinline__ void icw_fir_stage_t(const IcwFirArgs &f, int s, int ch0, double *xs, int px, int tt,
+                                                int nout, int sh, int tid, int nthr)
 {
     const int T = f.T, M = f.M;
-    const unsigned char *src = f.in + (size_t)s * f.in_stride + (size_t)ch * f.csz;
+    const unsigned char *src = f.in + (size_t)s * f.in_stride + (size_t)ch0 * f.csz;
     const long long p0 = f.pos[s] + f.t0;
     const long long ns = f.fade[s * 3 + 0], fi = f.fade[s * 3 + 1], fo = f.fade[s * 3 + 2];
-    const double *hin = f.hist_in + ((size_t)s * 2 + ch) * M;
-    double *hout = f.hist_out + ((size_t)s * 2 + ch) * M;
+    const double *hin = f.hist_in + ((size_t)s * 2 + ch0) * M;
+    double *hout = f.hist_out + ((size_t)s * 2 + ch0) * M;
     const bool mono = f.nch == 1;
     const int nl = sh + M + nout + 24;               /* logical extent: pad, history, tile, margin */
     const int nf = min(nout, T - tt);
@@ -205,45 +249,76 @@ __device__ __forceinline__ void icw_fir_stage(const IcwFirArgs &f, int s, int ch
     const long long ja = max(tt - M, 0), jb = (long long)tt + nf - 1;
     const bool nofade = p0 + ja >= fi && (p0 + jb <= ns - fo || p0 + ja >= ns);
     const bool need_hist = tt < M + sh;
-    /* 8 consecutive inputs per thread and pass, their loads issued together (clamped in range,
+    /* 8 consecutive frames per thread and pass, their loads issued together (clamped in range,
      * selected after): the staging is load-latency bound otherwise */
     constexpr int V = 8;
     for (int i0 = tid * V; i0 < nl; i0 += nthr * V) {
-        double raw[V], his[V];
+        double raw[NC][V], his[NC][V];
 #pragma unroll
         for (int e = 0; e < V; ++e) {
             const int j = tt - M + i0 + e - sh;
             const int jr = min(max(j, 0), T - 1);
-            raw[e] = icw_unpack(src + (size_t)jr * f.fsz, f.fmt);
-            his[e] = 0.0;
+            const unsigned char *p = src + (size_t)jr * f.fsz;
+#pragma unroll
+            for (int k = 0; k < NC; ++k) {
+                raw[k][e] = icw_unpack_f<FMT, AL>(p + k * f.csz);
+                his[k][e] = 0.0;
+            }
         }
         if (need_hist) {
 #pragma unroll
-            for (int e = 0; e < V; ++e) his[e] = hin[min(max(M + tt - M + i0 + e - sh, 0), M - 1)];
+            for (int e = 0; e < V; ++e) {
+                const int h = min(max(tt + i0 + e - sh, 0), M - 1);
+#pragma unroll
+                for (int k = 0; k < NC; ++k) his[k][e] = hin[k * M + h];
+            }
         }
 #pragma unroll
         for (int e = 0; e < V; ++e) {
             const int i = i0 + e;
             const int j = tt - M + i - sh;
-            double v = 0.0;
+            double v[NC];
+#pragma unroll
+            for (int k = 0; k < NC; ++k) v[k] = 0.0;
             if (i >= sh && j < tt + nf) {
                 if (j < 0) {
-                    v = his[e];
+#pragma unroll
+                    for (int k = 0; k < NC; ++k) v[k] = his[k][e];
                 } else {
-                    v = raw[e];
+#pragma unroll
+                    for (int k = 0; k < NC; ++k) v[k] = raw[k][e];
                     if (!nofade) {
                         const double fd = icw_fade(p0 + j, ns, fi, fo);
-                        if (fd >= 0.0) v *= fd;
+                        if (fd >= 0.0) {
+#pragma unroll
+                            for (int k = 0; k < NC; ++k) v[k] *= fd;
+                        }
                     }
                 }
                 if (j >= T - M && (j >= tt || tt == 0)) {
-                    hout[j - (T - M)] = v;
-                    if (mono) hout[M + j - (T - M)] = v;
+#pragma unroll
+                    for (int k = 0; k < NC; ++k) hout[k * M + j - (T - M)] = v[k];
+                    if (NC == 1 && mono) hout[M + j - (T - M)] = v[0];
                 }
             }
-            if (i < nl) xs[icw_fir_phys(i)] = v;
+            if (i < nl) {
+#pragma unroll
+                for (int k = 0; k < NC; ++k) xs[k * px + icw_fir_phys(i)] = v[k];
+            }
         }
     }
+}
+
+/* the staging of NC channels, its format and alignment resolved once (uniform) per workgroup */
+template <int NC>
+__device__ __forceinline__ void icw_fir_stage(const IcwFirArgs &f, int s, int ch0, double *xs, int px, int tt,
+                                              int nout, int sh, int tid, int nthr)
+{
+    const uintptr_t al = (uintptr_t)(f.in + (size_t)s * f.in_stride) | (uintptr_t)f.fsz;
+    icw_fmt_dispatch(f.fmt, al, [&](auto fc, auto ac) {
+        icw_fir_stage_t<decltype(fc)::value, decltype(ac)::value != 0, NC>(f, s, ch0, xs, px, tt, nout, sh, tid,
+                                                                           nthr);
+    });
 }
 
 /* The taps through the constant address space: every lane of a wave reads the same tap, so they
@@ -317,7 +392,7 @@ __global__ __launch_bounds__(256) void icw_fir_hilbert(IcwFirArgs a)
     const int sh = (8 - ((c - 1) & 7)) & 7;          /* c - 1 + sh = 8 a */
     const int av = (c - 1 + sh) >> 3;
     const int nf = min(TF, a.T - tt);
-    icw_fir_stage(a, s, ch, xs, tt, TF, sh, threadIdx.x, 256);
+    icw_fir_stage<1>(a, s, ch, xs, 0, tt, TF, sh, threadIdx.x, 256);
     const int px = icw_fir_phys(sh + M + TF + 24) + 1;
     double *qs = xs + px + ((a.nt + 1) & ~1);
     icw_ctap *gs = (icw_ctap *)a.g;
@@ -957,7 +1032,8 @@ __global__ __launch_bounds__(256, 4) void icw_fir_graph(IcwFirArgs f, IcwK2Args 
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const int ch = nchc == 2 ? lane >> 5 : 0;
     const int ll = nchc == 2 ? wv * 32 + (lane & 31) : threadIdx.x;   /* lane index within the channel */
-    for (int k = 0; k < nchc; ++k) icw_fir_stage(f, s, k, lds + k * px, tt, TF, sh, threadIdx.x, 256);
+    if (nchc == 2) icw_fir_stage<2>(f, s, 0, lds, px, tt, TF, sh, threadIdx.x, 256);
+    else icw_fir_stage<1>(f, s, 0, lds, px, tt, TF, sh, threadIdx.x, 256);
     __syncthreads();
     double q[ICW_FIR_R], vi[ICW_FIR_R];
     icw_fir_sums(lds + ch * px, gs, f.nt, ll, av, sh, c, q);
@@ -1187,23 +1263,27 @@ __global__ __launch_bounds__(ICW_K2_TILE) void icw_stream1(IcwS1Args a)
      * fades and the stores */
     const IcwK0Args &a0 = a.k0;
     const bool mono = a0.nch == 1;
-    for (int t0 = 0; t0 < a0.T; t0 += 4 * ICW_K2_TILE) {
-        double v[4][2];
+    icw_fmt_dispatch(a0.fmt, (uintptr_t)a0.in | (uintptr_t)a0.fsz, [&](auto fc, auto ac) {
+        constexpr int F = decltype(fc)::value;
+        constexpr bool AL = decltype(ac)::value != 0;
+        for (int t0 = 0; t0 < a0.T; t0 += 4 * ICW_K2_TILE) {
+            double v[4][2];
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const int t = t0 + k * ICW_K2_TILE + (int)threadIdx.x;
-            if (t < a0.T) {
-                const unsigned char *fp = a0.in + (size_t)t * a0.fsz;
-                v[k][0] = icw_unpack(fp, a0.fmt);
-                v[k][1] = mono ? v[k][0] : icw_unpack(fp + a0.csz, a0.fmt);
+            for (int k = 0; k < 4; ++k) {
+                const int t = t0 + k * ICW_K2_TILE + (int)threadIdx.x;
+                if (t < a0.T) {
+                    const unsigned char *fp = a0.in + (size_t)t * a0.fsz;
+                    v[k][0] = icw_unpack_f<F, AL>(fp);
+                    v[k][1] = mono ? v[k][0] : icw_unpack_f<F, AL>(fp + a0.csz);
+                }
+            }
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const int t = t0 + k * ICW_K2_TILE + (int)threadIdx.x;
+                if (t < a0.T) icw_store_frame(a0, t, 0, v[k]);
             }
         }
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const int t = t0 + k * ICW_K2_TILE + (int)threadIdx.x;
-            if (t < a0.T) icw_store_frame(a0, t, 0, v[k]);
-        }
-    }
+    });
     __syncthreads();
     stamp(1);
     /* waves 0-1 (SIMDs 0, 1): the recurrence; waves 2-3 (SIMDs 2, 3), idle otherwise: the block's
