@@ -75,6 +75,8 @@ struct IcwAdvArgs {
     int32_t scaled;
     const int *err;                /* with err_copy: the hand-off flag is copied next to the output, */
     int *err_copy;                 /* so a small host-pointer call reads both with one copy */
+    uint32_t *done;                /* K5 zero-copy call: `seq` stored here (host memory, system scope) */
+    uint32_t seq;                  /* after the output and the flag, so the host can poll for it */
 };
 
 /* Arguments of the serial graph kernel (bus form; one lane = one stream, loops over frames). */

@@ -157,6 +157,8 @@ struct icw_ctx {
     /* ICW_ZEROCOPY=0: small calls copy the staging buffer to and from HBM instead of the kernels
      * reading the input from, and writing the output to, the pinned buffer directly */
     bool zero_copy = true;
+    bool spin_wait = true;                /* ICW_SPIN=0: K5 zero-copy calls wait on the stream instead */
+    uint32_t s1_seq = 0;                  /* K5 completion sequence number (host-polled) */
     /* the serial render (K4 bus-form graph + K3b) runs on a fourth stream, one block behind K2:
      * its inputs are double-buffered like the block scratch */
     hipStream_t stream4 = nullptr;
@@ -620,6 +622,21 @@ bool host_pinned(const void *p)
     return a.type == hipMemoryTypeHost;
 }
 
+/* wait for a K5 call's sequence number in host memory; the stream is queried now and then, so a
+ * failed launch or a device fault ends the wait with an error instead of a hang */
+bool poll_done(const uint32_t *flag, uint32_t seq, hipStream_t st)
+{
+    for (unsigned it = 1;; ++it) {
+        if (__atomic_load_n(flag, __ATOMIC_ACQUIRE) == seq) return true;
+        if ((it & 255u) == 0u) {
+            const hipError_t q = hipStreamQuery(st);
+            if (q == hipSuccess) return __atomic_load_n(flag, __ATOMIC_ACQUIRE) == seq;
+            if (q != hipErrorNotReady) return false;
+        }
+        __builtin_ia32_pause();
+    }
+}
+
 hipError_t quiesce(icw_ctx *c)
 {
     (void)c;
@@ -926,6 +943,8 @@ int icw_create(const icw_config *cfg, const icw_node *nodes, int n_nodes, int n_
         if (ns && atoi(ns) >= 2 && atoi(ns) <= kSets) c->max_sets = atoi(ns);
         const char *zc = getenv("ICW_ZEROCOPY");
         if (zc && !strcmp(zc, "0")) c->zero_copy = false;
+        const char *sw = getenv("ICW_SPIN");
+        if (sw && !strcmp(sw, "0")) c->spin_wait = false;
         const char *fb = getenv("ICW_FIRST_BLOCK");
         if (fb && atoi(fb) >= 0) c->first_block = atoi(fb);
         const char *tp = getenv("ICW_TAPER");
@@ -1377,6 +1396,12 @@ int icw_process_streams(icw_ctx *c, int first, int count, const void *in, size_t
         d_in = zcopy ? c->h_stage_dev : c->d_in;
         d_out = zcopy ? c->h_stage_dev + stage_in : c->d_out;
     }
+    /* K5 on the zero-copy buffer: the kernel stores the call's sequence number after its output and
+     * the host polls for it -- no completion signal and no waking of a waiting thread.  The word is
+     * 4-byte aligned inside the output's 16 spare bytes, after the error flag. */
+    const bool s1_poll = s1 && zcopy && c->spin_wait && !timing && !c->s1_stamps;
+    const size_t done_off = ((stage_in + dos * S + sizeof(int) + 3) & ~(size_t)3) - stage_in;
+    const uint32_t s1_seq = s1_poll ? ++c->s1_seq : 0u;
     double *d_pre = nullptr;
     if (flags & ICW_F_DEBUG_PRE) {
         if (!dbg) return ICW_EINVAL;
@@ -1641,6 +1666,10 @@ int icw_process_streams(icw_ctx *c, int first, int count, const void *in, size_t
             av.err = ds.err;
             av.err_copy = (int *)(d_out + dos * S);        /* the output buffer has 16 spare bytes */
         }
+        if (s1_poll) {
+            av.done = (uint32_t *)(d_out + done_off);
+            av.seq = s1_seq;
+        }
         return av;
     };
     /* K5: a one-stream call of one block (the drop-in's 576-frame calls, playback.c:619) runs its four
@@ -1852,7 +1881,9 @@ int icw_process_streams(icw_ctx *c, int first, int count, const void *in, size_t
             return ICW_EDEVICE;
         int e = 0;
         if (pinned) {
-            if (hipStreamSynchronize(st) != hipSuccess) return ICW_EDEVICE;
+            if (s1_poll ? !poll_done((const uint32_t *)(h_out + done_off), s1_seq, st)
+                        : hipStreamSynchronize(st) != hipSuccess)
+                return ICW_EDEVICE;
             memcpy(&e, h_out + dos * S, sizeof(int));     /* the flag icw_advance copied */
             for (size_t i = 0; i < S; ++i) memcpy((unsigned char *)out + i * out_stride, h_out + i * dos, dos);
         } else {

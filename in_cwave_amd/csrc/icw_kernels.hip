@@ -1296,7 +1296,15 @@ __global__ __launch_bounds__(ICW_K2_TILE) void icw_stream1(IcwS1Args a)
     icw_output_body<N, true, TRIG>(a.k2, 0, 0, lregs);
     __syncthreads();
     stamp(3);
-    if (threadIdx.x == 0) icw_advance_stream(a.adv, 0);
+    if (threadIdx.x == 0) {
+        icw_advance_stream(a.adv, 0);
+        if (a.adv.done) {
+            /* the workgroup's output stores are in L2 (the barrier's release); write them and the
+             * flag back to host memory, then the call's sequence number the host polls for */
+            __threadfence_system();
+            __hip_atomic_store(a.adv.done, a.adv.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+    }
 }
 
 /* ------------------------------------------------------ serial render kernel (K3) ------ */

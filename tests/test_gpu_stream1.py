@@ -88,3 +88,29 @@ def test_stream1_drop_in_boundary(oracle, icw):
         ro, _ = ref.process(blk, 576)
         assert np.array_equal(buf, ro), b
     lib.icw_mod_context_destroy(mc)
+
+
+@pytest.mark.parametrize("fmt,ch,b24", [(abi.FMT_I24, 1, True), (abi.FMT_I16, 2, False), (abi.FMT_U8, 1, False)])
+@pytest.mark.parametrize("spin", ["1", "0"])
+def test_stream1_polled_completion(oracle, icw, fmt, ch, b24, spin, monkeypatch):
+    """zero-copy calls (no pre-render doubles requested): the host polls for the sequence number K5
+    stores after the output and the error flag (ICW_SPIN=0: a stream wait instead).  Odd block
+    lengths and frame sizes put the word at every offset of the staging buffer"""
+    monkeypatch.setenv("ICW_SPIN", spin)
+    monkeypatch.setenv("ICW_STREAM1", "1")
+    monkeypatch.setenv("ICW_K1_MODE", "row")
+    cfg = graph.default_config(44100, fmt=fmt, channels=ch, need24bits=b24)
+    nodes = graph.graph_shift_master()
+    ctx = icw.Context(cfg, nodes, 1)
+    ref = oracle.Stream(cfg, nodes)
+    lens = [576, 1, 3, 577, 2, 4096, 575, 576, 576]
+    raw = synth.batch_pcm(1, sum(lens), cfg.sample_rate, channels=ch, fmt=fmt, first=11)
+    t = 0
+    for n in lens:
+        seg = np.ascontiguousarray(raw[:, t * ctx.fsz:(t + n) * ctx.fsz])
+        out, _ = ctx.process(seg, n)
+        ro, _ = ref.process(seg[0], n)
+        assert np.array_equal(out[0], ro), (n, t)
+        t += n
+    assert ctx.n_frame(0) == ref.n_frame()
+    ctx.close()
