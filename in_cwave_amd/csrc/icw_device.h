@@ -294,6 +294,10 @@ struct IcwS1Args {
     IcwTrigArgs trig;              /* the block's rotation table (has_trig), computed beside the recurrence */
     int32_t has_trig;
     unsigned long long *stamps;    /* diagnostic: [4][2] phase-boundary stamps (null: none) */
+    int32_t ovl;                   /* request (host) / set (launcher): output phase beside the recurrence */
+    int32_t rows_off;              /* ovl: the w rows' offset in dynamic LDS (doubles, after K2's registers) */
+    int32_t lpitch;                /* ovl: doubles per w row in LDS (T + N + 1, even) */
 };
+#define ICW_S1_OVL_LDS (128 * 1024)   /* ovl: dynamic LDS budget (register file + w rows) */
 
 #endif

@@ -204,6 +204,7 @@ struct icw_ctx {
     int fir_par = 0;
     bool fir_fuse = true;                 /* ICW_FIR_FUSED=0: KF + K2 as two kernels (A/B) */
     bool stream1 = true;                  /* ICW_STREAM1=0: one-stream calls keep the four kernels (A/B) */
+    bool s1_ovl = true;                   /* ICW_S1_OVL=0: K5's output phase after the recurrence (A/B) */
     bool chain_ok = true;                 /* ICW_CHAIN=0: chain programs keep the LDS register file (A/B) */
     unsigned long long *s1_stamps = nullptr;   /* ICW_S1_STAMPS=1: K5 phase stamps, printed per call */
     std::mutex mu;
@@ -969,6 +970,8 @@ int icw_create(const icw_config *cfg, const icw_node *nodes, int n_nodes, int n_
         }
         const char *s1e = getenv("ICW_STREAM1");
         if (s1e && !strcmp(s1e, "0")) c->stream1 = false;
+        const char *s1o = getenv("ICW_S1_OVL");
+        if (s1o && !strcmp(s1o, "0")) c->s1_ovl = false;
         const char *s1s = getenv("ICW_S1_STAMPS");
         if (s1s && !strcmp(s1s, "1") && dalloc(&c->s1_stamps, 8) != ICW_OK) c->s1_stamps = nullptr;
         const char *kl = getenv("ICW_K1_LDS");
@@ -1682,6 +1685,7 @@ int icw_process_streams(icw_ctx *c, int first, int count, const void *in, size_t
         a5.k2 = k2_args(0);
         a5.adv = adv_args();
         a5.stamps = c->s1_stamps;
+        a5.ovl = c->s1_ovl ? 1 : 0;
         if (c->prog.needs_omega && c->prog.n_trig > 0 && !bus) {
             /* the one stream's rotation factors, computed by the kernel's idle waves beside the
              * recurrence: the output phase reads them instead of evaluating sin / cos per frame */

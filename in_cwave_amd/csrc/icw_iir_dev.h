@@ -269,8 +269,23 @@ __device__ __forceinline__ void icw_row_restart(double (&W)[N], double (&P)[N], 
  * slot = 2 stream + channel (stream, left channel under the dedup).  The two channels of a
  * stream are rows r, r ^ 1 of one wave; a wave's chains share a filter kind, hence the
  * zero-input parity whenever their Hilbert phases agree in parity. */
-template <int N>
-__device__ __forceinline__ void icw_iir_row_body(const IcwK1Args &a, int gl)
+/* PUB (K5's overlapped form, one stream): the w rows go to the LDS rows lw (chain c = ch*2 + f at
+ * lw + c * lpitch) instead of a.w, and lane 0 of each wave publishes in prog[f] how many of the
+ * block's frames have final rows, after each checked block: the output waves poll it and take
+ * those frames while the recurrence runs on.  One wave's LDS operations are performed in issue
+ * order, so a reader that sees the count also sees the rows stored before it. */
+template <bool PUB>
+__device__ __forceinline__ void icw_row_publish(int *prog, int gl, int f, int done)
+{
+    if constexpr (PUB) {
+        asm volatile("" ::: "memory");
+        if ((gl & 63) == 0) *(volatile __attribute__((address_space(3))) int *)(prog + f) = done;
+    }
+}
+
+template <int N, bool PUB = false>
+__device__ __forceinline__ void icw_iir_row_body(const IcwK1Args &a, int gl, double *lw = nullptr, int lpitch = 0,
+                                                 int *prog = nullptr)
 {
     const int wv = gl >> 6, r = (gl >> 4) & 3, lr = gl & 15;
     const int f = wv & 1;
@@ -302,7 +317,7 @@ __device__ __forceinline__ void icw_iir_row_body(const IcwK1Args &a, int gl)
     int zoff = 0;
     asm volatile("" : "+s"(zoff));
     const double *xp2 = xp + zoff;             /* still a global-memory pointer (no flat loads) */
-    double *wrow = a.w + (size_t)g * a.w_pitch;
+    double *wrow = PUB ? lw + (size_t)(ch * 2 + f) * lpitch : a.w + (size_t)g * a.w_pitch;
     icw_row_store<N>(W, wrow, writer);
 
     const int T = a.T;
@@ -335,6 +350,7 @@ __device__ __forceinline__ void icw_iir_row_body(const IcwK1Args &a, int gl)
                     icw_row_block<N, 0, 0, 1, true>(W, P, P2, xv, xv2, xp + t + 2 * N, xp2 + t + 2 * N, c, mn);
                     icw_row_store<N>(W, wrow + 2 * N + t, writer);
                     if (__any(mn < 1.0)) { fail = true; break; }
+                    icw_row_publish<PUB>(prog, gl, f, t + 2 * N);
                 }
             } else if (phi0) {
                 /* even order: the same zero steps in every block */
@@ -342,12 +358,14 @@ __device__ __forceinline__ void icw_iir_row_body(const IcwK1Args &a, int gl)
                     icw_row_block<N, 0, 0, 0, true>(W, P, P2, xv, xv2, xp + t + N, xp2 + t + N, c, mn);
                     icw_row_store<N>(W, wrow + N + t, writer);
                     if (__any(mn < 1.0)) { fail = true; break; }
+                    icw_row_publish<PUB>(prog, gl, f, t + N);
                 }
             } else {
                 for (; t + N <= T; t += N) {
                     icw_row_block<N, 0, 1, 1, true>(W, P, P2, xv, xv2, xp + t + N, xp2 + t + N, c, mn);
                     icw_row_store<N>(W, wrow + N + t, writer);
                     if (__any(mn < 1.0)) { fail = true; break; }
+                    icw_row_publish<PUB>(prog, gl, f, t + N);
                 }
             }
             if (fail) icw_row_restart<N>(W, P, P2, xv, xv2, xp, xp2, wrow, t, c);
@@ -367,16 +385,19 @@ __device__ __forceinline__ void icw_iir_row_body(const IcwK1Args &a, int gl)
                     icw_row_store<N>(W, wrow + N + t, writer);
                     icw_row_block<N, 0, 0, 1, false>(W, P, P2, xv, xv2, xp + t + 2 * N, xp2 + t + 2 * N, c, mn);
                     icw_row_store<N>(W, wrow + 2 * N + t, writer);
+                    icw_row_publish<PUB>(prog, gl, f, t + 2 * N);
                 }
             } else if (phi0) {
                 for (; t + N <= T; t += N) {
                     icw_row_block<N, 0, 0, 0, false>(W, P, P2, xv, xv2, xp + t + N, xp2 + t + N, c, mn);
                     icw_row_store<N>(W, wrow + N + t, writer);
+                    icw_row_publish<PUB>(prog, gl, f, t + N);
                 }
             } else {
                 for (; t + N <= T; t += N) {
                     icw_row_block<N, 0, 1, 1, false>(W, P, P2, xv, xv2, xp + t + N, xp2 + t + N, c, mn);
                     icw_row_store<N>(W, wrow + N + t, writer);
+                    icw_row_publish<PUB>(prog, gl, f, t + N);
                 }
             }
             icw_load_x<N>(xv, xp + t);
@@ -385,6 +406,7 @@ __device__ __forceinline__ void icw_iir_row_body(const IcwK1Args &a, int gl)
             icw_row_block<N, 0, 2, 2, false>(W, P, P2, xv, xv2, xp + t + N, xp2 + t + N, c, mn,
                                              ((phi + (unsigned)t) & 1u) != 0u);
             icw_row_store<N>(W, wrow + N + t, writer);
+            icw_row_publish<PUB>(prog, gl, f, t + N);
         }
     }
     const int rem = T - t;
@@ -401,6 +423,7 @@ __device__ __forceinline__ void icw_iir_row_body(const IcwK1Args &a, int gl)
         }
         icw_normalise_ring<N>(W, rem);
     }
+    icw_row_publish<PUB>(prog, gl, f, T);
     if (writer) {
         icw_store_hist<N, 0>(W, a.hist, g, a.n_chains);
         if (dedup) icw_store_hist<N, 0>(W, a.hist, g + 2, a.n_chains);

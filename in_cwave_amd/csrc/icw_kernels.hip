@@ -827,6 +827,79 @@ __device__ __forceinline__ void icw_meters_wg(const IcwK2Args &a, int s, unsigne
     }
 }
 
+/* One frame of K2: the four chains' output sums from their w rows (w[c]: the row at the frame's
+ * window, w[c][N] the state after the frame), the de-subnorm counts, the fs/4 un-mix, then the
+ * frame graph.  dup: mono input with bit-identical converters, chains 2-3 are copies of 0-1. */
+template <int N, bool KAHAN, bool TRIG, bool FCK>
+__device__ __forceinline__ void icw_output_frame(const IcwK2Args &a, const IcwProg *P, const IcwRegFile &R, int s,
+                                                 int t, const double *const (&w)[4], bool dup, const double *lc,
+                                                 IcwFes (&fes)[2], bool count_sn, unsigned (&sn)[4], bool use_tab,
+                                                 unsigned &clip_l, unsigned &clip_r, double &pk_l, double &pk_r)
+{
+    IcwLR in;
+    if (a.cw) {
+        /* complex (CWAVE) input: the analytic signal as read (xwave_reader.c:939-966) */
+        const double *xs = a.xin + (size_t)s * 4 * a.x_pitch + t;
+        in.lre = xs[0]; in.lim = xs[a.x_pitch]; in.rre = xs[2 * a.x_pitch]; in.rim = xs[3 * a.x_pitch];
+    } else {
+        const int nc = dup ? 2 : 4;
+        if (count_sn) {
+#pragma unroll
+            for (int c = 0; c < 4; ++c)
+                if (c < nc) sn[c] += (w[c][N] == 0.0) ? 1u : 0u;
+        }
+        /* filter outputs of the 4 chains (L-I, L-Q, R-I, R-Q) */
+        double y[4];
+        if constexpr (FCK) {
+#pragma unroll 1
+            for (int c = 0; c < 4; ++c) y[c] = icw_iir_out_fc(w[c], N, KAHAN, lc, lc + 20, a.d0, fes[c >> 1]);
+        } else if (dup) {
+            const double *const wins[2] = {w[0], w[1]};
+            double y2[2];
+            icw_iir_out_n<N, KAHAN, 2>(wins, lc, lc + 20, a.d0, y2);
+            y[0] = y[2] = y2[0];
+            y[1] = y[3] = y2[1];
+        } else {
+            icw_iir_out_n<N, KAHAN, 4>(w, lc, lc + 20, a.d0, y);
+        }
+        /* fs/4 un-mix (lpf_hilbert_quad.c:129-156) */
+        double oI[2], oQ[2];
+#pragma unroll
+        for (int ch = 0; ch < 2; ++ch) {
+            const double yi = y[ch * 2], yq = y[ch * 2 + 1];
+            const unsigned kq = (a.hq_phase[s * 2 + ch] + (unsigned)(a.t0 + t)) & 3u;
+            switch (kq) {
+            case 0: oI[ch] = yi * 2.0; oQ[ch] = yq * 2.0; break;
+            case 1: oI[ch] = -yq * 2.0; oQ[ch] = yi * 2.0; break;
+            case 2: oI[ch] = -yi * 2.0; oQ[ch] = -yq * 2.0; break;
+            default: oI[ch] = yq * 2.0; oQ[ch] = -yi * 2.0; break;
+            }
+        }
+        in.lre = oI[0]; in.lim = oQ[0]; in.rre = oI[1]; in.rim = oQ[1];
+    }
+    icw_frame_graph<TRIG>(a, P, R, s, t, in, use_tab, clip_l, clip_r, pk_l, pk_r);
+}
+
+/* the workgroup's de-subnorm counts, one atomic per chain (nc chains computed; dup: the right
+ * converters ran identically, so they rejected the same samples) */
+__device__ __forceinline__ void icw_sn_wg(const IcwK2Args &a, int s, const unsigned (&sn)[4], int nc,
+                                          unsigned (*red_sn)[ICW_K2_TILE / 64])
+{
+    const int tl = threadIdx.x, wv = tl >> 6;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        unsigned v = sn[c];
+        for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+        if ((tl & 63) == 0) red_sn[c][wv] = v;
+    }
+    __syncthreads();
+    if (tl < 4) {
+        unsigned long long tot = 0;
+        for (int i = 0; i < ICW_K2_TILE / 64; ++i) tot += red_sn[tl < nc ? tl : tl - 2][i];
+        if (tot) atomicAdd(&a.sncnt[(size_t)s * 4 + tl], tot);
+    }
+}
+
 /* Output kernel (K2).  A workgroup owns a.tpw (<= ICW_K2_TPW) consecutive 256-frame tiles of one
  * stream (fewer when a launch would have too few workgroups to spread over the chip).
  * The w window of tile k+1 is loaded into registers while tile k is computed, then written to the
@@ -914,50 +987,9 @@ __device__ __forceinline__ void icw_output_body(const IcwK2Args &a, int bx, int 
         const double (&W)[4][TILE + 24] = lw[k & 1];
         const int zk = a.zero * k;
         if (t < T) {
-            IcwLR in;
-            if (a.cw) {
-                /* complex (CWAVE) input: the analytic signal as read (xwave_reader.c:939-966) */
-                const double *xs = a.xin + (size_t)s * 4 * a.x_pitch + t;
-                in.lre = xs[0]; in.lim = xs[a.x_pitch]; in.rre = xs[2 * a.x_pitch]; in.rim = xs[3 * a.x_pitch];
-            } else {
-                if (count_sn) {
-#pragma unroll
-                    for (int c = 0; c < 4; ++c)
-                        if (c < nc) sn[c] += (W[c][tl + N] == 0.0) ? 1u : 0u;
-                }
-                /* filter outputs of the 4 chains (L-I, L-Q, R-I, R-Q) */
-                double y[4];
-                if constexpr (FCK) {
-#pragma unroll 1
-                    for (int c = 0; c < 4; ++c)
-                        y[c] = icw_iir_out_fc(&W[c][tl], N, KAHAN, lcoef + zk, lcoef + 20 + zk, a.d0, fes[c >> 1]);
-                } else if (dup) {
-                    const double *const wins[2] = {&W[0][tl], &W[1][tl]};
-                    double y2[2];
-                    icw_iir_out_n<N, KAHAN, 2>(wins, lcoef + zk, lcoef + 20 + zk, a.d0, y2);
-                    y[0] = y[2] = y2[0];
-                    y[1] = y[3] = y2[1];
-                } else {
-                    const double *const wins[4] = {&W[0][tl], &W[1][tl], &W[2][tl], &W[3][tl]};
-                    icw_iir_out_n<N, KAHAN, 4>(wins, lcoef + zk, lcoef + 20 + zk, a.d0, y);
-                }
-                /* fs/4 un-mix (lpf_hilbert_quad.c:129-156) */
-                double oI[2], oQ[2];
-#pragma unroll
-                for (int ch = 0; ch < 2; ++ch) {
-                    const double yi = y[ch * 2], yq = y[ch * 2 + 1];
-                    const unsigned kq = (a.hq_phase[s * 2 + ch] + (unsigned)(a.t0 + t)) & 3u;
-                    switch (kq) {
-                    case 0: oI[ch] = yi * 2.0; oQ[ch] = yq * 2.0; break;
-                    case 1: oI[ch] = -yq * 2.0; oQ[ch] = yi * 2.0; break;
-                    case 2: oI[ch] = -yi * 2.0; oQ[ch] = -yq * 2.0; break;
-                    default: oI[ch] = yq * 2.0; oQ[ch] = -yi * 2.0; break;
-                    }
-                }
-                in.lre = oI[0]; in.lim = oQ[0]; in.rre = oI[1]; in.rim = oQ[1];
-            }
-
-            icw_frame_graph<TRIG>(a, P, R, s, t, in, use_tab, clip_l, clip_r, pk_l, pk_r);
+            const double *const w[4] = {&W[0][tl], &W[1][tl], &W[2][tl], &W[3][tl]};
+            icw_output_frame<N, KAHAN, TRIG, FCK>(a, P, R, s, t, w, dup, lcoef + zk, fes, count_sn, sn, use_tab, clip_l,
+                                                  clip_r, pk_l, pk_r);
         }
         if (more) {
             /* the other half was last read in tile k-1, before the previous barrier */
@@ -972,20 +1004,7 @@ __device__ __forceinline__ void icw_output_body(const IcwK2Args &a, int bx, int 
     }
     if (count_sn) {
         __shared__ unsigned red_sn[4][TILE / 64];
-        const int wv = tl >> 6;
-#pragma unroll
-        for (int c = 0; c < 4; ++c) {
-            unsigned v = sn[c];
-            for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
-            if ((tl & 63) == 0) red_sn[c][wv] = v;
-        }
-        __syncthreads();
-        if (tl < 4) {
-            unsigned long long tot = 0;
-            for (int i = 0; i < TILE / 64; ++i) tot += red_sn[tl < nc ? tl : tl - 2][i];
-            /* dup: the right converters ran identically, so they rejected the same samples */
-            if (tot) atomicAdd(&a.sncnt[(size_t)s * 4 + tl], tot);
-        }
+        icw_sn_wg(a, s, sn, nc, red_sn);
     }
     if (a.do_render) icw_meters_wg(a, s, clip_l, clip_r, pk_l, pk_r, red_clip, red_pk);
 }
@@ -1233,6 +1252,87 @@ __global__ __launch_bounds__(64) void icw_advance(IcwAdvArgs a)
     if (s < a.n_streams) icw_advance_stream(a, s);
 }
 
+/* K5's overlapped form (a.ovl, the launcher checks that the rows fit in LDS): after K0, waves 0-1
+ * run the recurrence with its w rows in LDS and publish how many frames are final
+ * (icw_iir_row_body<N, true>); waves 2-3 take the output phase frame by frame behind it -- wave w
+ * the 64-frame groups g = w, w + 2, ..: the group's rotation factors (no dependence on the
+ * recurrence), then, once its rows are final, its outputs.  The output phase's ~20 us (576 frames)
+ * but its last group hide behind the recurrence.  Per frame the same code as K2 (icw_output_frame),
+ * so the results are the pipeline's bit for bit. */
+__device__ __forceinline__ void icw_s1_stamp(unsigned long long *stp, int k)
+{
+    if (stp && threadIdx.x == 0) {
+        stp[2 * k] = __builtin_amdgcn_s_memtime();
+        stp[2 * k + 1] = __builtin_amdgcn_s_memrealtime();
+    }
+}
+
+template <int N, bool TRIG>
+__device__ __forceinline__ void icw_s1_overlapped(const IcwS1Args &a, double *lregs)
+{
+    auto stamp = [&a](int k) { icw_s1_stamp(a.stamps, k); };
+    __shared__ double coef[40];
+    __shared__ unsigned red_clip[2][ICW_K2_TILE / 64], red_sn[4][ICW_K2_TILE / 64];
+    __shared__ double red_pk[2][ICW_K2_TILE / 64];
+    const IcwK2Args &a2 = a.k2;
+    const int tid = threadIdx.x, T = a2.T;
+    double *rows = lregs + a.rows_off;
+    int *prog = (int *)(rows + (size_t)4 * a.lpitch);
+    if (tid < 2) prog[tid] = 0;
+    if (tid < 40) coef[tid] = tid < 20 ? a2.pc[tid] : a2.pd[tid - 20];
+    /* mono input with bit-identical converters in phase (K2's `dup`): the flags as the block starts,
+     * read before the recurrence updates them */
+    const bool dup = a2.nch == 1 && a.k1.lr_equal[0] && a.k1.lr_equal[1] && a2.hq_phase[0] == a2.hq_phase[1];
+    __syncthreads();
+    stamp(1);
+    unsigned clip_l = 0, clip_r = 0;
+    double pk_l = 0.0, pk_r = 0.0;
+    unsigned sn[4] = {0u, 0u, 0u, 0u};
+    const bool count_sn = a2.sncnt != nullptr;
+    if (tid < 128) {
+        icw_iir_row_body<N, true>(a.k1, tid, rows, a.lpitch, prog);
+    } else {
+        const int k = tid - 128, w2 = k >> 6, lane = k & 63;
+        const IcwProg *P = a2.prog;
+        IcwRegFile R;
+        R.base = lregs + tid;
+        for (int r = 0; r < P->n_persist; ++r) {
+            const double *b = a2.bus + (size_t)P->persist_slot[r] * 4;
+            IcwLR v; v.lre = b[0]; v.lim = b[1]; v.rre = b[2]; v.rim = b[3];
+            R.set(P->persist_reg[r], v);
+        }
+        const bool use_tab = TRIG && a2.trig_tab;
+        IcwFes fes[2] = {};
+        const volatile __attribute__((address_space(3))) int *vp = (__attribute__((address_space(3))) int *)prog;
+        for (int g = w2; g * 64 < T; g += 2) {
+            const int t = g * 64 + lane;
+            const int need = min(g * 64 + 64, T);
+            if (a.has_trig && t < T) icw_trig_row(a.trig, t);
+            /* bounded: a recurrence that never published (never in a healthy run) flags the call's
+             * error and the wave goes on, so the grid drains */
+            for (unsigned spin = 0; min(vp[0], vp[1]) < need; ++spin) {
+                if (spin >= (1u << 24)) {
+                    if (lane == 0 && a.k1.err) atomicOr(a.k1.err, 1);
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(1);
+            }
+            asm volatile("" ::: "memory");
+            if (t < T) {
+                const size_t lp = a.lpitch;
+                const double *const w[4] = {rows + t, rows + lp + t, rows + 2 * lp + t, rows + 3 * lp + t};
+                icw_output_frame<N, true, TRIG, false>(a2, P, R, 0, t, w, dup, coef + a2.zero * g, fes, count_sn,
+                                                       sn, use_tab, clip_l, clip_r, pk_l, pk_r);
+            }
+        }
+    }
+    __syncthreads();
+    stamp(2);
+    if (count_sn) icw_sn_wg(a2, 0, sn, dup ? 2 : 4, red_sn);
+    icw_meters_wg(a2, 0, clip_l, clip_r, pk_l, pk_r, red_clip, red_pk);
+    stamp(3);
+}
+
 /* K5 icw_stream1: one stream's whole launch block in ONE workgroup -- the per-call form of the
  * drop-in boundary (icw_amod_process_samples: playback.c:619 renders 576-frame blocks, NS_PERTIME,
  * in_cwave.h:133).  The pipeline's four launches (K0, K1r, K2, icw_advance) and their ~6 us gaps
@@ -1250,13 +1350,7 @@ __global__ __launch_bounds__(ICW_K2_TILE) void icw_stream1(IcwS1Args a)
     extern __shared__ __attribute__((aligned(16))) double lregs[];   /* K2's register file */
     /* diagnostic build only (ICW_S1_STAMPS, tools/s1_phases.py): shader-clock and 100 MHz stamps at
      * the phase boundaries */
-    unsigned long long *stp = a.stamps;
-    auto stamp = [&](int k) {
-        if (stp && threadIdx.x == 0) {
-            stp[2 * k] = __builtin_amdgcn_s_memtime();
-            stp[2 * k + 1] = __builtin_amdgcn_s_memrealtime();
-        }
-    };
+    auto stamp = [&a](int k) { icw_s1_stamp(a.stamps, k); };
     stamp(0);
     /* K0: all the block's loads first (the zero-copy input is read across PCIe: one round trip per
      * pass instead of one per frame -- a frame's stores could alias the next frame's loads), then the
@@ -1284,18 +1378,22 @@ __global__ __launch_bounds__(ICW_K2_TILE) void icw_stream1(IcwS1Args a)
             }
         }
     });
-    __syncthreads();
-    stamp(1);
-    /* waves 0-1 (SIMDs 0, 1): the recurrence; waves 2-3 (SIMDs 2, 3), idle otherwise: the block's
-     * Shift / PM rotation factors, which depend only on the frame counter, for the output phase */
-    if (threadIdx.x < 128) icw_iir_row_body<N>(a.k1, threadIdx.x);
-    else if (a.has_trig)
-        for (int t = (int)threadIdx.x - 128; t < a.trig.T; t += 128) icw_trig_row(a.trig, t);
-    __syncthreads();
-    stamp(2);
-    icw_output_body<N, true, TRIG>(a.k2, 0, 0, lregs);
-    __syncthreads();
-    stamp(3);
+    if (a.ovl) {
+        icw_s1_overlapped<N, TRIG>(a, lregs);
+    } else {
+        __syncthreads();
+        stamp(1);
+        /* waves 0-1 (SIMDs 0, 1): the recurrence; waves 2-3 (SIMDs 2, 3), idle otherwise: the block's
+         * Shift / PM rotation factors, which depend only on the frame counter, for the output phase */
+        if (threadIdx.x < 128) icw_iir_row_body<N>(a.k1, threadIdx.x);
+        else if (a.has_trig)
+            for (int t = (int)threadIdx.x - 128; t < a.trig.T; t += 128) icw_trig_row(a.trig, t);
+        __syncthreads();
+        stamp(2);
+        icw_output_body<N, true, TRIG>(a.k2, 0, 0, lregs);
+        __syncthreads();
+        stamp(3);
+    }
     if (threadIdx.x == 0) {
         icw_advance_stream(a.adv, 0);
         if (a.adv.done) {
@@ -2338,7 +2436,19 @@ template <int N>
 static hipError_t launch_s1_t(IcwS1Args a, hipStream_t st)
 {
     a.k2.tpw = (a.k2.T + ICW_K2_TILE - 1) / ICW_K2_TILE;
-    const size_t lds = (size_t)a.k2.n_regs * 4 * ICW_K2_TILE * sizeof(double);
+    const size_t regs = (size_t)a.k2.n_regs * 4 * ICW_K2_TILE * sizeof(double);
+    a.lpitch = (a.k2.T + N + 2) & ~1;
+    a.rows_off = a.k2.n_regs * 4 * ICW_K2_TILE;
+    const size_t rows = (size_t)4 * a.lpitch * sizeof(double) + 16;
+    a.ovl = a.ovl && regs + rows <= ICW_S1_OVL_LDS;
+    const size_t lds = regs + (a.ovl ? rows : 0);
+    if (lds > 64 * 1024) {
+        const hipError_t e = a.k2.trig ? hipFuncSetAttribute((const void *)icw_stream1<N, true>,
+                                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds)
+                                       : hipFuncSetAttribute((const void *)icw_stream1<N, false>,
+                                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        if (e != hipSuccess) return e;
+    }
     if (a.k2.trig) hipLaunchKernelGGL((icw_stream1<N, true>), dim3(1), dim3(ICW_K2_TILE), lds, st, a);
     else hipLaunchKernelGGL((icw_stream1<N, false>), dim3(1), dim3(ICW_K2_TILE), lds, st, a);
     return hipGetLastError();

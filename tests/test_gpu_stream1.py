@@ -114,3 +114,22 @@ def test_stream1_polled_completion(oracle, icw, fmt, ch, b24, spin, monkeypatch)
         t += n
     assert ctx.n_frame(0) == ref.n_frame()
     ctx.close()
+
+
+@pytest.mark.parametrize("ovl", ["1", "0"])
+@pytest.mark.parametrize("kind", ["shift_master", "pm_shift_mix", "long_chain", "random"])
+@pytest.mark.parametrize("ch", [1, 2])
+def test_stream1_overlapped_output_phase(oracle, icw, ovl, kind, ch, monkeypatch):
+    """K5's output phase beside the recurrence (ICW_S1_OVL=1, the default: the w rows in LDS, the
+    output waves polling the recurrence's published frame count) and after it (ICW_S1_OVL=0): both
+    the oracle's bytes, for block lengths around the 64-frame groups and the recurrence's blocks,
+    register-file and chain programs, stereo and mono (dedup)"""
+    monkeypatch.setenv("ICW_S1_OVL", ovl)
+    cfg = graph.default_config(48000, channels=ch)
+    if kind == "random":
+        nodes = random_list(np.random.default_rng(77))
+    else:
+        nodes = {"shift_master": graph.graph_shift_master, "pm_shift_mix": graph.graph_pm_shift_mix,
+                 "long_chain": graph.graph_long_chain}[kind]()
+    lens = [576, 1, 19, 38, 63, 64, 65, 128, 129, 2048, 2500, 576]
+    calls(oracle, icw, cfg, nodes, lens, monkeypatch, True)
