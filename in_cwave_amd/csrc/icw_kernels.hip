@@ -221,6 +221,9 @@ __global__ __launch_bounds__(256) void icw_unpack_frames(IcwK0Args a)
  * window at the same phase of that pattern, so all offsets inside a block are immediates.  Taps past
  * the last multiple of 8 run one at a time. */
 #define ICW_FIR_R 8                                  /* outputs per lane */
+#ifndef ICW_CHAIN4
+#define ICW_CHAIN4 1                                 /* KF2: chain programs op by op over a lane's frames */
+#endif
 
 __device__ __forceinline__ int icw_fir_phys(int i) { return i + (i >> 3); }
 
@@ -801,6 +804,123 @@ __device__ __forceinline__ void icw_frame_graph(const IcwK2Args &a, const IcwPro
     }
 }
 
+/* A chain program's op fields as the frame loop uses them, read once per op for all the frames a
+ * lane holds (not per frame: the op list lives in global memory, and the loads came back after
+ * every store of the frame loop) */
+struct IcwOpK {
+    int mode, chain_in, xch, iq0, iq1, tout0, tout1, act0, act1, ts0, ts1, wb;
+    double g0, g1;
+};
+
+__device__ __forceinline__ IcwOpK icw_op_k(const IcwOp &op)
+{
+    IcwOpK k;
+    k.mode = op.mode; k.chain_in = op.chain_in; k.xch = op.xch;
+    k.iq0 = op.iqinv[0]; k.iq1 = op.iqinv[1];
+    k.tout0 = op.tout[0]; k.tout1 = op.tout[1];
+    k.act0 = op.act[0]; k.act1 = op.act[1];
+    k.ts0 = op.tslot[0]; k.ts1 = op.tslot[1];
+    k.wb = op.wb_slot;
+    k.g0 = op.gain[0]; k.g1 = op.gain[1];
+    return k;
+}
+
+/* R frames of one lane (t0 + r; the first nv are in the block) through a chain program, op by op:
+ * the op's fields are read once for the R frames and their rotation factors (the per-frame table,
+ * every stream in step) are loaded together before the arithmetic.  Per frame the arithmetic of
+ * icw_frame_graph + icw_exec_op in the same order, so the bits are the same; the rendered integers
+ * go to dv (0 for frames past the block). */
+template <bool TRIG, int R>
+__device__ __forceinline__ void icw_chain_frames(const IcwK2Args &a, const IcwProg *P, int s, int t0, int nv,
+                                                 const IcwLR (&in)[R], unsigned &clip_l, unsigned &clip_r,
+                                                 double &pk_l, double &pk_r, int (&dv)[R][2])
+{
+    const int T = a.T;
+    double *bus_s = a.bus + (size_t)s * ICW_N_INPUTS * 4;
+    IcwLR prev[R];
+    double lOut[R], rOut[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        prev[r] = in[r];
+        lOut[r] = rOut[r] = 0.0;
+        if (r < nv && t0 + r == T - 1) {
+            bus_s[0] = in[r].lre; bus_s[1] = in[r].lim; bus_s[2] = in[r].rre; bus_s[3] = in[r].rim;
+        }
+    }
+    const bool bypass = P->bypass != 0;
+    for (int oi = 0; oi < P->n_ops; ++oi) {
+        const IcwOpK k = icw_op_k(P->ops[oi]);
+        const bool rot = TRIG && (k.mode == ICW_MODE_SHIFT || k.mode == ICW_MODE_PM);
+        double cs[R][2], sn[R][2];
+        if (rot) {
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                const double *trow = a.trig_tab + (size_t)min(t0 + r, T - 1) * a.trig_pitch;
+                cs[r][0] = k.act0 ? trow[k.ts0 * 2] : 0.0;
+                sn[r][0] = k.act0 ? trow[k.ts0 * 2 + 1] : 0.0;
+                cs[r][1] = k.act1 ? trow[k.ts1 * 2] : 0.0;
+                sn[r][1] = k.act1 ? trow[k.ts1 * 2 + 1] : 0.0;
+            }
+        }
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            IcwLR d;
+            if (bypass) {
+                d = in[r];
+            } else {
+                d.lre = d.lim = d.rre = d.rim = 0.0;
+                if (k.chain_in & 1) { d.lre += in[r].lre; d.lim += in[r].lim; d.rre += in[r].rre; d.rim += in[r].rim; }
+                if (k.chain_in & 2) { d.lre += prev[r].lre; d.lim += prev[r].lim; d.rre += prev[r].rre; d.rim += prev[r].rim; }
+            }
+            double xt;
+            switch (k.xch) {
+            case ICW_XCH_SWAP:
+                xt = d.lre; d.lre = d.rre; d.rre = xt;
+                xt = d.lim; d.lim = d.rim; d.rim = xt;
+                break;
+            case ICW_XCH_LEFTONLY: d.rre = d.lre; d.rim = d.lim; break;
+            case ICW_XCH_RIGHTONLY: d.lre = d.rre; d.lim = d.rim; break;
+            case ICW_XCH_MIXLR:
+                d.lre = d.rre = (d.lre + d.rre) / 2.0;
+                d.lim = d.rim = (d.lim + d.rim) / 2.0;
+                break;
+            default: break;
+            }
+            if (k.iq0) { xt = d.lre; d.lre = d.lim; d.lim = xt; }
+            if (k.iq1) { xt = d.rre; d.rre = d.rim; d.rim = xt; }
+            d.lre *= k.g0; d.lim *= k.g0;
+            d.rre *= k.g1; d.rim *= k.g1;
+            if (k.mode == ICW_MODE_MASTER) {
+                lOut[r] = icw_master(k.tout0, d.lre, d.lim);
+                rOut[r] = icw_master(k.tout1, d.rre, d.rim);
+                continue;
+            }
+            IcwLR o = d;
+            if (rot) {
+                if (k.act0) icw_rot(d.lre, d.lim, cs[r][0], sn[r][0], o.lre, o.lim);
+                if (k.act1) icw_rot(d.rre, d.rim, cs[r][1], sn[r][1], o.rre, o.rim);
+            }
+            prev[r] = o;
+            if (k.wb >= 0 && r < nv && t0 + r == T - 1) {
+                double *b = bus_s + k.wb * 4;
+                b[0] = o.lre; b[1] = o.lim; b[2] = o.rre; b[3] = o.rim;
+            }
+        }
+    }
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        dv[r][0] = dv[r][1] = 0;
+        if (r < nv) {
+            if (a.pre) {
+                double *p = a.pre + (size_t)s * a.pre_stride + (size_t)(t0 + r) * 2;
+                p[0] = lOut[r]; p[1] = rOut[r];
+            }
+            dv[r][0] = icw_render_round(lOut[r], a.rk, clip_l, pk_l);
+            dv[r][1] = icw_render_round(rOut[r], a.rk, clip_r, pk_r);
+        }
+    }
+}
+
 /* per-workgroup meters (ICW_K2_TILE threads): wave reduce, LDS, one atomic per stream/channel */
 __device__ __forceinline__ void icw_meters_wg(const IcwK2Args &a, int s, unsigned clip_l, unsigned clip_r, double pk_l,
                                               double pk_r, unsigned (*red_clip)[ICW_K2_TILE / 64],
@@ -1081,6 +1201,27 @@ __global__ __launch_bounds__(256, 4) void icw_fir_graph(IcwFirArgs f, IcwK2Args 
         const int h = ch ? 4 : 0;
         int dv[4][2];
         const int fr0 = ICW_FIR_R * ll + h;
+        if (ICW_CHAIN4 && P->chain && (TAB || !TRIG) && !a.iq_out && a.do_render) {
+            /* chain program, factors from the table (or none): the four frames op by op */
+            IcwLR in4[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const double oi = __shfl_xor(ch ? vi[r] : vi[r + 4], 32);
+                const double oq = __shfl_xor(ch ? q[r] : q[r + 4], 32);
+                if (ch) { in4[r].lre = oi; in4[r].lim = oq; in4[r].rre = vi[r + 4]; in4[r].rim = q[r + 4]; }
+                else { in4[r].lre = vi[r]; in4[r].lim = q[r]; in4[r].rre = oi; in4[r].rim = oq; }
+            }
+            /* two frames per pass: four at once spill (128 VGPRs) */
+#pragma unroll
+            for (int hh = 0; hh < 4; hh += 2) {
+                const IcwLR in2[2] = {in4[hh], in4[hh + 1]};
+                int dv2[2][2];
+                icw_chain_frames<TRIG, 2>(a, P, s, tt + fr0 + hh, min(2, max(nf - fr0 - hh, 0)), in2, clip_l, clip_r,
+                                          pk_l, pk_r, dv2);
+                dv[hh][0] = dv2[0][0]; dv[hh][1] = dv2[0][1];
+                dv[hh + 1][0] = dv2[1][0]; dv[hh + 1][1] = dv2[1][1];
+            }
+        } else {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
             const double oi = __shfl_xor(ch ? vi[r] : vi[r + 4], 32);
@@ -1093,6 +1234,7 @@ __global__ __launch_bounds__(256, 4) void icw_fir_graph(IcwFirArgs f, IcwK2Args 
                 else { in.lre = vi[r]; in.lim = q[r]; in.rre = oi; in.rim = oq; }
                 icw_frame_graph<TRIG, TAB, true>(a, P, Rf, s, tt + fr, in, use_tab, clip_l, clip_r, pk_l, pk_r, dv[r]);
             }
+        }
         }
         if (a.do_render && !a.iq_out) {
             unsigned char *o = a.out + (size_t)s * a.out_stride;
