@@ -1280,6 +1280,59 @@ __global__ __launch_bounds__(256, 4) void icw_fir_graph(IcwFirArgs f, IcwK2Args 
                 }
             }
         }
+    } else if (ICW_CHAIN4 && P->chain && (TAB || !TRIG) && !a.iq_out && a.do_render) {
+        /* mono input, chain program: the lane's 8 frames op by op, two at a time, and their 8
+         * rendered frames stored together (32 / 48 contiguous bytes per lane) */
+        const int fr0 = ICW_FIR_R * ll;
+        const bool b24 = a.rk.is24;
+        unsigned w[ICW_FIR_R / 2 * 3];               /* packed output: 16-bit frames in w[0..8) */
+#pragma unroll
+        for (int hh = 0; hh < ICW_FIR_R; hh += 2) {
+            IcwLR in2[2];
+#pragma unroll
+            for (int r = 0; r < 2; ++r) {
+                in2[r].lre = in2[r].rre = vi[hh + r];
+                in2[r].lim = in2[r].rim = q[hh + r];
+            }
+            int dv[2][2];
+            icw_chain_frames<TRIG, 2>(a, P, s, tt + fr0 + hh, min(2, max(nf - fr0 - hh, 0)), in2, clip_l, clip_r, pk_l,
+                                      pk_r, dv);
+            if (b24) {
+                const unsigned l0 = (unsigned)dv[0][0] & 0xffffffu, r0 = (unsigned)dv[0][1] & 0xffffffu;
+                const unsigned l1 = (unsigned)dv[1][0] & 0xffffffu, r1 = (unsigned)dv[1][1] & 0xffffffu;
+                w[hh / 2 * 3 + 0] = l0 | (r0 << 24);
+                w[hh / 2 * 3 + 1] = (r0 >> 8) | (l1 << 16);
+                w[hh / 2 * 3 + 2] = (l1 >> 16) | (r1 << 8);
+            } else {
+                w[hh] = ((unsigned)dv[0][0] & 0xffffu) | ((unsigned)dv[0][1] << 16);
+                w[hh + 1] = ((unsigned)dv[1][0] & 0xffffu) | ((unsigned)dv[1][1] << 16);
+            }
+        }
+        unsigned char *o = a.out + (size_t)s * a.out_stride;
+        const int nv = min(ICW_FIR_R, max(nf - fr0, 0));
+        if (b24) {
+            unsigned char *p = o + (size_t)(tt + fr0) * 6;
+            if (nv == ICW_FIR_R && !((uintptr_t)p & 7)) {
+                uint2 *q2 = (uint2 *)p;
+#pragma unroll
+                for (int i = 0; i < ICW_FIR_R / 2 * 3 / 2; ++i) q2[i] = make_uint2(w[2 * i], w[2 * i + 1]);
+            } else {
+                /* byte r of the packed run is byte r of the output */
+#pragma unroll
+                for (int i = 0; i < ICW_FIR_R * 6; ++i)
+                    if (i < nv * 6) p[i] = (unsigned char)(w[i >> 2] >> (8 * (i & 3)));
+            }
+        } else {
+            unsigned *p = (unsigned *)(o + (size_t)(tt + fr0) * 4);
+            if (nv == ICW_FIR_R && !((uintptr_t)p & 15)) {
+                *(uint4 *)p = make_uint4(w[0], w[1], w[2], w[3]);
+                *(uint4 *)(p + 4) = make_uint4(w[4], w[5], w[6], w[7]);
+            } else {
+#pragma unroll
+                for (int r = 0; r < ICW_FIR_R; ++r)
+                    if (r < nv) p[r] = w[r];
+            }
+        }
     } else {
 #pragma unroll 1
         for (int r = 0; r < ICW_FIR_R; ++r) {

@@ -262,3 +262,19 @@ def test_fir_state_blob_records_order(icw):
 def C_sizeof_blob():
     import ctypes
     return ctypes.sizeof(abi.StateBlob)
+
+
+@pytest.mark.parametrize("ch", [1, 2])
+@pytest.mark.parametrize("b24", [False, True])
+@pytest.mark.parametrize("nodes", ["shift_master", "pm_shift_mix", "master"])
+def test_fir_chain_frames_round_renders(oracle, icw, ch, b24, nodes):
+    """KF2's chain programs op by op over a lane's frames (icw_chain_frames): mono and stereo, 16-
+    and 24-bit ROUND output, ragged block ends (the last lane's frames partly past the block: the
+    packed stores fall back to per-frame / per-byte stores)"""
+    cfg = graph.default_config(48000, fmt=abi.FMT_I16, channels=ch, need24bits=b24)
+    nodes = {"shift_master": graph.graph_shift_master, "pm_shift_mix": graph.graph_pm_shift_mix,
+             "master": graph.graph_master_only}[nodes]()
+    raw = synth.batch_pcm(3, 5003, 48000, channels=ch)
+    ctx, out, pre, ro, rp = run_fir(oracle, icw, cfg, nodes, raw, 5003, 254, blocks=[2049, 7, 2947])
+    assert_parity(out, pre, ro, rp)
+    ctx.close()
