@@ -222,6 +222,7 @@ struct IcwK2Args {
     const double *trig_tab;        /* nullable [T][trig_pitch]: (cos, sin) per active Shift / PM channel
                                       for streams whose call-start counter equals stream 0's */
     int32_t trig_pitch;
+    int32_t trig_perm_q;           /* the table's row order (icw_trig_index) */
     int32_t zero;                  /* always 0: an offset the compiler cannot fold (keeps loads in a loop) */
     uint32_t *fes;                 /* FP_CHECK census, as in IcwK1Args; null: no FC() */
     int32_t tpw;                   /* tiles per workgroup (1..ICW_K2_TPW), set by the launcher */
@@ -237,8 +238,10 @@ struct IcwTrigArgs {
     int32_t T, scaled, trig_pitch;
     unsigned long long ssr;
     uint32_t sample_rate;
-    double *tab;                   /* [T][trig_pitch] */
+    double *tab;                   /* [T][trig_pitch], rows in icw_trig_index order */
+    int32_t perm_q;                /* 0: row t at t; > 0 (KF2): row t at (t & 7) * perm_q + (t >> 3) */
 };
+
 
 /* FC() of fp_check.c:52-100 (except_stats_check): a NaN or a denormal becomes 0.0, an infinity
  * +-INF_HUGE_VALUE (65535.0, fp_check.h:60); each is counted in FP_EXCEPT_STATS order total, snan,

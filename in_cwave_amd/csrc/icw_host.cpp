@@ -1430,7 +1430,7 @@ int icw_process_streams(icw_ctx *c, int first, int count, const void *in, size_t
     const bool table = c->prog.needs_omega && !bus && c->prog.n_trig > 0 && count > 1;
     bool in_step = table;
     for (int i = 1; in_step && i < count; ++i) in_step = c->nf_host[first + i] == c->nf_host[first];
-    if (table && grow((void **)&c->trig, &c->trig_bytes, (size_t)Tb * 2 * c->prog.n_trig * sizeof(double)))
+    if (table && grow((void **)&c->trig, &c->trig_bytes, (size_t)((Tb + 7) & ~7) * 2 * c->prog.n_trig * sizeof(double)))
         return ICW_ENOMEM;
     if (bus)
         for (int p = 0; p < n_sets; ++p)
@@ -1766,10 +1766,13 @@ int icw_process_streams(icw_ctx *c, int first, int count, const void *in, size_t
             at.ssr = ssr;
             at.sample_rate = cfg.sample_rate;
             at.tab = c->trig;
+            /* the fused FIR kernel's lanes hold 4 / 8 consecutive frames: rows 8 frames apart */
+            at.perm_q = fir_fused ? (T + 7) / 8 : 0;
             /* same stream as K2: the previous block's K2 has read the table before it is rewritten */
             if (icw_launch_trig_table(&at, s2) != hipSuccess) return ICW_EDEVICE;
             a2.trig_tab = c->trig;
             a2.trig_pitch = at.trig_pitch;
+            a2.trig_perm_q = at.perm_q;
         }
         /* rpre[p] / iq[p] were last read by the serial render of block b - n_sets (on sR) */
         if (c->serial_render && b >= n_sets && sR != s2 && hipStreamWaitEvent(s2, c->k3done[p], 0) != hipSuccess)

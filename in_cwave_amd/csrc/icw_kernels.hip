@@ -561,6 +561,14 @@ struct IcwRegFile {
     }
 };
 
+/* row of frame t in the rotation table: frame-major, or (perm_q > 0, the fused FIR kernel, whose
+ * lanes hold 4 or 8 consecutive frames) frames 8 apart in consecutive rows, so that a wave's loads
+ * of one frame slot cover 1-2 KB contiguously instead of one row every 128 / 256 B */
+__device__ __forceinline__ size_t icw_trig_index(int t, int perm_q)
+{
+    return perm_q ? (size_t)(t & 7) * (size_t)perm_q + (size_t)(t >> 3) : (size_t)t;
+}
+
 /* rotate (re,im) by e^{j phi} given cos/sin (adv_modulator.c:546-547, 576-577) */
 __device__ __forceinline__ void icw_rot(double re, double im, double cs, double sn, double &ore, double &oim)
 {
@@ -721,7 +729,7 @@ __device__ __forceinline__ void icw_frame_graph(const IcwK2Args &a, const IcwPro
         double *q = a.iq_out + ((size_t)s * T + t) * 4;
         q[0] = in.lre; q[1] = in.lim; q[2] = in.rre; q[3] = in.rim;
     } else {
-        const double *trow = use_tab ? a.trig_tab + (size_t)t * a.trig_pitch : nullptr;
+        const double *trow = use_tab ? a.trig_tab + icw_trig_index(t, a.trig_perm_q) * a.trig_pitch : nullptr;
         const double omega = (TRIG && !use_tab) ? icw_omega(a.n_frame[s], a.t0 + t, a.scaled, a.ssr, a.sample_rate)
                                                 : 0.0;
         /* DSP list (adv_modulator.c:637-751) */
@@ -855,11 +863,12 @@ __device__ __forceinline__ void icw_chain_frames(const IcwK2Args &a, const IcwPr
         if (rot) {
 #pragma unroll
             for (int r = 0; r < R; ++r) {
-                const double *trow = a.trig_tab + (size_t)min(t0 + r, T - 1) * a.trig_pitch;
-                cs[r][0] = k.act0 ? trow[k.ts0 * 2] : 0.0;
-                sn[r][0] = k.act0 ? trow[k.ts0 * 2 + 1] : 0.0;
-                cs[r][1] = k.act1 ? trow[k.ts1 * 2] : 0.0;
-                sn[r][1] = k.act1 ? trow[k.ts1 * 2 + 1] : 0.0;
+                /* (cos, sin) of a channel: one 16-byte load (rows and columns are 16-byte aligned) */
+                const double *trow = a.trig_tab + icw_trig_index(min(t0 + r, T - 1), a.trig_perm_q) * a.trig_pitch;
+                const double2 f0 = k.act0 ? *(const double2 *)(trow + k.ts0 * 2) : make_double2(0.0, 0.0);
+                const double2 f1 = k.act1 ? *(const double2 *)(trow + k.ts1 * 2) : make_double2(0.0, 0.0);
+                cs[r][0] = f0.x; sn[r][0] = f0.y;
+                cs[r][1] = f1.x; sn[r][1] = f1.y;
             }
         }
 #pragma unroll
@@ -1356,7 +1365,7 @@ __device__ __forceinline__ void icw_trig_row(const IcwTrigArgs &a, int t)
 {
     const IcwProg *P = a.prog;
     const double omega = icw_omega(a.n_frame[0], a.t0 + t, a.scaled, a.ssr, a.sample_rate);
-    double *row = a.tab + (size_t)t * a.trig_pitch;
+    double *row = a.tab + icw_trig_index(t, a.perm_q) * a.trig_pitch;
     for (int oi = 0; oi < P->n_ops; ++oi) {
         const IcwOp &op = P->ops[oi];
         if (op.mode != ICW_MODE_SHIFT && op.mode != ICW_MODE_PM) continue;
