@@ -1160,14 +1160,16 @@ __global__ __launch_bounds__(ICW_K2_TILE, ICW_K2_MINWG) void icw_output(IcwK2Arg
  * live across it in scratch -- 44 B per thread written to HBM, most of the kernel's 2.95x write
  * traffic (profiles/r02_c2fir_pmc.json: 198 MB per launch against 67 MB of output); giving that
  * variant 168 VGPRs instead (3 workgroups per CU) removed the spills but cost c2fir 22 %. */
-template <bool TRIG, bool TAB>
+/* NC: computed channels (1: mono input, 2: stereo), a template parameter so that each form gets its
+ * own register allocation (the mono graph phase holds 8 frames per lane, the stereo one 4) */
+template <bool TRIG, bool TAB, int NC>
 __global__ __launch_bounds__(256, 4) void icw_fir_graph(IcwFirArgs f, IcwK2Args a)
 {
     extern __shared__ double lds[];
     __shared__ unsigned red_clip[2][ICW_K2_TILE / 64];
     __shared__ double red_pk[2][ICW_K2_TILE / 64];
     const int s = blockIdx.y;
-    const int nchc = f.nch > 1 ? 2 : 1;
+    constexpr int nchc = NC;
     const int TF = 256 * ICW_FIR_R / nchc;
     const int tt = blockIdx.x * TF;
     const int M = f.M, c = M >> 1;
@@ -1211,19 +1213,19 @@ __global__ __launch_bounds__(256, 4) void icw_fir_graph(IcwFirArgs f, IcwK2Args 
         int dv[4][2];
         const int fr0 = ICW_FIR_R * ll + h;
         if (ICW_CHAIN4 && P->chain && (TAB || !TRIG) && !a.iq_out && a.do_render) {
-            /* chain program, factors from the table (or none): the four frames op by op */
-            IcwLR in4[4];
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const double oi = __shfl_xor(ch ? vi[r] : vi[r + 4], 32);
-                const double oq = __shfl_xor(ch ? q[r] : q[r + 4], 32);
-                if (ch) { in4[r].lre = oi; in4[r].lim = oq; in4[r].rre = vi[r + 4]; in4[r].rim = q[r + 4]; }
-                else { in4[r].lre = vi[r]; in4[r].lim = q[r]; in4[r].rre = oi; in4[r].rim = oq; }
-            }
-            /* two frames per pass: four at once spill (128 VGPRs) */
+            /* chain program, factors from the table (or none): the four frames op by op, two per
+             * pass (four at once spill at 128 VGPRs), each pass's I / Q exchange just before it */
 #pragma unroll
             for (int hh = 0; hh < 4; hh += 2) {
-                const IcwLR in2[2] = {in4[hh], in4[hh + 1]};
+                IcwLR in2[2];
+#pragma unroll
+                for (int j = 0; j < 2; ++j) {
+                    const int r = hh + j;
+                    const double oi = __shfl_xor(ch ? vi[r] : vi[r + 4], 32);
+                    const double oq = __shfl_xor(ch ? q[r] : q[r + 4], 32);
+                    if (ch) { in2[j].lre = oi; in2[j].lim = oq; in2[j].rre = vi[r + 4]; in2[j].rim = q[r + 4]; }
+                    else { in2[j].lre = vi[r]; in2[j].lim = q[r]; in2[j].rre = oi; in2[j].rim = oq; }
+                }
                 int dv2[2][2];
                 icw_chain_frames<TRIG, 2>(a, P, s, tt + fr0 + hh, min(2, max(nf - fr0 - hh, 0)), in2, clip_l, clip_r,
                                           pk_l, pk_r, dv2);
@@ -2505,21 +2507,27 @@ extern "C" size_t icw_fir_graph_lds(int M, int nt, int nch, int n_regs)
 }
 
 /* in_step: every stream of the launch is in step with the rotation table (a->trig_tab) */
+template <int NC>
+static hipError_t launch_fir_graph_nc(const IcwFirArgs *f, const IcwK2Args *a, int in_step, size_t lds, hipStream_t st)
+{
+    const int TF = 256 * ICW_FIR_R / NC;
+    dim3 grid((f->T + TF - 1) / TF, f->n_streams);
+    const void *fn = !a->trig ? (const void *)icw_fir_graph<false, false, NC>
+                   : in_step ? (const void *)icw_fir_graph<true, true, NC> : (const void *)icw_fir_graph<true, false, NC>;
+    if (fir_lds_attr(fn, lds) != hipSuccess) return hipErrorInvalidValue;
+    if (!a->trig) hipLaunchKernelGGL((icw_fir_graph<false, false, NC>), grid, dim3(256), lds, st, *f, *a);
+    else if (in_step) hipLaunchKernelGGL((icw_fir_graph<true, true, NC>), grid, dim3(256), lds, st, *f, *a);
+    else hipLaunchKernelGGL((icw_fir_graph<true, false, NC>), grid, dim3(256), lds, st, *f, *a);
+    return hipGetLastError();
+}
+
 extern "C" hipError_t icw_launch_fir_graph(const IcwFirArgs *f, const IcwK2Args *a, int in_step, hipStream_t st)
 {
     if (!fir_ok(f->M, f->nt)) return hipErrorInvalidValue;
     const size_t lds = icw_fir_graph_lds(f->M, f->nt, f->nch, a->n_regs);
     if (!lds) return hipErrorInvalidValue;
     if (in_step && !(a->trig && a->trig_tab)) return hipErrorInvalidValue;
-    const int TF = 256 * ICW_FIR_R / (f->nch > 1 ? 2 : 1);
-    dim3 grid((f->T + TF - 1) / TF, f->n_streams);
-    const void *fn = !a->trig ? (const void *)icw_fir_graph<false, false>
-                   : in_step ? (const void *)icw_fir_graph<true, true> : (const void *)icw_fir_graph<true, false>;
-    if (fir_lds_attr(fn, lds) != hipSuccess) return hipErrorInvalidValue;
-    if (!a->trig) hipLaunchKernelGGL((icw_fir_graph<false, false>), grid, dim3(256), lds, st, *f, *a);
-    else if (in_step) hipLaunchKernelGGL((icw_fir_graph<true, true>), grid, dim3(256), lds, st, *f, *a);
-    else hipLaunchKernelGGL((icw_fir_graph<true, false>), grid, dim3(256), lds, st, *f, *a);
-    return hipGetLastError();
+    return f->nch > 1 ? launch_fir_graph_nc<2>(f, a, in_step, lds, st) : launch_fir_graph_nc<1>(f, a, in_step, lds, st);
 }
 
 template <int N, bool K>
