@@ -434,15 +434,11 @@ def measure_gpu(wname, streams, frames, steps, warmup, e2e_steps, dev, local_dev
     if W.get("fir"):
         ctx.set_fir_hilbert(W["fir"], FIR_BETA)
     # synthetic input of the workload's shape for this rank's shard of streams (SURVEY 8(d)
-    # generator); 16 distinct generated streams are tiled over the shard to bound setup time
-    n_gen = min(S, 16)
+    # generator): every stream its own seed (global stream index), generated by host threads
     first = rank * S
-    gen = synth.batch_pcm(n_gen, T, fs, channels=W["ch"], fmt=fmt, first=first)   # uint8 [n_gen, T*fsz]
-    d_in = torch.empty((S, gen.shape[1]), dtype=torch.uint8, device=dev)
-    g = torch.from_numpy(gen).to(dev)
-    for s in range(S):
-        d_in[s].copy_(g[s % n_gen])
-    del g
+    gen = synth.batch_pcm(S, T, fs, channels=W["ch"], fmt=fmt, first=first,
+                          workers=synth.cpu_workers())                      # uint8 [S, T*fsz]
+    d_in = torch.from_numpy(gen).to(dev)
     osz = 2 * ctx.render_size
     d_out = torch.empty((S, T * osz), dtype=torch.uint8, device=dev)
     torch.cuda.synchronize()
@@ -484,8 +480,7 @@ def measure_gpu(wname, streams, frames, steps, warmup, e2e_steps, dev, local_dev
         # pinned host buffers (icw_host_alloc): the call copies each launch block's slices in and
         # out on a copy stream beside the other blocks' kernels
         h_in = L.host_array((S, gen.shape[1]))
-        for s0 in range(0, S, n_gen):
-            h_in[s0:s0 + n_gen] = gen[:min(n_gen, S - s0)]
+        h_in[:] = gen
         h_out = L.host_array((S, T * osz))
         ctx.process(h_in, T, out=h_out)                       # warm the staging buffers
         te = time.perf_counter()

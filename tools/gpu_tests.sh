@@ -1,7 +1,7 @@
 #!/bin/bash
 # GPU-box test pass: the -m gpu suite (one process, per-test timeout) then smoke; stop at a crash.
 mkdir -p gpurun_out
-timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread "$@" \
+timeout -k 10 1050 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread "$@" \
     > gpurun_out/pytest_gpu.txt 2>&1
 rc=$?
 echo "[pytest_gpu] rc=$rc" | tee -a gpurun_out/steps.txt
