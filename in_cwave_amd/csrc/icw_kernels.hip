@@ -224,6 +224,12 @@ __global__ __launch_bounds__(256) void icw_unpack_frames(IcwK0Args a)
 #ifndef ICW_FIR_INTERIOR
 #define ICW_FIR_INTERIOR 1                           /* FIR staging: the interior tiles' short form */
 #endif
+#ifndef ICW_FIR_OCC
+#define ICW_FIR_OCC 4                                /* KF2 workgroups per CU the register budget is sized for */
+#endif
+#ifndef ICW_FIR_STAMPS
+#define ICW_FIR_STAMPS 0                             /* diagnostic: KF2 phase stamps (tools/fir_phases.py) */
+#endif
 #ifndef ICW_CHAIN4
 #define ICW_CHAIN4 1                                 /* KF2: chain programs op by op over a lane's frames */
 #endif
@@ -1176,7 +1182,7 @@ __global__ __launch_bounds__(ICW_K2_TILE, ICW_K2_MINWG) void icw_output(IcwK2Arg
 /* Fused FIR converter + graph + render (KF2): one workgroup per stream and 1024-frame tile (2048
  * for mono).  Wave w owns frames [256 w, 256 w + 256) of the tile: lanes 0-31 sum channel L's
  * outputs and lanes 32-63 channel R's, 8 consecutive frames each (icw_fir_sums).  A lane pair
- * (l, l + 32) then swaps half of its I / Q values (__shfl_xor 32), so lane l holds both channels
+ * (l, l + 32) then swaps half of its I / Q values (v_permlane32_swap), so lane l holds both channels
  * of frames 0-3 of its eight and lane l + 32 of frames 4-7, and each takes its 4 frames straight
  * through K2's per-frame code (icw_frame_graph: DSP list, pre-render, ROUND render, meters).  The
  * analytic signal never leaves the registers (KF + K2 move 32 B per frame through HBM twice); the
@@ -1188,11 +1194,47 @@ __global__ __launch_bounds__(ICW_K2_TILE, ICW_K2_MINWG) void icw_output(IcwK2Arg
  * live across it in scratch -- 44 B per thread written to HBM, most of the kernel's 2.95x write
  * traffic (profiles/r02_c2fir_pmc.json: 198 MB per launch against 67 MB of output); giving that
  * variant 168 VGPRs instead (3 workgroups per CU) removed the spills but cost c2fir 22 %. */
+/* The stereo I / Q exchange between lane l (channel L) and lane l + 32 (channel R) of a wave: with
+ * a = x[r] and b = x[r + 4] of each lane, afterwards a = L's value and b = R's value of the lane's
+ * frame (lane l: frame r, lane l + 32: frame r + 4).  v_permlane32_swap trades the upper half of one
+ * VGPR with the lower half of another on the VALU, two per double, where __shfl_xor(x, 32) took two
+ * ds_bpermute round trips through the LDS plus a select (c2fir kernel 0.331 -> 0.328 ms, c4fir
+ * 3.114 -> 3.084 ms, profiles/r03_fir_swap_ab.jsonl). */
+__device__ __forceinline__ void icw_swap32(double &a, double &b)
+{
+    const unsigned long long ua = __double_as_longlong(a), ub = __double_as_longlong(b);
+    const auto lo = __builtin_amdgcn_permlane32_swap((unsigned)ua, (unsigned)ub, false, false);
+    const auto hi = __builtin_amdgcn_permlane32_swap((unsigned)(ua >> 32), (unsigned)(ub >> 32), false, false);
+    a = __longlong_as_double(((unsigned long long)hi[0] << 32) | lo[0]);
+    b = __longlong_as_double(((unsigned long long)hi[1] << 32) | lo[1]);
+}
+
 /* NC: computed channels (1: mono input, 2: stereo), a template parameter so that each form gets its
  * own register allocation (the mono graph phase holds 8 frames per lane, the stereo one 4) */
-template <bool TRIG, bool TAB, int NC>
-__global__ __launch_bounds__(256, 4) void icw_fir_graph(IcwFirArgs f, IcwK2Args a)
+#if ICW_FIR_STAMPS
+/* diagnostic build only (tools/fir_phases.py): per workgroup of the last KF2 launch, wave 0's
+ * shader-clock stamps at the phase boundaries and the 100 MHz clock at its start and end */
+__device__ unsigned long long icw_fir_stp[(1 << 16) * 8];
+#define ICW_FIR_STAMP(k)                                                                              \
+    do {                                                                                              \
+        if (threadIdx.x == 0 && blockIdx.y * gridDim.x + blockIdx.x < (1u << 16))                     \
+            icw_fir_stp[(blockIdx.y * gridDim.x + blockIdx.x) * 8 + (k)] =                            \
+                ((k) == 0 || (k) == 7) ? __builtin_amdgcn_s_memrealtime() : __builtin_amdgcn_s_memtime(); \
+    } while (0)
+extern "C" int icw_fir_stamps_read(unsigned long long *dst, size_t n)
 {
+    return hipMemcpyFromSymbol(dst, HIP_SYMBOL(icw_fir_stp), n * sizeof(unsigned long long)) == hipSuccess ? 0 : -1;
+}
+#else
+#define ICW_FIR_STAMP(k) do { } while (0)
+#endif
+
+/* ICW_FIR_OCC 5 (96 VGPRs) spills and ran 2.4x slower (profiles/r03_fir_swap_ab.jsonl) */
+template <bool TRIG, bool TAB, int NC>
+__global__ __launch_bounds__(256, ICW_FIR_OCC) void icw_fir_graph(IcwFirArgs f, IcwK2Args a)
+{
+    ICW_FIR_STAMP(0);
+    ICW_FIR_STAMP(1);                                /* diagnostic build: 0 / 7 = 100 MHz clock, 1-6 shader clock */
     extern __shared__ double lds[];
     __shared__ unsigned red_clip[2][ICW_K2_TILE / 64];
     __shared__ double red_pk[2][ICW_K2_TILE / 64];
@@ -1212,12 +1254,18 @@ __global__ __launch_bounds__(256, 4) void icw_fir_graph(IcwFirArgs f, IcwK2Args 
     const int ll = nchc == 2 ? wv * 32 + (lane & 31) : threadIdx.x;   /* lane index within the channel */
     if (nchc == 2) icw_fir_stage<2>(f, s, 0, lds, px, tt, TF, sh, threadIdx.x, 256);
     else icw_fir_stage<1>(f, s, 0, lds, px, tt, TF, sh, threadIdx.x, 256);
+    ICW_FIR_STAMP(2);
     __syncthreads();
+    ICW_FIR_STAMP(3);
     double q[ICW_FIR_R], vi[ICW_FIR_R];
     icw_fir_sums(lds + ch * px, gs, f.nt, ll, av, sh, c, q);
     const int ix = 8 * av + 1;                               /* logical index of x[tt - c] */
 #pragma unroll
     for (int r = 0; r < ICW_FIR_R; ++r) vi[r] = lds[ch * px + icw_fir_phys(ICW_FIR_R * ll + r + ix)];
+#if ICW_FIR_STAMPS
+    if (threadIdx.x == 0 && q[0] + vi[0] == 1.2345e300) icw_fir_stp[0] = 1;     /* the sums before stamp 4 */
+#endif
+    ICW_FIR_STAMP(4);
 
     const IcwProg *P = a.prog;
     IcwRegFile Rf;
@@ -1249,10 +1297,10 @@ __global__ __launch_bounds__(256, 4) void icw_fir_graph(IcwFirArgs f, IcwK2Args 
 #pragma unroll
                 for (int j = 0; j < 2; ++j) {
                     const int r = hh + j;
-                    const double oi = __shfl_xor(ch ? vi[r] : vi[r + 4], 32);
-                    const double oq = __shfl_xor(ch ? q[r] : q[r + 4], 32);
-                    if (ch) { in2[j].lre = oi; in2[j].lim = oq; in2[j].rre = vi[r + 4]; in2[j].rim = q[r + 4]; }
-                    else { in2[j].lre = vi[r]; in2[j].lim = q[r]; in2[j].rre = oi; in2[j].rim = oq; }
+                    double xl = vi[r], xr = vi[r + 4], yl = q[r], yr = q[r + 4];
+                    icw_swap32(xl, xr);
+                    icw_swap32(yl, yr);
+                    in2[j].lre = xl; in2[j].lim = yl; in2[j].rre = xr; in2[j].rim = yr;
                 }
                 int dv2[2][2];
                 icw_chain_frames<TRIG, 2>(a, P, s, tt + fr0 + hh, min(2, max(nf - fr0 - hh, 0)), in2, clip_l, clip_r,
@@ -1263,14 +1311,14 @@ __global__ __launch_bounds__(256, 4) void icw_fir_graph(IcwFirArgs f, IcwK2Args 
         } else {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-            const double oi = __shfl_xor(ch ? vi[r] : vi[r + 4], 32);
-            const double oq = __shfl_xor(ch ? q[r] : q[r + 4], 32);
+            double xl = vi[r], xr = vi[r + 4], yl = q[r], yr = q[r + 4];
+            icw_swap32(xl, xr);
+            icw_swap32(yl, yr);
             const int fr = fr0 + r;
             dv[r][0] = dv[r][1] = 0;
             if (fr < nf) {
                 IcwLR in;
-                if (ch) { in.lre = oi; in.lim = oq; in.rre = vi[r + 4]; in.rim = q[r + 4]; }
-                else { in.lre = vi[r]; in.lim = q[r]; in.rre = oi; in.rim = oq; }
+                in.lre = xl; in.lim = yl; in.rre = xr; in.rim = yr;
                 icw_frame_graph<TRIG, TAB, true>(a, P, Rf, s, tt + fr, in, use_tab, clip_l, clip_r, pk_l, pk_r, dv[r]);
             }
         }
@@ -1384,7 +1432,10 @@ __global__ __launch_bounds__(256, 4) void icw_fir_graph(IcwFirArgs f, IcwK2Args 
             }
         }
     }
+    ICW_FIR_STAMP(5);
     if (a.do_render) icw_meters_wg(a, s, clip_l, clip_r, pk_l, pk_r, red_clip, red_pk);
+    ICW_FIR_STAMP(6);
+    ICW_FIR_STAMP(7);
 }
 
 /* Per-frame rotation table: the Shift / PM factors of frame t depend only on the modulator frame
