@@ -36,7 +36,7 @@ def run(name, frames=1 << 16):
     torch.cuda.synchronize()
     lib = L.load()
     tf = 1024 if W["ch"] == 2 else 2048
-    n_wg = S * ((frames + tf - 1) // tf)
+    n_wg = min(S * ((frames + tf - 1) // tf), 1 << 16)     # the stamp array holds the first 65 536 workgroups
     buf = np.zeros(n_wg * 8, dtype=np.uint64)
     lib.icw_fir_stamps_read.argtypes = [C.c_void_p, C.c_size_t]
     if lib.icw_fir_stamps_read(buf.ctypes.data, buf.size) != 0:
