@@ -659,7 +659,8 @@ def main():
             "metric": "Msamples/s through Hilbert+mod+render",
             "value": value, "unit": "Msamples/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
             "ms_per_step": ms_per_step, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
-            "dtype": "f64", "data": "synthetic",
+            "input_mframes_per_s": value / 2.0,             # input frames/s beside the metric
+            "dtype": "f64", "data": "synthetic, every stream its own generated input (SURVEY 8(d) generator)",
             "config": {"workload": W["desc"],
                        "streams_per_gpu": S, "frames_per_stream_per_step": T, "fs": fs,
                        "parallelism": f"stream-shard x{world}"},
