@@ -1478,8 +1478,12 @@ int icw_process_streams(icw_ctx *c, int first, int count, const void *in, size_t
             c->ev_io.push_back(e);
         }
     }
-    /* every stream starts after everything already queued on st (inputs, previous calls) */
-    if (hipEventRecord(c->join, st) != hipSuccess)
+    /* every stream starts after everything already queued on st (inputs, previous calls); a call
+     * whose kernels all run on st (one launch block: the drop-in) records no event -- the marker
+     * packet sat in front of its kernel on the queue */
+    bool other = false;
+    for (hipStream_t x : {sK, sA, sD, sR, sF, sC}) other = other || (x && x != st);
+    if (other && hipEventRecord(c->join, st) != hipSuccess)
         return ICW_EDEVICE;
     for (hipStream_t x : {sK, sA, sD, sR, sF, sC})
         if (x && x != st && hipStreamWaitEvent(x, c->join, 0) != hipSuccess) return ICW_EDEVICE;
