@@ -16,8 +16,10 @@ barrier + synchronize around the K timed steps, max elapsed over ranks.
 
 --gpus N without a launcher (RANK unset) starts N rank processes itself, before anything here
 touches the GPU, and exits with the worst rank's status; under torch.distributed.run the world
-size must equal --gpus.  With fewer devices than ranks (the 1-GPU box) the ranks share devices
-and use gloo for the barrier and the timing reduce (RCCL needs a GPU per rank).
+size must equal --gpus.  The control plane (barriers, the max-reduce of the elapsed time) runs
+on gloo by default (ICW_BENCH_BACKEND=nccl opts into RCCL, one GPU per rank): the data path has
+no collective, so the 8-GPU run executes the same code as the 2-rank tests.  With fewer devices
+than ranks (the 1-GPU box) the ranks share devices.
 
 --workload picks one of the BASELINE.json configs; the default, c2, is the one the
 headline metric is quoted on.  A default run at N=1 also measures the other configs briefly
@@ -569,6 +571,20 @@ def measure_gpu(wname, streams, frames, steps, warmup, e2e_steps, dev, local_dev
             "fs": fs}
 
 
+def control_backend(ndev, world):
+    """torch.distributed backend of the bench's control plane: the barriers and the one-scalar
+    max-reduce of the elapsed time.  The data path has no collective (north_star: streams are
+    sharded, nothing is exchanged), so the timing needs no RCCL; gloo on the host is the default
+    whatever the device count -- the code the 8-GPU run executes is the code the 2-rank tests run.
+    ICW_BENCH_BACKEND=nccl opts into RCCL, which needs one device per rank."""
+    b = os.environ.get("ICW_BENCH_BACKEND", "gloo")
+    if b not in ("gloo", "nccl"):
+        raise SystemExit(f"bench.py: ICW_BENCH_BACKEND={b!r} (gloo | nccl)")
+    if b == "nccl" and ndev < world:
+        b = "gloo"          # ranks sharing a device (the 1-GPU rehearsal) cannot use RCCL
+    return b
+
+
 def main():
     a = parse()
     if a.workload == "c1":
@@ -587,11 +603,11 @@ def main():
     ndev = torch.cuda.device_count()          # counts without initialising the GPU
     dist = None
     local_dev = local % max(1, ndev)
+    backend = None
     if world > 1:
         import torch.distributed as dist
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        # ranks sharing a device (the 1-GPU rehearsal) cannot use RCCL
-        backend = "gloo" if ndev < world else os.environ.get("ICW_BENCH_BACKEND", "nccl")
+        backend = control_backend(ndev, world)
         torch.cuda.set_device(local_dev)
         dist.init_process_group(backend, rank=rank, world_size=world)
     dev = torch.device("cuda", local_dev)
@@ -663,7 +679,8 @@ def main():
             "dtype": "f64", "data": "synthetic, every stream its own generated input (SURVEY 8(d) generator)",
             "config": {"workload": W["desc"],
                        "streams_per_gpu": S, "frames_per_stream_per_step": T, "fs": fs,
-                       "parallelism": f"stream-shard x{world}"},
+                       "parallelism": f"stream-shard x{world}",
+                       "control_backend": backend},
             "roofline": roof,
             "e2e_host_buffers": e2e,
             "cpu_baseline": cpu,

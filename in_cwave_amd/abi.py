@@ -29,7 +29,7 @@ NSHAPE_MAX = 17
 SEED_LEFT, SEED_RIGHT = 0x13579BDF, 0x479B22AB
 SR_ZERO_SIGNAL_DB = -555.0
 
-F_DEVICE_PTRS, F_DEBUG_PRE, F_TIMING = 1, 2, 4
+F_DEVICE_PTRS, F_DEBUG_PRE, F_TIMING, F_DEBUG_INPUT = 1, 2, 4, 8
 
 
 class Node(C.Structure):
@@ -136,6 +136,11 @@ SIGNATURES = {
     "icw_set_graph": (_i, [_vp, C.POINTER(Node), _i, _i, C.POINTER(_i)]),
     "icw_set_render": (_i, [_vp, C.POINTER(RenderCfg)]),
     "icw_clear_bus_slot": (_i, [_vp, _i]),
+    "icw_graph_del_last": (_i, [_vp]),
+    "icw_graph_del_all": (_i, [_vp]),
+    "icw_graph_add_last": (_i, [_vp, C.POINTER(Node)]),
+    "icw_graph_set_output_plug": (_i, [_vp, _i, _i]),
+    "icw_prepare": (_i, [_vp, _i]),
     "icw_set_hilbert_filter": (_i, [_vp, C.c_uint32]),
     "icw_set_hilbert_config": (_i, [_vp, _i, _i]),
     "icw_fir_taps": (_i, [C.c_int32, C.c_double, _vp, C.c_int]),
@@ -148,6 +153,12 @@ SIGNATURES = {
     "icw_mod_context_seek": (_i, [_vp, C.c_int64, _i]),
     "icw_mod_context_out_size": (_i, [_vp]),
     "icw_mod_context_meters": (_i, [_vp, _i, C.POINTER(Meters)]),
+    "icw_amod_get_clips_peaks": (_i, [C.POINTER(_vp), _i, C.POINTER(C.c_uint), C.POINTER(C.c_uint),
+                                      C.POINTER(C.c_double), C.POINTER(C.c_double), _i]),
+    "icw_amod_del_lastdsp": (_i, [C.POINTER(_vp), _i]),
+    "icw_amod_del_dsplist": (_i, [C.POINTER(_vp), _i]),
+    "icw_amod_add_lastdsp": (_i, [C.POINTER(_vp), _i, C.POINTER(Node)]),
+    "icw_amod_set_output_plug": (_i, [C.POINTER(_vp), _i, _i, _i]),
     "icw_process_batch": (_i, [_vp, _vp, _sz, _vp, _sz, _i, _u, _vp, _vp]),
     "icw_process_streams": (_i, [_vp, _i, _i, _vp, _sz, _vp, _sz, _i, _u, _vp, _vp]),
     "icw_synchronize": (_i, [_vp]),

@@ -4,7 +4,9 @@
  * rendered by the gfx950 kernels (there is no CPU path).
  *
  * Mirrors: mod_context_init / mod_context_fopen (in_cwave.c:46-80, 207-236), the DSP half of
- * amod_process_samples (adv_modulator.c:604-760), amod_get_clips_peaks (adv_modulator.c:445-465).
+ * amod_process_samples (adv_modulator.c:604-760), amod_get_clips_peaks (adv_modulator.c:445-465)
+ * over the decoding contexts, and the DSP-list primitives amod_add_lastdsp / amod_del_lastdsp /
+ * amod_del_dsplist / amod_set_output_plug (adv_modulator.c:360-441) over them.
  */
 #include <stdlib.h>
 #include <string.h>
@@ -40,6 +42,13 @@ icw_mod_context *icw_mod_context_create(const icw_config *cfg, const icw_node *n
         return NULL;
     }
     mc->out_size = 2 * icw_render_size(mc->ctx);
+    rc = icw_prepare(mc->ctx, 0);
+    if (rc != ICW_OK) {
+        icw_destroy(mc->ctx);
+        free(mc);
+        if (status) *status = rc;
+        return NULL;
+    }
     return mc;
 }
 
@@ -99,4 +108,67 @@ int icw_mod_context_meters(icw_mod_context *mc, int reset, icw_meters *m)
 {
     if (!mc) return ICW_EINVAL;
     return icw_get_meters(mc->ctx, 0, reset, m);
+}
+
+int icw_amod_get_clips_peaks(icw_mod_context *const *mcs, int n, unsigned *lc, unsigned *rc, double *lpv,
+                             double *rpv, int is_reset)
+{
+    unsigned cl[2] = {0u, 0u};
+    double pk[2] = {ICW_SR_ZERO_SIGNAL_DB, ICW_SR_ZERO_SIGNAL_DB};
+    int i, ch, st;
+    icw_meters m;
+    if (!mcs || n < 0 || !lc || !rc || !lpv || !rpv) return ICW_EINVAL;
+    /* the reset clears every context first (am.l/r_clips = 0, am.l/r_peak = SR_ZERO_SIGNAL_DB) */
+    if (is_reset)
+        for (i = 0; i < n; ++i)
+            if (mcs[i] && (st = icw_get_meters(mcs[i]->ctx, 0, 1, &m)) != ICW_OK) return st;
+    for (i = 0; i < n; ++i) {
+        if (!mcs[i]) continue;
+        if ((st = icw_get_meters(mcs[i]->ctx, 0, 0, &m)) != ICW_OK) return st;
+        for (ch = 0; ch < 2; ++ch) {
+            cl[ch] += m.clips[ch];
+            if (m.peak_db[ch] > pk[ch]) pk[ch] = m.peak_db[ch];
+        }
+    }
+    *lc = cl[0];
+    *rc = cl[1];
+    *lpv = pk[0];
+    *rpv = pk[1];
+    return ICW_OK;
+}
+
+int icw_amod_del_lastdsp(icw_mod_context *const *mcs, int n)
+{
+    int i, st, rc = ICW_OK;
+    if (!mcs || n < 0) return ICW_EINVAL;
+    for (i = 0; i < n; ++i)
+        if (mcs[i] && (st = icw_graph_del_last(mcs[i]->ctx)) != ICW_OK && rc == ICW_OK) rc = st;
+    return rc;
+}
+
+int icw_amod_del_dsplist(icw_mod_context *const *mcs, int n)
+{
+    int i, st, rc = ICW_OK;
+    if (!mcs || n < 0) return ICW_EINVAL;
+    for (i = 0; i < n; ++i)
+        if (mcs[i] && (st = icw_graph_del_all(mcs[i]->ctx)) != ICW_OK && rc == ICW_OK) rc = st;
+    return rc;
+}
+
+int icw_amod_add_lastdsp(icw_mod_context *const *mcs, int n, const icw_node *node)
+{
+    int i, st, rc = ICW_OK;
+    if (!mcs || n < 0 || !node) return ICW_EINVAL;
+    for (i = 0; i < n; ++i)
+        if (mcs[i] && (st = icw_graph_add_last(mcs[i]->ctx, node)) != ICW_OK && rc == ICW_OK) rc = st;
+    return rc;
+}
+
+int icw_amod_set_output_plug(icw_mod_context *const *mcs, int n, int index, int plug)
+{
+    int i, st, rc = ICW_OK;
+    if (!mcs || n < 0) return ICW_EINVAL;
+    for (i = 0; i < n; ++i)
+        if (mcs[i] && (st = icw_graph_set_output_plug(mcs[i]->ctx, index, plug)) != ICW_OK && rc == ICW_OK) rc = st;
+    return rc;
 }

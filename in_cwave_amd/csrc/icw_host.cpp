@@ -149,6 +149,8 @@ struct icw_ctx {
     size_t d_in_bytes = 0, d_out_bytes = 0;
     double *d_pre = nullptr;
     size_t d_pre_bytes = 0;
+    double *d_xin = nullptr;              /* ICW_F_DEBUG_INPUT: K0's rows of the call, [2*streams][n_frames] */
+    size_t d_xin_bytes = 0;
     /* small host-pointer calls (the one-stream drop-in, 576-frame blocks): inputs and outputs are
      * staged through this pinned buffer, so the copies are asynchronous and the call waits once */
     unsigned char *h_stage = nullptr;
@@ -207,6 +209,7 @@ struct icw_ctx {
     bool s1_ovl = true;                   /* ICW_S1_OVL=0: K5's output phase after the recurrence (A/B) */
     bool chain_ok = true;                 /* ICW_CHAIN=0: chain programs keep the LDS register file (A/B) */
     unsigned long long *s1_stamps = nullptr;   /* ICW_S1_STAMPS=1: K5 phase stamps, printed per call */
+    unsigned long long calls = 0;         /* icw_process_* calls so far (icw_prepare needs a fresh context) */
     std::mutex mu;
 };
 
@@ -522,8 +525,10 @@ void render_consts(const icw_render_cfg &cfg, int is24, IcwRenderK &k)
 /* The normalised list (graph_accept) as the device program: register form, or the bus form when a
  * slot is read before its writer runs.  With frmod_scaled the PM frequencies are scaled from f
  * (dsp_pm) and the Shift ones from |f| (dsp_shift), as DGET_SCALED_FR does per frame. */
-int build_prog(const icw_config &cfg, std::vector<icw_node> &nodes, IcwProg &P)
+int build_prog(const icw_config &cfg, std::vector<icw_node> nodes, IcwProg &P)
 {
+    /* by value: the context keeps the list as given (unscaled), so that the list primitives can edit
+     * and recompile it */
     if (cfg.frmod_scaled)
         for (auto &n : nodes)
             if (n.mode == ICW_MODE_PM)
@@ -715,7 +720,7 @@ void free_all(icw_ctx *c)
 {
     DevState &s = c->st;
     void *ptrs[] = {c->s1_stamps, s.mt, s.mt_idx, s.rs, s.lr_equal, s.fes, s.err, s.hist, s.sncnt, s.hq_phase, s.pos, s.fade,
-                    s.n_frame, s.bus, s.clips, s.peak_bits, c->d_prog, c->trig, c->d_in, c->d_out, c->d_pre,
+                    s.n_frame, s.bus, s.clips, s.peak_bits, c->d_prog, c->trig, c->d_in, c->d_out, c->d_pre, c->d_xin,
                     c->d_fir_g, c->fir_hist[0], c->fir_hist[1]};
     for (void *p : ptrs)
         if (p) (void)hipFree(p);
@@ -820,6 +825,40 @@ int clear_slot(icw_ctx *c, int slot)
     const size_t pitch = (size_t)ICW_N_INPUTS * 4 * sizeof(double);
     return hipMemset2D(c->st.bus + (size_t)slot * 4, pitch, 0, 4 * sizeof(double), (size_t)c->n_streams) == hipSuccess
                ? ICW_OK : ICW_EDEVICE;
+}
+
+/* the device's Hilbert phases of streams [first, ...): [stream][L, R] */
+const uint32_t *ds_phase_of(const icw_ctx *c, int first) { return c->st.hq_phase + (size_t)first * 2; }
+
+/* the output slot replace_output_plug clears for node n (adv_modulator.c:180-205): Shift / PM / Mix
+ * own one, a Master none (-1) */
+int plug_slot(const icw_node &n)
+{
+    return (n.mode == ICW_MODE_SHIFT || n.mode == ICW_MODE_PM || n.mode == ICW_MODE_MIX) ? n.n_out : -1;
+}
+
+/* A live list edit (the caller holds c->mu and has waited for the context's work): compile the
+ * normalised list nv, zero the bus slots the reference's edit clears, then install the program.
+ * The slots are cleared before the program goes to the device, so an error leaves the old program
+ * on both sides. */
+int apply_graph(icw_ctx *c, std::vector<icw_node> &nv, int bypass, const std::vector<int> &clears)
+{
+    icw_config cfg = c->cfg;
+    cfg.bypass_list = bypass;
+    IcwProg P;
+    int rc = build_prog(cfg, nv, P);
+    if (rc) return rc;
+    if (!c->chain_ok) P.chain = 0;
+    const bool serial = needs_serial(cfg, c->rk, P);
+    if (serial && (rc = ensure_render_state(c))) return rc;
+    for (int slot : clears)
+        if (clear_slot(c, slot) != ICW_OK) return ICW_EDEVICE;
+    if (hipMemcpy(c->d_prog, &P, sizeof(IcwProg), hipMemcpyHostToDevice) != hipSuccess) return ICW_EDEVICE;
+    c->cfg.bypass_list = cfg.bypass_list;
+    c->nodes = nv;
+    c->prog = P;
+    c->serial_render = serial;
+    return ICW_OK;
 }
 
 }  // namespace
@@ -1189,28 +1228,73 @@ int icw_set_graph(icw_ctx *c, const icw_node *nodes, int n_nodes, int bypass_lis
     if (!ok) return ICW_EGRAPH;
     std::lock_guard<std::mutex> lk(c->mu);
     if (set_dev(c) || quiesce(c) != hipSuccess) return ICW_EDEVICE;
-    icw_config cfg = c->cfg;
-    cfg.bypass_list = bypass_list ? 1 : 0;
-    IcwProg P;
-    int rc = build_prog(cfg, nv, P);
-    if (rc) return rc;
-    if (!c->chain_ok) P.chain = 0;
-    const bool serial = needs_serial(cfg, c->rk, P);
-    if (serial && (rc = ensure_render_state(c))) return rc;
-    if (hipMemcpy(c->d_prog, &P, sizeof(IcwProg), hipMemcpyHostToDevice) != hipSuccess) return ICW_EDEVICE;
     /* replace_output_plug (adv_modulator.c:176-209) of the removed / re-plugged nodes, matched by
      * position (include/icw.h): their old output slots read zero from now on */
+    std::vector<int> clears;
     for (size_t i = 0; i < c->nodes.size(); ++i) {
         const icw_node &o = c->nodes[i];
         if (o.mode != ICW_MODE_SHIFT && o.mode != ICW_MODE_PM && o.mode != ICW_MODE_MIX) continue;
-        if (i >= nv.size() || nv[i].mode != o.mode || nv[i].n_out != o.n_out)
-            if (clear_slot(c, o.n_out) != ICW_OK) return ICW_EDEVICE;
+        if (i >= nv.size() || nv[i].mode != o.mode || nv[i].n_out != o.n_out) clears.push_back(o.n_out);
     }
-    c->cfg.bypass_list = cfg.bypass_list;
-    c->nodes = nv;
-    c->prog = P;
-    c->serial_render = serial;
-    return ICW_OK;
+    return apply_graph(c, nv, bypass_list ? 1 : 0, clears);
+}
+
+/* the list primitives (include/icw.h): the reference's own edits, each with replace_output_plug's
+ * clear (adv_modulator.c:176-209) and nothing else */
+int icw_graph_del_last(icw_ctx *c)
+{
+    if (!c) return ICW_EINVAL;
+    std::lock_guard<std::mutex> lk(c->mu);
+    if (set_dev(c) || quiesce(c) != hipSuccess) return ICW_EDEVICE;
+    if (c->nodes.size() <= 1) return ICW_OK;                        /* am.tail->prev == NULL */
+    std::vector<icw_node> nv(c->nodes.begin(), c->nodes.end() - 1);
+    std::vector<int> clears;
+    const int r = plug_slot(c->nodes.back());
+    if (r >= 0) clears.push_back(r);
+    return apply_graph(c, nv, c->cfg.bypass_list, clears);
+}
+
+int icw_graph_del_all(icw_ctx *c)
+{
+    if (!c) return ICW_EINVAL;
+    std::lock_guard<std::mutex> lk(c->mu);
+    if (set_dev(c) || quiesce(c) != hipSuccess) return ICW_EDEVICE;
+    if (c->nodes.size() <= 1) return ICW_OK;
+    std::vector<int> clears;
+    for (size_t i = c->nodes.size() - 1; i >= 1; --i) {             /* tail first (adv_modulator.c:364-371) */
+        const int r = plug_slot(c->nodes[i]);
+        if (r >= 0) clears.push_back(r);
+    }
+    std::vector<icw_node> nv(c->nodes.begin(), c->nodes.begin() + 1);
+    return apply_graph(c, nv, c->cfg.bypass_list, clears);
+}
+
+int icw_graph_add_last(icw_ctx *c, const icw_node *node)
+{
+    if (!c || !node) return ICW_EINVAL;
+    if (node->mode == ICW_MODE_MASTER) return ICW_EGRAPH;           /* create_node_dsp: NULL */
+    std::lock_guard<std::mutex> lk(c->mu);
+    std::vector<icw_node> nv(c->nodes);
+    nv.push_back(*node);
+    if (!graph_accept(nv)) return ICW_EGRAPH;
+    if (set_dev(c) || quiesce(c) != hipSuccess) return ICW_EDEVICE;
+    return apply_graph(c, nv, c->cfg.bypass_list, std::vector<int>());
+}
+
+int icw_graph_set_output_plug(icw_ctx *c, int index, int n)
+{
+    if (!c || n < -1 || n >= ICW_N_INPUTS || n == 0) return ICW_EINVAL;
+    std::lock_guard<std::mutex> lk(c->mu);
+    if (index < 0 || index >= (int)c->nodes.size()) return ICW_EINVAL;
+    if (set_dev(c) || quiesce(c) != hipSuccess) return ICW_EDEVICE;
+    std::vector<icw_node> nv(c->nodes);
+    std::vector<int> clears;
+    const int r = plug_slot(nv[index]);
+    if (r >= 0) {
+        clears.push_back(r);
+        if (n >= 0) nv[index].n_out = n;
+    }
+    return apply_graph(c, nv, c->cfg.bypass_list, clears);
 }
 
 int icw_clear_bus_slot(icw_ctx *c, int slot)
@@ -1286,6 +1370,7 @@ int icw_process_streams(icw_ctx *c, int first, int count, const void *in, size_t
     if (n_frames == 0) return ICW_OK;
     std::lock_guard<std::mutex> lk(c->mu);
     if (set_dev(c)) return ICW_EDEVICE;
+    ++c->calls;
     hipStream_t st = hip_stream ? (hipStream_t)hip_stream : c->stream;
     /* A NULL handle with device pointers means the legacy default stream (torch's default stream):
      * the call starts after the work already queued there, and returns when its results are in
@@ -1302,6 +1387,11 @@ int icw_process_streams(icw_ctx *c, int first, int count, const void *in, size_t
     const int osz = 2 * (cfg.need24bits ? 3 : 2);
     const bool dev = flags & ICW_F_DEVICE_PTRS;
     const bool timing = flags & 4u;
+    /* ICW_F_DEBUG_INPUT: K0's output of every launch block is copied aside (test hook, host dbg) */
+    const bool xin = flags & ICW_F_DEBUG_INPUT;
+    if (xin && (dev || !dbg || (flags & ICW_F_DEBUG_PRE) || c->cfg.in_format >= ICW_FMT_CW_F64 || c->fir_M > 0 ||
+                c->cfg.fp_check))
+        return ICW_EINVAL;
     const size_t S = (size_t)count;
     if (!dev && (in_stride < (size_t)n_frames * fsz || out_stride < (size_t)n_frames * osz)) return ICW_EINVAL;
 
@@ -1349,7 +1439,7 @@ int icw_process_streams(icw_ctx *c, int first, int count, const void *in, size_t
     const int n_blocks = (int)blocks.size();
     /* K5 (icw_stream1): one stream, one block, the row recurrence, register-form graph, ROUND / flat */
     const bool s1 = c->stream1 && count == 1 && n_blocks == 1 && !cw && !fcm && k1_mode == 3 && !c->serial_render &&
-                    !bus && n_frames <= ICW_S1_MAX;
+                    !bus && n_frames <= ICW_S1_MAX && !xin;
 
     const unsigned char *d_in;
     unsigned char *d_out;
@@ -1404,7 +1494,24 @@ int icw_process_streams(icw_ctx *c, int first, int count, const void *in, size_t
      * 4-byte aligned inside the output's 16 spare bytes, after the error flag. */
     const bool s1_poll = s1 && zcopy && c->spin_wait && !timing && !c->s1_stamps;
     const size_t done_off = ((stage_in + dos * S + sizeof(int) + 3) & ~(size_t)3) - stage_in;
-    const uint32_t s1_seq = s1_poll ? ++c->s1_seq : 0u;
+    uint32_t s1_seq = 0u;
+    if (s1_poll) {
+        if (++c->s1_seq == 0u) ++c->s1_seq;           /* 0 is never a call's number */
+        s1_seq = c->s1_seq;
+        /* the word sits in the reused staging buffer, where an earlier, larger call may have left
+         * input or output bytes that happen to equal this call's number: store a value that cannot
+         * match before the launch (which orders after this store), so the poll sees only the
+         * kernel's own store */
+        __atomic_store_n((uint32_t *)(c->h_stage + stage_in + done_off), ~s1_seq, __ATOMIC_RELEASE);
+    }
+    std::vector<uint32_t> xin_phase;
+    if (xin) {
+        if (grow((void **)&c->d_xin, &c->d_xin_bytes, S * 2 * (size_t)n_frames * sizeof(double))) return ICW_ENOMEM;
+        xin_phase.resize(S * 2);
+        if (hipMemcpyAsync(xin_phase.data(), ds_phase_of(c, first), S * 2 * sizeof(uint32_t), hipMemcpyDeviceToHost, st) !=
+                hipSuccess || hipStreamSynchronize(st) != hipSuccess)
+            return ICW_EDEVICE;
+    }
     double *d_pre = nullptr;
     if (flags & ICW_F_DEBUG_PRE) {
         if (!dbg) return ICW_EINVAL;
@@ -1582,6 +1689,10 @@ int icw_process_streams(icw_ctx *c, int first, int count, const void *in, size_t
         } else if (icw_launch_unpack(&a0, s0) != hipSuccess) {
             return ICW_EDEVICE;
         }
+        /* test hook: this block's rows aside before K1 may start (K1 waits for k0done) */
+        if (xin && hipMemcpy2DAsync(c->d_xin + a0.t0, (size_t)n_frames * sizeof(double), a0.xd, x_pitch * sizeof(double),
+                                    (size_t)a0.T * sizeof(double), S * 2, hipMemcpyDeviceToDevice, s0) != hipSuccess)
+            return ICW_EDEVICE;
         if (hipEventRecord(c->k0done[p], s0) != hipSuccess) return ICW_EDEVICE;
         return ICW_OK;
     };
@@ -1890,6 +2001,12 @@ int icw_process_streams(icw_ctx *c, int first, int count, const void *in, size_t
             return ICW_EDEVICE;
         if (d_pre && hipMemcpyAsync(dbg, d_pre, S * (size_t)n_frames * 2 * sizeof(double), hipMemcpyDeviceToHost, st) != hipSuccess)
             return ICW_EDEVICE;
+        std::vector<double> rows;
+        if (xin) {
+            rows.resize(S * 2 * (size_t)n_frames);
+            if (hipMemcpyAsync(rows.data(), c->d_xin, rows.size() * sizeof(double), hipMemcpyDeviceToHost, st) != hipSuccess)
+                return ICW_EDEVICE;
+        }
         int e = 0;
         if (pinned) {
             if (s1_poll ? !poll_done((const uint32_t *)(h_out + done_off), s1_seq, st)
@@ -1902,6 +2019,21 @@ int icw_process_streams(icw_ctx *c, int first, int count, const void *in, size_t
             if (hipMemcpy(&e, ds.err, sizeof(int), hipMemcpyDeviceToHost) != hipSuccess) return ICW_EDEVICE;
         }
         if (e) return ICW_EDEVICE;
+        if (xin) {
+            /* the rows hold the channel's signed sample {x, -x, -x, x}[k] at Hilbert phase k (icw_store_frame):
+             * the sign undone is x exactly; a mono call (R = L, the dedup writes the left row only) repeats L */
+            if (hipStreamSynchronize(st) != hipSuccess) return ICW_EDEVICE;
+            double *o = (double *)dbg;
+            for (size_t i = 0; i < S; ++i)
+                for (int ch = 0; ch < 2; ++ch) {
+                    const int rc = nch > 1 ? ch : 0;
+                    const double *r = rows.data() + (i * 2 + rc) * (size_t)n_frames;
+                    for (int t = 0; t < n_frames; ++t) {
+                        const unsigned k = (xin_phase[i * 2 + rc] + (unsigned)t) & 3u;
+                        o[(i * (size_t)n_frames + t) * 2 + ch] = (k == 0u || k == 3u) ? r[t] : -r[t];
+                    }
+                }
+        }
     }
     if (s1 && c->s1_stamps) {
         unsigned long long sp[8];
@@ -1925,6 +2057,39 @@ int icw_process_streams(icw_ctx *c, int first, int count, const void *in, size_t
         c->last_launches[0] = c->last_launches[1] = n_blocks;
     }
     return hipGetLastError() == hipSuccess ? ICW_OK : ICW_EDEVICE;
+}
+
+/* Warm-up of a fresh context (include/icw.h): one call of n_frames frames of digital silence through
+ * the path the context's configuration takes, then the fresh state back (icw_stream_init is exactly
+ * the state icw_create leaves).  What the first call would otherwise pay happens here: the pinned
+ * staging buffer, the device buffers (sized for the widest frame, so a later track's format does
+ * not grow them) and the lazy load of the kernels' code objects on the first launch.  The drop-in
+ * measured 7 ms for its first 576-frame block (BENCH_r03 C1 block_latency_us.first), against
+ * ~113 us for the others. */
+int icw_prepare(icw_ctx *c, int n_frames)
+{
+    if (!c || n_frames < 0) return ICW_EINVAL;
+    if (n_frames == 0) n_frames = ICW_S1_MAX;
+    const size_t S = (size_t)c->n_streams;
+    {
+        std::lock_guard<std::mutex> lk(c->mu);
+        if (c->calls) return ICW_EINVAL;          /* would have to restore state it cannot know */
+        if (set_dev(c)) return ICW_EDEVICE;
+        const size_t widest = 2 * fmt_size(ICW_FMT_CW_F64), osz = 2 * 3;
+        if (grow((void **)&c->d_in, &c->d_in_bytes, (size_t)n_frames * widest * S) ||
+            grow((void **)&c->d_out, &c->d_out_bytes, (size_t)n_frames * osz * S + 16))
+            return ICW_ENOMEM;
+    }
+    const unsigned fsz = fmt_size(c->cfg.in_format) * c->cfg.in_channels;
+    const size_t osz = 2 * (size_t)(c->cfg.need24bits ? 3 : 2);
+    std::vector<unsigned char> in((size_t)n_frames * fsz * S, 0), out((size_t)n_frames * osz * S);
+    if (c->cfg.in_format == ICW_FMT_U8) std::fill(in.begin(), in.end(), (unsigned char)0x80);   /* u8 silence */
+    int rc = icw_process_streams(c, 0, (int)S, in.data(), (size_t)n_frames * fsz, out.data(), (size_t)n_frames * osz,
+                                 n_frames, 0u, nullptr, nullptr);
+    if (rc == ICW_OK) rc = icw_stream_init(c, 0, (int)S);
+    std::lock_guard<std::mutex> lk(c->mu);
+    c->calls = 0;
+    return rc;
 }
 
 int icw_process_batch(icw_ctx *c, const void *in, size_t in_stride, void *out, size_t out_stride, int n_frames,
@@ -2002,6 +2167,13 @@ int icw_n_frame(icw_ctx *c, int s, uint64_t *nf)
     unsigned long long v = 0;
     if (hipMemcpy(&v, c->st.n_frame + s, sizeof(v), hipMemcpyDeviceToHost) != hipSuccess) return ICW_EDEVICE;
     *nf = v;
+    /* the host mirror decides whether the fused FIR kernel may take every Shift / PM factor from the
+     * shared table (in_step): a device-side write it did not follow would give the stream another
+     * stream's rotation, so a divergence fails this read loudly */
+    if (c->nf_host[s] != v) {
+        fprintf(stderr, "icw_n_frame: stream %d frame counter %llu, host mirror %llu\n", s, v, c->nf_host[s]);
+        return ICW_EDEVICE;
+    }
     return ICW_OK;
 }
 

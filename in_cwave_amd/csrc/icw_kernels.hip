@@ -1679,11 +1679,18 @@ __global__ __launch_bounds__(ICW_K2_TILE) void icw_stream1(IcwS1Args a)
         __syncthreads();
         stamp(3);
     }
+    if (a.adv.done) {
+        /* every wave waits for its own zero-copy output stores to be acknowledged before the barrier
+         * (a workgroup-scope release need not wait on vmcnt outside threadgroup-split mode), so thread
+         * 0's system-scope fence below covers the whole workgroup's output, not only wave 0's */
+        __builtin_amdgcn_s_waitcnt(0);
+        __syncthreads();
+    }
     if (threadIdx.x == 0) {
         icw_advance_stream(a.adv, 0);
         if (a.adv.done) {
-            /* the workgroup's output stores are in L2 (the barrier's release); write them and the
-             * flag back to host memory, then the call's sequence number the host polls for */
+            /* write the output and the error flag back to host memory, then the call's sequence
+             * number the host polls for */
             __threadfence_system();
             __hip_atomic_store(a.adv.done, a.adv.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         }

@@ -160,6 +160,30 @@ class Context:
         """mod_context_clear_all_inouts for every stream (icw_clear_bus_slot): slot 0..26 to zero"""
         _check(self._lib.icw_clear_bus_slot(self.h, int(slot)), "icw_clear_bus_slot")
 
+    def graph_del_last(self):
+        """amod_del_lastdsp (icw_graph_del_last): the tail goes, its output slot is cleared"""
+        _check(self._lib.icw_graph_del_last(self.h), "icw_graph_del_last")
+
+    def graph_del_all(self):
+        """amod_del_dsplist (icw_graph_del_all): every node but the Master, each slot cleared"""
+        _check(self._lib.icw_graph_del_all(self.h), "icw_graph_del_all")
+
+    def graph_add_last(self, node):
+        """amod_add_lastdsp + the GUI's field writes (icw_graph_add_last); False if refused"""
+        rc = self._lib.icw_graph_add_last(self.h, C.byref(node))
+        if rc == abi.EGRAPH:
+            return False
+        _check(rc, "icw_graph_add_last")
+        return True
+
+    def graph_set_output_plug(self, index, n):
+        """amod_set_output_plug (icw_graph_set_output_plug): node `index`'s slot to n (-1: clear only)"""
+        _check(self._lib.icw_graph_set_output_plug(self.h, int(index), int(n)), "icw_graph_set_output_plug")
+
+    def prepare(self, n_frames=0):
+        """icw_prepare: warm a fresh context (one call of silence, then the fresh state back)"""
+        _check(self._lib.icw_prepare(self.h, int(n_frames)), "icw_prepare")
+
     def set_render(self, render):
         """srenders_set_vcfg for every stream (icw_set_render): an abi.RenderCfg"""
         _check(self._lib.icw_set_render(self.h, C.byref(render)), "icw_set_render")
@@ -201,6 +225,19 @@ class Context:
                                              out.strides[0], n_frames, flags, _ptr(pre), None),
                "icw_process_streams")
         return out, pre
+
+    def unpacked_input(self, inp, n_frames, first=0, count=None):
+        """Test hook (ICW_F_DEBUG_INPUT): process like `process` and return float64 [count, n_frames, 2],
+        the unpacked, faded samples K0 hands the Hilbert converters (pre-Hilbert, R = L for mono)"""
+        count = self.n_streams - first if count is None else count
+        inp = np.ascontiguousarray(inp)
+        assert inp.dtype == np.uint8 and inp.shape[0] == count and inp.shape[1] >= n_frames * self.fsz
+        out = np.zeros((count, n_frames * 2 * self.render_size), dtype=np.uint8)
+        x = np.zeros((count, n_frames, 2), dtype=np.float64)
+        in_stride = inp.strides[0] if count > 1 else inp.shape[1]
+        _check(self._lib.icw_process_streams(self.h, first, count, _ptr(inp), in_stride, _ptr(out), out.strides[0],
+                                             n_frames, abi.F_DEBUG_INPUT, _ptr(x), None), "icw_process_streams")
+        return x, out
 
     def process_device(self, d_in, in_stride, d_out, out_stride, n_frames, first=0, count=None,
                        timing=False, hip_stream=None):

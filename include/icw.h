@@ -140,7 +140,9 @@ typedef struct icw_config {
                                      the render (sound_render.c:403-489, 815-903); icw_get_fp_census */
 } icw_config;
 
-/* Per-stream meters (the reference keeps them global in `am`, adv_modulator.c:54-56). */
+/* Per-stream meters.  The reference keeps one set, global in `am` (adv_modulator.c:54-56), that
+ * both decoding contexts feed (adv_modulator.c:757-758); icw_amod_get_clips_peaks (icw_amod.h)
+ * combines the per-context meters into it: clips summed, peaks maxed, a reset clearing all. */
 typedef struct icw_meters {
     uint32_t clips[2];            /* InterlockedIncrement'ed clip counters, sound_render.c:782-795 */
     double   peak_db[2];          /* max 20*log10(|q|/hi_bound), SR_ZERO_SIGNAL_DB if silent */
@@ -153,6 +155,10 @@ typedef struct icw_ctx icw_ctx;
 #define ICW_F_DEVICE_PTRS  1u     /* in/out are device pointers already resident in HBM */
 #define ICW_F_DEBUG_PRE    2u     /* also write the 2 pre-render doubles/frame to dbg (tests) */
 #define ICW_F_TIMING       4u     /* time the kernels with HIP events (icw_last_timing) */
+#define ICW_F_DEBUG_INPUT  8u     /* tests: write the unpacked, faded samples the Hilbert converters get
+                                     (what xwave_unpack_csample hands hq_rp_process, xwave_reader.c:
+                                     974-998; R = L for mono) to dbg as double[n_streams][n_frames][2]:
+                                     real input through the quadrature IIR, host pointers only */
 
 /* Create a context for n_streams streams on HIP device `device` (-1: current device).
  * The DSP list is normalised exactly as amod_init (adv_modulator.c:216-331) does; a list it
@@ -198,7 +204,8 @@ int icw_set_input(icw_ctx *ctx, uint32_t sample_rate, uint32_t fmt, uint32_t cha
  *                    the old one by position: an old Shift / PM / Mix node whose position is gone,
  *                    now holds a node of another mode, or whose n_out changed has its old slot
  *                    zeroed for every stream.  Edits that position matching cannot see (a re-plug to
- *                    the same slot, delete + add of an identical node) call icw_clear_bus_slot.
+ *                    the same slot, delete + add of an identical node) are the list primitives below:
+ *                    a host that binds the GUI forwards each primitive as it happens, not a diff.
  * icw_clear_bus_slot <- mod_context_clear_all_inouts (in_cwave.c:255-261): bus slot 0..26 of
  *                    every stream to zero (the 4 doubles L re/im, R re/im).
  * icw_set_render  <- srenders_set_vcfg (in_cwave.c:457-469) -> sound_render_setup
@@ -213,6 +220,29 @@ int icw_set_input(icw_ctx *ctx, uint32_t sample_rate, uint32_t fmt, uint32_t cha
  *                    subnormal reject; the rings stay, the de-subnorm counters restart. */
 int icw_set_graph(icw_ctx *ctx, const icw_node *nodes, int n_nodes, int bypass_list, int *accepted);
 int icw_clear_bus_slot(icw_ctx *ctx, int slot);
+
+/* The list primitives one by one, each with exactly the reference's bus clearing -- no position
+ * matching.  replace_output_plug (adv_modulator.c:176-209) clears a Shift / PM / Mix node's OLD
+ * output slot in every stream, also when it is re-plugged to the same slot; a Master clears nothing.
+ *   icw_graph_del_last      <- amod_del_lastdsp (adv_modulator.c:378-390): the tail node goes and
+ *                              its slot is cleared; a list of the Master alone is left as it is.
+ *   icw_graph_del_all       <- amod_del_dsplist (adv_modulator.c:360-374): tail first, down to the
+ *                              Master, each removed node's slot cleared.
+ *   icw_graph_add_last      <- amod_add_lastdsp (adv_modulator.c:394-411) followed by the GUI's
+ *                              field writes of the new node (amod_gui_control.c:1858): `node` is
+ *                              appended after the tail, its L/R locks fanned out as amod_init does;
+ *                              nothing is cleared.  A Master is refused (create_node_dsp, :112-123):
+ *                              ICW_EGRAPH.
+ *   icw_graph_set_output_plug <- amod_set_output_plug (adv_modulator.c:436-441, the GUI's plug
+ *                              selector amod_gui_control.c:1125): node `index` (0 = the head) gets
+ *                              output slot n (1..26), or keeps its slot with n = -1 ("remove only");
+ *                              either way its old slot is cleared.
+ * The field writes of existing nodes (gains, frequencies, inputs, locks) and the bypass flag clear
+ * nothing: icw_set_graph with the same structure. */
+int icw_graph_del_last(icw_ctx *ctx);
+int icw_graph_del_all(icw_ctx *ctx);
+int icw_graph_add_last(icw_ctx *ctx, const icw_node *node);
+int icw_graph_set_output_plug(icw_ctx *ctx, int index, int n);
 int icw_set_render(icw_ctx *ctx, const icw_render_cfg *render);
 int icw_set_hilbert_filter(icw_ctx *ctx, uint32_t type);
 int icw_set_hilbert_config(icw_ctx *ctx, int kahan, int subnorm_reject);
@@ -254,6 +284,14 @@ int icw_process_batch(icw_ctx *ctx, const void *in, size_t in_stride_bytes, void
 int icw_process_streams(icw_ctx *ctx, int first, int count, const void *in,
                         size_t in_stride_bytes, void *out, size_t out_stride_bytes,
                         int n_frames, unsigned flags, void *dbg, void *hip_stream);
+
+/* Warm a FRESH context (no call made yet) for calls of up to n_frames frames per stream (0: 4096,
+ * the longest one-launch call of one stream): one call of silence through the path its
+ * configuration takes, then the fresh state back (icw_stream_init).  The pinned staging, the device
+ * buffers and the lazily loaded kernel code objects are then in place, so the first real call costs
+ * what the later ones do -- the DecodeThread's first block (playback.c:619) included.
+ * icw_mod_context_create calls it.  ICW_EINVAL once a call has been made. */
+int icw_prepare(icw_ctx *ctx, int n_frames);
 
 int icw_synchronize(icw_ctx *ctx);
 /* Pinned (page-locked) host memory for a call's in / out buffers: their copies then overlap the

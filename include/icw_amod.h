@@ -27,7 +27,9 @@ extern "C" {
 typedef struct icw_mod_context icw_mod_context;
 
 /* mod_context_init (in_cwave.c:46-80) + amod_init (adv_modulator.c:216-331).
- * Returns NULL on failure (*status holds the ICW_E* code). */
+ * Returns NULL on failure (*status holds the ICW_E* code).  The context is warmed (icw_prepare: one
+ * call of silence, then the fresh state back), so the DecodeThread's first block (playback.c:619)
+ * costs what the others do. */
 icw_mod_context *icw_mod_context_create(const icw_config *cfg, const icw_node *nodes, int n_nodes,
                                         int device, int *status);
 void icw_mod_context_destroy(icw_mod_context *mc);
@@ -55,6 +57,36 @@ int icw_mod_context_out_size(const icw_mod_context *mc);
 /* amod_get_clips_peaks (adv_modulator.c:445-465): reset clears the clips / peaks first and returns
  * the cleared values, as the reference does; the de-subnorm count is kept. */
 int icw_mod_context_meters(icw_mod_context *mc, int reset, icw_meters *m);
+
+/* amod_get_clips_peaks (adv_modulator.c:445-465) exactly: the reference keeps ONE set of meters in
+ * its `am` singleton (adv_modulator.c:54-55), and every decoding context renders into it
+ * (sound_render_value(&buf, lOut, &am.l_clips, &am.l_peak, ...), adv_modulator.c:757-758) -- the
+ * playback and the transcode context alike (in_cwave.h:473-474).  Here each context keeps its own;
+ * this call combines the n contexts the host decodes with into the reference's one set:
+ *   - is_reset != 0 clears every context's clips and peaks FIRST and returns the cleared values
+ *     (0 clips, ICW_SR_ZERO_SIGNAL_DB), as the reference clears am before reading it;
+ *   - *lc / *rc: the clip counts summed over the contexts (unsigned, wrapping as the reference's
+ *     InterlockedIncrement'ed counters wrap);
+ *   - *lpv / *rpv: the largest peak in dB over the contexts (each context's samples in dB against
+ *     its own render's bound, sound_render.c:769-780: the max over all samples, whichever context).
+ * The de-subnorm counters are per context (mod_context_get_desubnorm_counter, in_cwave.c:300-310)
+ * and stay with icw_mod_context_meters.  Pass NULL entries to skip a context that is not open. */
+int icw_amod_get_clips_peaks(icw_mod_context *const *mcs, int n, unsigned *lc, unsigned *rc, double *lpv,
+                             double *rpv, int is_reset);
+
+/* The DSP-list primitives over the decoding contexts: the reference's list is one (am.head, shared
+ * by both contexts, adv_modulator.c:51-52), and replace_output_plug clears the removed / re-plugged
+ * node's old slot in every context (mod_context_clear_all_inouts, in_cwave.c:255-261).  Each applies
+ * the icw.h primitive of the same name to every non-NULL context; the first error is returned.
+ *   icw_amod_del_lastdsp      <- amod_del_lastdsp       (adv_modulator.c:378-390)
+ *   icw_amod_del_dsplist      <- amod_del_dsplist       (adv_modulator.c:360-374)
+ *   icw_amod_add_lastdsp      <- amod_add_lastdsp + the GUI's field writes (adv_modulator.c:394-411)
+ *   icw_amod_set_output_plug  <- amod_set_output_plug   (adv_modulator.c:436-441): list node
+ *                                `index` (0 = the Master at the head), slot n or -1 (clear only) */
+int icw_amod_del_lastdsp(icw_mod_context *const *mcs, int n);
+int icw_amod_del_dsplist(icw_mod_context *const *mcs, int n);
+int icw_amod_add_lastdsp(icw_mod_context *const *mcs, int n, const icw_node *node);
+int icw_amod_set_output_plug(icw_mod_context *const *mcs, int n, int index, int plug);
 
 /* The context's one-stream icw_ctx, for the live edits of icw.h (icw_set_graph, icw_set_render,
  * icw_set_hilbert_filter / _config): the reference's GUI applies each edit to both decoding

@@ -461,6 +461,11 @@ typedef struct orc_stream {
     int64_t pos, n_samples, n_fade_in, n_fade_out;
     uint32_t clips[2];
     double peak[2];
+    /* the meters render_value updates: this stream's own clips / peak, or another stream's when
+     * orc_share_meters makes them one accumulator -- the reference's single am.l/r_clips and
+     * am.l/r_peak, which every decoding context feeds (adv_modulator.c:54-55, 757-758) */
+    uint32_t *am_clips;
+    double *am_peak;
 } orc_stream;
 
 static double unpack1(const unsigned char *p, unsigned fmt)
@@ -521,6 +526,20 @@ static void unpack_iq(const unsigned char *p, unsigned fmt, double *vI, double *
         *vQ = le_f32(p + 4);
         break;
     }
+}
+
+/* test hooks: n samples of real format fmt at src -> the scaled doubles unpack1 gives (pre-fade),
+ * and n complex samples of CWAVE format fmt -> I / Q (tests/test_reader_pinned.py pins both against
+ * the reference's own unpack_lsb.h, compiled by `make -C oracle ref`) */
+static unsigned fmt_size(unsigned fmt);
+void orc_unpack_real(unsigned fmt, const unsigned char *src, size_t n, double *dst)
+{
+    for (size_t i = 0; i < n; ++i) dst[i] = unpack1(src + i * fmt_size(fmt), fmt);
+}
+
+void orc_unpack_cw(unsigned fmt, const unsigned char *src, size_t n, double *vI, double *vQ)
+{
+    for (size_t i = 0; i < n; ++i) unpack_iq(src + i * fmt_size(fmt), fmt, vI + i, vQ + i);
 }
 
 /* HRW_FMT_* sample sizes and CWAVE cw_slen (xwave_reader.c:246-252) */
@@ -655,6 +674,8 @@ orc_stream *orc_stream_new(const icw_config *cfg, const icw_node *nodes, int n_n
     render_init(&s->rd[1], &cfg->render, cfg->need24bits, cfg->seed_right);
     s->rd[0].fes.on = s->rd[1].fes.on = cfg->fp_check != 0;
     s->peak[0] = s->peak[1] = ICW_SR_ZERO_SIGNAL_DB;
+    s->am_clips = s->clips;
+    s->am_peak = s->peak;
     s->n_samples = INT64_MAX / 4;
     return s;
 }
@@ -710,6 +731,56 @@ int orc_set_graph(orc_stream *s, const icw_node *nodes, int n_nodes, int bypass)
     s->n_nodes = n_nodes;
     s->cfg.bypass_list = bypass ? 1 : 0;
     return 1;
+}
+
+/* The list primitives themselves, as the GUI calls them (amod_gui_control.c:1125, 1165, 1172,
+ * 1858), one at a time.  replace_output_plug (adv_modulator.c:176-209): a Shift / PM / Mix node's
+ * old output slot is cleared -- also when it is re-plugged to the same slot, and with n = -1 the
+ * node keeps its n_out but the slot is cleared all the same; a Master clears nothing. */
+static void replace_output_plug(orc_stream *s, icw_node *n, int to)
+{
+    int nrem = -1;
+    if (n->mode == ICW_MODE_SHIFT || n->mode == ICW_MODE_PM || n->mode == ICW_MODE_MIX) {
+        nrem = n->n_out;
+        if (to >= 0) n->n_out = to;
+    }
+    if (nrem >= 0) orc_clear_inout(s, nrem);
+}
+
+/* amod_del_lastdsp (adv_modulator.c:378-390): the head (Master) stays */
+void orc_del_lastdsp(orc_stream *s)
+{
+    if (s->n_nodes > 1) {
+        --s->n_nodes;
+        replace_output_plug(s, &s->nodes[s->n_nodes], -1);
+    }
+}
+
+/* amod_del_dsplist (adv_modulator.c:360-374): tail first, down to the head */
+void orc_del_dsplist(orc_stream *s)
+{
+    while (s->n_nodes > 1) orc_del_lastdsp(s);
+}
+
+/* amod_add_lastdsp (adv_modulator.c:394-411) and the GUI's field writes of the new node (a Master
+ * cannot be created there: create_node_dsp returns NULL, :112-123); the L/R locks are applied as
+ * amod_init applies them.  Returns 0 if refused. */
+int orc_add_lastdsp(orc_stream *s, const icw_node *node)
+{
+    icw_node tmp[64];
+    if (!node || node->mode == ICW_MODE_MASTER || s->n_nodes >= 64) return 0;
+    memcpy(tmp, s->nodes, sizeof(icw_node) * (size_t)s->n_nodes);
+    tmp[s->n_nodes] = *node;
+    if (!graph_accept(tmp, s->n_nodes + 1)) return 0;
+    s->nodes[s->n_nodes] = tmp[s->n_nodes];
+    ++s->n_nodes;
+    return 1;
+}
+
+/* amod_set_output_plug (adv_modulator.c:436-441) on node `index` of the list */
+void orc_set_output_plug(orc_stream *s, int index, int to)
+{
+    if (index >= 0 && index < s->n_nodes) replace_output_plug(s, &s->nodes[index], to);
 }
 
 /* srenders_set_vcfg (in_cwave.c:457-469) -> sound_render_setup (sound_render.c:625-629): copy the
@@ -934,16 +1005,38 @@ int orc_process(orc_stream *s, const void *in, unsigned n_frames, void *out, dou
             }
         }
         if (pre) { pre[2 * f] = lOut; pre[2 * f + 1] = rOut; }
-        render_value(&op, lOut, &s->clips[0], &s->peak[0], &s->rd[0]);
-        render_value(&op, rOut, &s->clips[1], &s->peak[1], &s->rd[1]);
+        render_value(&op, lOut, &s->am_clips[0], &s->am_peak[0], &s->rd[0]);
+        render_value(&op, rOut, &s->am_clips[1], &s->am_peak[1], &s->rd[1]);
     }
     return (int)n_frames;
 }
 
+/* s renders into owner's meters from now on (owner: s itself to separate them again): the two
+ * decoding contexts of the reference, the.mc_playback and the.mc_transcode (in_cwave.h:473-474),
+ * both pass &am.l_clips / &am.l_peak ... to sound_render_value (adv_modulator.c:757-758) */
+void orc_share_meters(orc_stream *s, orc_stream *owner)
+{
+    s->am_clips = owner->clips;
+    s->am_peak = owner->peak;
+}
+
+/* amod_get_clips_peaks (adv_modulator.c:445-465) on the accumulator s renders into: with reset
+ * the clips and peaks are cleared first and the cleared values read back */
+void orc_get_clips_peaks(orc_stream *s, int reset, icw_meters *m)
+{
+    if (reset) {
+        s->am_clips[0] = s->am_clips[1] = 0;
+        s->am_peak[0] = s->am_peak[1] = ICW_SR_ZERO_SIGNAL_DB;
+    }
+    m->clips[0] = s->am_clips[0]; m->clips[1] = s->am_clips[1];
+    m->peak_db[0] = s->am_peak[0]; m->peak_db[1] = s->am_peak[1];
+    m->desubnorm = s->hq[0].I.sncnt + s->hq[0].Q.sncnt + s->hq[1].I.sncnt + s->hq[1].Q.sncnt;
+}
+
 void orc_get_meters(orc_stream *s, icw_meters *m)
 {
-    m->clips[0] = s->clips[0]; m->clips[1] = s->clips[1];
-    m->peak_db[0] = s->peak[0]; m->peak_db[1] = s->peak[1];
+    m->clips[0] = s->am_clips[0]; m->clips[1] = s->am_clips[1];
+    m->peak_db[0] = s->am_peak[0]; m->peak_db[1] = s->am_peak[1];
     m->desubnorm = s->hq[0].I.sncnt + s->hq[0].Q.sncnt + s->hq[1].I.sncnt + s->hq[1].Q.sncnt;
 }
 

@@ -56,6 +56,13 @@ def load():
         lib.orc_set_graph.argtypes = [vp, C.POINTER(abi.Node), C.c_int, C.c_int]
         lib.orc_set_render.argtypes = [vp, C.POINTER(abi.RenderCfg)]
         lib.orc_clear_inout.argtypes = [vp, C.c_int]
+        lib.orc_share_meters.argtypes = [vp, vp]
+        lib.orc_get_clips_peaks.argtypes = [vp, C.c_int, C.POINTER(abi.Meters)]
+        lib.orc_del_lastdsp.argtypes = [vp]
+        lib.orc_del_dsplist.argtypes = [vp]
+        lib.orc_add_lastdsp.restype = C.c_int
+        lib.orc_add_lastdsp.argtypes = [vp, C.POINTER(abi.Node)]
+        lib.orc_set_output_plug.argtypes = [vp, C.c_int, C.c_int]
         lib.orc_set_hilbert_filter.argtypes = [vp, C.c_uint]
         lib.orc_set_hilbert_config.argtypes = [vp, C.c_int, C.c_int]
         lib.orc_set_fir.restype = C.c_int
@@ -116,6 +123,34 @@ class Stream:
     def clear_bus_slot(self, slot):
         """mod_context_clear_all_inouts (in_cwave.c:255-261): bus slot `slot` to zero"""
         load().orc_clear_inout(self.h, int(slot))
+
+    def del_lastdsp(self):
+        """amod_del_lastdsp (adv_modulator.c:378-390), with replace_output_plug's clear"""
+        load().orc_del_lastdsp(self.h)
+
+    def del_dsplist(self):
+        """amod_del_dsplist (adv_modulator.c:360-374)"""
+        load().orc_del_dsplist(self.h)
+
+    def add_lastdsp(self, node):
+        """amod_add_lastdsp (adv_modulator.c:394-411) + the GUI's field writes; False if refused"""
+        return bool(load().orc_add_lastdsp(self.h, C.byref(node)))
+
+    def set_output_plug(self, index, n):
+        """amod_set_output_plug (adv_modulator.c:436-441) on list node `index` (n = -1: clear only)"""
+        load().orc_set_output_plug(self.h, int(index), int(n))
+
+    def share_meters(self, owner):
+        """render into owner's clips / peaks: the reference's one `am` accumulator that both decoding
+        contexts feed (adv_modulator.c:54-55, 757-758); owner = self separates them again"""
+        load().orc_share_meters(self.h, owner.h)
+        self._meters_owner = owner           # keeps the accumulator's memory alive
+
+    def clips_peaks(self, reset=False):
+        """amod_get_clips_peaks (adv_modulator.c:445-465) of the accumulator this stream feeds"""
+        m = abi.Meters()
+        load().orc_get_clips_peaks(self.h, int(bool(reset)), C.byref(m))
+        return {"clips": (m.clips[0], m.clips[1]), "peak_db": (m.peak_db[0], m.peak_db[1])}
 
     def set_render(self, render):
         """srenders_set_vcfg"""

@@ -5,6 +5,8 @@ import subprocess
 import sys
 from pathlib import Path
 
+import pytest
+
 ROOT = Path(__file__).resolve().parents[1]
 sys.path.insert(0, str(ROOT))
 
@@ -60,3 +62,19 @@ def test_roofline_inputs_from_committed_profiles():
     # the issue floor's cycles per VALU: the Kahan add chain of the committed latency probe
     cfl, src = bench.fp64_issue_floor()
     assert src == "r01_fp64_latency_probe.txt" and 3.5 < cfl < cpv
+
+
+def test_control_backend_defaults_to_gloo(monkeypatch):
+    """the bench's control plane (barriers, the elapsed-time max-reduce) is gloo whatever the
+    device count, so an 8-GPU run executes the code the 2-rank tests run; RCCL only on request and
+    only with one device per rank"""
+    import bench
+    monkeypatch.delenv("ICW_BENCH_BACKEND", raising=False)
+    assert bench.control_backend(8, 8) == "gloo"
+    assert bench.control_backend(1, 2) == "gloo"
+    monkeypatch.setenv("ICW_BENCH_BACKEND", "nccl")
+    assert bench.control_backend(8, 8) == "nccl"
+    assert bench.control_backend(1, 2) == "gloo"
+    monkeypatch.setenv("ICW_BENCH_BACKEND", "mpi")
+    with pytest.raises(SystemExit):
+        bench.control_backend(8, 8)

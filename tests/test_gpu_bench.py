@@ -64,6 +64,8 @@ def test_bench_gpus_flag_self_launches():
     assert r.returncode == 0, r.stderr[-3000:]
     d = _line(r.stdout)
     assert d["n_gpus"] == 2
+    # the control plane the 8-GPU run uses too: gloo, whatever the device count (bench.control_backend)
+    assert d["config"]["control_backend"] == "gloo"
     assert abs(d["value"] - 2.0 * 2 * 64 * 32768 / (d["ms_per_step"] / 1e3) / 1e6) < 1e-6 * d["value"]
     assert d["roofline"]["avg_launch_ms"] > 0 and 0 < d["roofline"]["frac"] < 1
     cpu = d["cpu_baseline"]

@@ -158,6 +158,8 @@ def test_fir_state_roundtrip(oracle, icw):
     b.set_fir_hilbert(510, BETA)
     for s in range(2):
         b.set_state(s, blobs[s])
+    for s in range(2):
+        assert b.n_frame(s) == a.n_frame(s) == 2500      # set_state moves the host mirror too
     out, pre = b.process(np.ascontiguousarray(raw[:, 2500 * 4:]), 2500, want_pre=True)
     assert np.array_equal(pre.view(np.uint64), refp[:, 2500:].view(np.uint64))
     assert np.array_equal(out, ref[:, 2500 * 4:])
@@ -235,6 +237,10 @@ def test_fir_subset_calls_keep_other_streams_history(oracle, icw, monkeypatch):
             assert np.array_equal(pre[i].view(np.uint64), rp.view(np.uint64)), (k, s)
             assert np.array_equal(out[i], ro), (k, s)
             pos[s] += n
+        # the host mirror of the frame counters (in_step) follows every subset call: icw_n_frame
+        # fails loudly on a divergence
+        for s in range(S):
+            assert ctx.n_frame(s) == refs[s].n_frame(), (k, s)
     ctx.close()
 
 

@@ -116,6 +116,30 @@ def test_stream1_polled_completion(oracle, icw, fmt, ch, b24, spin, monkeypatch)
     ctx.close()
 
 
+def test_stream1_stale_completion_word(oracle, icw, monkeypatch):
+    """the completion word lives in the reused staging buffer.  A ramp input (frame n =
+    (L = n, R = 0): the little-endian word n) in two 4000-frame calls (sequence numbers 1, 2) leaves
+    word 3 at byte 12, where a 1-frame call (number 3: 4 B in, 4 B out, the word at 8 + 4) polls.  The
+    host stores a value that cannot match before the launch, so the call returns the kernel's output,
+    not the stale bytes."""
+    monkeypatch.setenv("ICW_SPIN", "1")
+    monkeypatch.setenv("ICW_STREAM1", "1")
+    monkeypatch.setenv("ICW_K1_MODE", "row")
+    cfg = graph.default_config(44100)
+    nodes = graph.graph_shift_master()
+    ctx = icw.Context(cfg, nodes, 1)
+    ref = oracle.Stream(cfg, nodes)
+    ramp = np.zeros((1, 4000, 2), np.int16)
+    ramp[0, :, 0] = np.arange(4000)
+    ramp = ramp.view(np.uint8).reshape(1, -1)
+    for n, seg in ((4000, ramp), (4000, ramp), (1, ramp[:, :4]), (2, ramp[:, 8:16]), (1, ramp[:, 4:8])):
+        out, _ = ctx.process(np.ascontiguousarray(seg), n)
+        ro, _ = ref.process(np.ascontiguousarray(seg[0]), n)
+        assert np.array_equal(out[0], ro), n
+    assert ctx.n_frame(0) == ref.n_frame()
+    ctx.close()
+
+
 @pytest.mark.parametrize("ovl", ["1", "0"])
 @pytest.mark.parametrize("kind", ["shift_master", "pm_shift_mix", "long_chain", "random"])
 @pytest.mark.parametrize("ch", [1, 2])

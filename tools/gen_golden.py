@@ -4,6 +4,10 @@
 Reference-pinned (produced from the reference's own files / reference-built code):
   mt19937ar_kat.json   -- the reference's known-answer data (test_mt_jrnd/mt19937ar_out.c:
                           init_by_array {0x123,0x234,0x345,0x456}, first 1000 genrand_int32)
+  unpack_ref.npz       -- the REFERENCE's unpack_int16/24/32/float/double (unpack_lsb.h:53-125) on
+                          random and edge-case bytes (oracle/_ref/libref_unpack.so: oracle/ref_unpack.c
+                          compiled with -I /root/reference/src, no stand-in headers)
+  cwave_layout.json    -- sizeof / offsetof of HCWAVE_V1 / V2 and the HCW_* constants of cwave.h
   mt_ref_seeds.npz     -- outputs of the REFERENCE mt_jrnd.c (oracle/_ref/libref_mt.so, compiled
                           from /root/reference/src/mersene_twister/mt_jrnd.c by oracle/Makefile)
                           for the two render seeds 0x13579BDF / 0x479B22AB (in_cwave.c:69-70):
@@ -89,6 +93,55 @@ def crc_ref():
     (GOLD / "crc32_ref.json").write_text(json.dumps(doc, indent=1) + "\n")
 
 
+# edge-case patterns per unpacker, little-endian values: i24 sign extension, integer extremes,
+# signed zeros, infinities, quiet / signalling / negative NaNs with payloads, denormals
+UNPACK_EDGES = {
+    "i16": [0x0000, 0x0001, 0x7FFF, 0x8000, 0x8001, 0xFFFF, 0x00FF, 0xFF00],
+    "i24": [0x000000, 0x000001, 0x7FFFFF, 0x800000, 0x800001, 0xFFFFFF, 0x00FF80, 0xFF007F],
+    "i32": [0, 1, 0x7FFFFFFF, 0x80000000, 0x80000001, 0xFFFFFFFF, 0x00008000, 0xFFFF8000],
+    "f32": [0x00000000, 0x80000000, 0x7F800000, 0xFF800000, 0x7FC00000, 0x7FA00001, 0xFFC00123, 0xFF800001,
+            0x00000001, 0x007FFFFF, 0x80000001, 0x807FFFFF, 0x00800000, 0x3F800000, 0xBF800000, 0x7F7FFFFF],
+    "f64": [0, 1 << 63, 0x7FF0000000000000, 0xFFF0000000000000, 0x7FF8000000000000, 0x7FF4000000000001,
+            0xFFF8000000000123, 0x0000000000000001, 0x000FFFFFFFFFFFFF, 0x8000000000000001,
+            0x0010000000000000, 0x3FF0000000000000, 0x40DFFFC000000000, 0xC0E0000000000000, 0x7FEFFFFFFFFFFFFF],
+}
+UNPACK_KINDS = {"i16": (0, 2), "i24": (1, 3), "i32": (2, 4), "f32": (3, 4), "f64": (4, 8)}
+
+
+def unpack_ref():
+    """the REFERENCE's LE unpackers (unpack_lsb.h:53-125) and CWAVE header layout (cwave.h:31-87),
+    compiled where they lie by oracle/Makefile (`ref`: oracle/ref_unpack.c includes them), run on
+    random bytes (numpy.random.default_rng(53), 1024 samples per kind) followed by the edge cases"""
+    lib = C.CDLL(str(ROOT / "oracle/_ref/libref_unpack.so"))
+    lib.ref_unpack_batch.argtypes = [C.c_int, C.c_void_p, C.c_size_t, C.c_void_p]
+    lib.ref_cwave_layout.argtypes = [C.c_void_p, C.c_int]
+    lib.ref_cwave_magic.restype = C.c_char_p
+    rng = np.random.default_rng(53)
+    out = {}
+    for name, (kind, size) in UNPACK_KINDS.items():
+        rnd = rng.integers(0, 256, 1024 * size, dtype=np.uint8)
+        edge = np.concatenate([np.frombuffer(int(v).to_bytes(size, "little"), np.uint8) for v in UNPACK_EDGES[name]])
+        raw = np.ascontiguousarray(np.concatenate([rnd, edge]))
+        n = raw.size // size
+        val = np.zeros(n, dtype=np.uint64 if name == "f64" else (np.uint32 if name == "f32" else np.int32))
+        assert lib.ref_unpack_batch(kind, raw.ctypes.data, n, val.ctypes.data) == 0
+        out[name + "_bytes"] = raw
+        out[name + "_val"] = val
+    np.savez_compressed(GOLD / "unpack_ref.npz", **out)
+    lay = np.zeros(64, dtype=np.int64)
+    m = lib.ref_cwave_layout(lay.ctypes.data, lay.size)
+    fields = ["sizeof", "magic", "hsize", "version", "format", "n_channels", "n_samples", "sample_rate", "k_M"]
+    doc = {"generator": "oracle/ref_unpack.c on cwave.h (reference, compiled where it lies)",
+           "HCWAVE_V1": dict(zip(fields + ["pad0", "k_beta"], map(int, lay[0:11]))),
+           "HCWAVE_V2": dict(zip(fields + ["n_CRC32", "k_beta"], map(int, lay[11:22]))),
+           "HCW_VERSION": dict(zip(["BAD", "V1", "V2", "CUR"], map(int, lay[22:26]))),
+           "HCW_FMT": dict(zip(["BAD_FMT", "PCM_DBL64", "PCM_INT16", "PCM_INT16_FLT32", "PCM_FLT32"],
+                               map(int, lay[26:31]))),
+           "HCW_MAGIC": lib.ref_cwave_magic().decode()}
+    assert m == 31
+    (GOLD / "cwave_layout.json").write_text(json.dumps(doc, indent=1) + "\n")
+
+
 def e2e():
     from in_cwave_amd import abi, graph, synth
     from oracle import oracle as O
@@ -147,5 +200,6 @@ if __name__ == "__main__":
         kat()
         ref_seeds()
         crc_ref()
+        unpack_ref()
     e2e()
     print("golden fixtures written to", GOLD)
