@@ -98,6 +98,19 @@ int icw_nodes_from_ref(const NODE_DSP *head, icw_node *nodes, int max_nodes)
     return n;
 }
 
+void icw_node_from_ref(const NODE_DSP *nd, icw_node *out)
+{
+    node_from_ref(nd, out);
+}
+
+int icw_node_index(const NODE_DSP *nd)
+{
+    int i = 0;
+    for (; nd && nd->prev; nd = nd->prev)        /* the head (Master) has no prev */
+        ++i;
+    return i;
+}
+
 int icw_fmt_from_reader(const XWAVE_READER *xr)
 {
     unsigned f;

@@ -12,6 +12,7 @@
  *                        (adv_modulator.c:56, amod_get_bypass_list_flag in_cwave.h:624)
  *   icw_nodes_from_ref   a NODE_DSP list (in_cwave.h:273-287, MAKE_* :207-269), head first along
  *                        ->next, as amod_init walks it (adv_modulator.c:231-296)
+ *   icw_node_from_ref    one NODE_DSP; icw_node_index its list position along ->prev
  *   icw_fmt_from_reader  XWAVE_READER (in_cwave.h:375-405): type, spec.rwave.format (HRW_FMT_*,
  *                        :324-330) or spec.cwave.header.format (HCW_FMT_*, cwave.h:70-80)
  *   cfg_to_icw           the two above in one call, as INTEGRATION.md 1 uses it
@@ -31,6 +32,12 @@ int icw_config_from_ref(const IN_CWAVE_CFG *cfg, BOOL bypass_list, unsigned samp
  * ICW_EINVAL if the list is longer.  Locks are copied, not applied: icw_create applies them
  * exactly as amod_init does. */
 int icw_nodes_from_ref(const NODE_DSP *head, icw_node *nodes, int max_nodes);
+
+/* One node (for icw_graph_add_last / icw_amod_add_lastdsp after amod_add_lastdsp and the GUI's
+ * field writes), and a node's position in its list along ->prev (0 = the head), for
+ * icw_amod_set_output_plug (amod_set_output_plug takes the node itself, adv_modulator.c:436-441) */
+void icw_node_from_ref(const NODE_DSP *nd, icw_node *out);
+int icw_node_index(const NODE_DSP *nd);
 
 /* ICW_FMT_* of an open reader, or ICW_EINVAL for a format libicw does not take */
 int icw_fmt_from_reader(const XWAVE_READER *xr);

@@ -163,6 +163,7 @@ struct IcwProg {
  * (sound_render.c:499-581), so pow() runs once on the CPU exactly as in the reference. */
 struct IcwRenderK {
     double norm_mul, dth_mul, hi, lo, round_offset;
+    double clip_abs;               /* min(hi, -lo): a q with |q| below it clips at neither bound */
     int32_t sign_delta, norm_shift, is24;
     int32_t render_type, ns_kind, ns_n;
     double ns_c[40];

@@ -513,6 +513,7 @@ void render_consts(const icw_render_cfg &cfg, int is24, IcwRenderK &k)
         k.norm_mul = 1.0 / (double)(1ULL << k.norm_shift);
     }
     k.lo -= (double)k.sign_delta;
+    k.clip_abs = std::min(k.hi, -k.lo);
     k.is24 = is24;
     k.render_type = (int)cfg.render_type;
     unsigned t = cfg.nshape_type > ICW_NSHAPE_MAX ? ICW_NSHAPE_FLAT : cfg.nshape_type;

@@ -221,11 +221,17 @@ __global__ __launch_bounds__(256) void icw_unpack_frames(IcwK0Args a)
  * window at the same phase of that pattern, so all offsets inside a block are immediates.  Taps past
  * the last multiple of 8 run one at a time. */
 #define ICW_FIR_R 8                                  /* outputs per lane */
+#ifndef ICW_FIR_VEC
+#define ICW_FIR_VEC 1                                /* FIR staging: 16-byte loads, one LDS base per thread */
+#endif
 #ifndef ICW_FIR_INTERIOR
 #define ICW_FIR_INTERIOR 1                           /* FIR staging: the interior tiles' short form */
 #endif
 #ifndef ICW_FIR_OCC
 #define ICW_FIR_OCC 4                                /* KF2 workgroups per CU the register budget is sized for */
+#endif
+#ifndef ICW_FIR_CUT
+#define ICW_FIR_CUT 0                                /* diagnostic: 1 no graph, 2 no sums either (VALU by phase) */
 #endif
 #ifndef ICW_FIR_STAMPS
 #define ICW_FIR_STAMPS 0                             /* diagnostic: KF2 phase stamps (tools/fir_phases.py) */
@@ -264,6 +270,65 @@ __device__ __forceinline__ void icw_fir_stage_t(const IcwFirArgs &f, int s, int 
     /* 8 consecutive frames per thread and pass, their loads issued together (clamped in range,
      * selected after): the staging is load-latency bound otherwise */
     constexpr int V = 8;
+    /* An interior tile of a packed typed format (i16 / i32 / f32, the file frame exactly the computed
+     * channels): a thread's 8 frames are 8 * frame-size contiguous bytes, read by 16-byte loads from
+     * one address, unpacked from the registers (the same conversions as icw_unpack_f), and written to
+     * 8 consecutive LDS doubles per channel (logical 8t..8t+7 sit at physical 9t..9t+7) from one base.
+     * Only the threads at the ends of the staged range select zeros.  With M >= 32 every frame a
+     * thread loads lies in [0, T) (tt >= M + sh, and the last load ends 30 frames past the tile's
+     * outputs, tt + nout <= T - M).  The per-frame address, clamp and select of the general form were
+     * most of the staging's VALU instructions (c2fir: ~150 per wave). */
+    if constexpr (ICW_FIR_VEC && AL && (FMT == ICW_FMT_I16 || FMT == ICW_FMT_I32 || FMT == ICW_FMT_F32)) {
+        constexpr int CS = FMT == ICW_FMT_I16 ? 2 : 4;
+        constexpr int FB = NC * CS;                       /* bytes per frame */
+        constexpr int NW = V * FB / 4;                    /* 32-bit words per thread and pass */
+        const unsigned char *b0 = src + (size_t)(tt - M - sh) * f.fsz;
+        if (nofade && !need_hist && tt + nf <= T - M && M >= 32 && f.fsz == FB && !((uintptr_t)b0 & 15)) {
+            const int lim = sh + M + nf;                  /* logical [sh, lim) holds inputs, the rest zeros */
+            for (int i0 = tid * V; i0 < nl; i0 += nthr * V) {
+                const uint4 *p = (const uint4 *)(b0 + (size_t)i0 * FB);
+                uint32_t w[NW];
+#pragma unroll
+                for (int k = 0; k < NW / 4; ++k) {
+                    const uint4 q4 = p[k];
+                    w[4 * k] = q4.x; w[4 * k + 1] = q4.y; w[4 * k + 2] = q4.z; w[4 * k + 3] = q4.w;
+                }
+                double v[NC][V];
+#pragma unroll
+                for (int e = 0; e < V; ++e) {
+#pragma unroll
+                    for (int k = 0; k < NC; ++k) {
+                        const int si = e * NC + k;            /* sample index in the thread's run */
+                        if constexpr (FMT == ICW_FMT_I16) {
+                            const uint32_t u = w[si >> 1];
+                            v[k][e] = (double)((si & 1) ? ((int)u >> 16) : (int)(short)(u & 0xffffu));
+                        } else if constexpr (FMT == ICW_FMT_I32) {
+                            v[k][e] = ((double)(int)w[si]) / 65536.0;
+                        } else {
+                            v[k][e] = 32768.0 * (double)__uint_as_float(w[si]);
+                        }
+                    }
+                }
+                double *d = xs + icw_fir_phys(i0);
+                if (i0 >= sh && i0 + V <= lim) {
+#pragma unroll
+                    for (int k = 0; k < NC; ++k)
+#pragma unroll
+                        for (int e = 0; e < V; ++e) d[k * px + e] = v[k][e];
+                } else {
+#pragma unroll
+                    for (int e = 0; e < V; ++e) {
+                        const int i = i0 + e;
+                        if (i < nl) {
+#pragma unroll
+                            for (int k = 0; k < NC; ++k) d[k * px + e] = (i >= sh && i < lim) ? v[k][e] : 0.0;
+                        }
+                    }
+                }
+            }
+            return;
+        }
+    }
     if (ICW_FIR_INTERIOR && NC == 2 && nofade && !need_hist && tt + nf <= T - M) {
         /* an interior tile (most of them): no fade, no history to read or write -- a frame is its
          * input inside [tt - M, tt + nf) and zero outside (c2fir +3 %, c4fir +3 %; the mono form
@@ -636,13 +701,39 @@ __device__ __forceinline__ int icw_clamp_int(double q, const IcwRenderK &k, unsi
     return (int)fmax(fmin(q, k.hi - 1.0), k.lo + 1.0);
 }
 
+/* The q of sound_render_value for ROUND render + flat shaper (sound_render.c:747-767): x * norm_mul
+ * - prev_ns_err (0.0) + rnd * dth_mul (0.0 * dth_mul = +0.0), then +- round_offset by the sign.
+ * x - 0.0 is x; the + 0.0, and a mid-riser's +- 0.0 (round_offset 0, sign_delta -1), change only a
+ * zero's sign, which nothing downstream sees -- the peak takes fabs, the clip stage compares and
+ * truncates, and (int) +-0.0 is 0 -- so they are not executed; a mid-tread's +- 0.5 of a -0.0 is +0.5
+ * either way (-0.0 < 0 is false).  A norm_mul of 1.0 (16 sign bits) is not multiplied: x is a sum
+ * or product, never a signalling NaN, and x * 1.0 is x. */
+__device__ __forceinline__ double icw_round_in(double x, const IcwRenderK &k, int &delta)
+{
+    if (k.norm_mul != 1.0) x = x * k.norm_mul;
+    if (k.sign_delta) {
+        delta = x < 0.0 ? k.sign_delta : 0;
+        return x;
+    }
+    return icw_round_q(x, k.round_offset, k.sign_delta, delta);
+}
+
+/* the rendered integer of one channel-sample (ROUND + flat), q for the caller's meters */
+__device__ __forceinline__ int icw_render_round_q(double input, const IcwRenderK &k, double &q)
+{
+    int delta;
+    q = icw_round_in(input, k, delta);
+    /* x86 cvttsd2si semantics: NaN -> INT_MIN ("integer indefinite") */
+    const int vc = (int)fmax(fmin(q, k.hi - 1.0), k.lo + 1.0);   /* icw_clamp_int without the counts */
+    const int v = isnan(q) ? (int)0x80000000 : vc;
+    return (v + delta) << k.norm_shift;
+}
+
 /* sound_render_value for ROUND render + flat shaper (sound_render.c:691-809): elementwise */
 __device__ __forceinline__ int icw_render_round(double input, const IcwRenderK &k, unsigned &clips, double &pk)
 {
-    input = (input * k.norm_mul) - 0.0;           /* prev_ns_err == 0.0 for the flat shaper */
-    double q = input + (0.0 * k.dth_mul);         /* rnd_dth == 0.0 for ROUND */
     int delta;
-    q = icw_round_q(q, k.round_offset, k.sign_delta, delta);
+    const double q = icw_round_in(input, k, delta);
     pk = fmax(pk, fabs(q));
     /* x86 cvttsd2si semantics: NaN -> INT_MIN ("integer indefinite") */
     const int vc = icw_clamp_int(q, k, clips);    /* unconditional: a NaN counts no clip */
@@ -871,23 +962,38 @@ __device__ __forceinline__ IcwOpK icw_op_k(const IcwOp &op)
  * the op's fields are read once for the R frames and their rotation factors (the per-frame table,
  * every stream in step) are loaded together before the arithmetic.  Per frame the arithmetic of
  * icw_frame_graph + icw_exec_op in the same order, so the bits are the same; the rendered integers
- * go to dv (0 for frames past the block). */
-template <bool TRIG, int R>
+ * go to dv (0 for frames past the block).
+ * ROWP: the caller knows where the R frames' table rows are -- frame r's row at
+ * a.trig_tab + tro_u + r * tro_step + tro_lane, the first two wave-uniform, the last the lane's (KF2's
+ * lanes hold consecutive frames of a tile inside the block, icw_fir_graph) -- so a load needs no
+ * per-frame index arithmetic and no clamp.
+ * Three shortcuts, each exact: a gain of 1.0 is not multiplied (x * 1.0 is x for every value that is
+ * not a signalling NaN, and d is a sum or a converted input here, never one); the bus writes of the
+ * block's last frame are tested once per call (one lane of the launch holds it); and the clip
+ * counters take one compare per call -- a clip needs |q| >= min(hi, -lo) (clip_abs), so only a call
+ * whose largest |q| reaches that counts its samples one by one (a NaN q clips nothing, and fmax
+ * passes it over, as the per-sample compares did). */
+template <bool TRIG, int R, bool ROWP = false>
 __device__ __forceinline__ void icw_chain_frames(const IcwK2Args &a, const IcwProg *P, int s, int t0, int nv,
                                                  const IcwLR (&in)[R], unsigned &clip_l, unsigned &clip_r,
-                                                 double &pk_l, double &pk_r, int (&dv)[R][2])
+                                                 double &pk_l, double &pk_r, int (&dv)[R][2], uint32_t tro_lane = 0,
+                                                 size_t tro_u = 0, size_t tro_step = 0)
 {
     const int T = a.T;
     double *bus_s = a.bus + (size_t)s * ICW_N_INPUTS * 4;
+    const int lastr = T - 1 - t0;                    /* the block's last frame is frame lastr here */
+    const bool has_last = lastr >= 0 && lastr < nv;
     IcwLR prev[R];
     double lOut[R], rOut[R];
 #pragma unroll
     for (int r = 0; r < R; ++r) {
         prev[r] = in[r];
         lOut[r] = rOut[r] = 0.0;
-        if (r < nv && t0 + r == T - 1) {
-            bus_s[0] = in[r].lre; bus_s[1] = in[r].lim; bus_s[2] = in[r].rre; bus_s[3] = in[r].rim;
-        }
+    }
+    if (has_last) {
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+            if (r == lastr) { bus_s[0] = in[r].lre; bus_s[1] = in[r].lim; bus_s[2] = in[r].rre; bus_s[3] = in[r].rim; }
     }
     const bool bypass = P->bypass != 0;
     for (int oi = 0; oi < P->n_ops; ++oi) {
@@ -898,7 +1004,8 @@ __device__ __forceinline__ void icw_chain_frames(const IcwK2Args &a, const IcwPr
 #pragma unroll
             for (int r = 0; r < R; ++r) {
                 /* (cos, sin) of a channel: one 16-byte load (rows and columns are 16-byte aligned) */
-                const double *trow = a.trig_tab + icw_trig_index(min(t0 + r, T - 1), a.trig_perm_q) * a.trig_pitch;
+                const double *trow = ROWP ? a.trig_tab + tro_u + (size_t)r * tro_step + tro_lane
+                                          : a.trig_tab + icw_trig_index(min(t0 + r, T - 1), a.trig_perm_q) * a.trig_pitch;
                 const double2 f0 = k.act0 ? *(const double2 *)(trow + k.ts0 * 2) : make_double2(0.0, 0.0);
                 const double2 f1 = k.act1 ? *(const double2 *)(trow + k.ts1 * 2) : make_double2(0.0, 0.0);
                 cs[r][0] = f0.x; sn[r][0] = f0.y;
@@ -931,8 +1038,8 @@ __device__ __forceinline__ void icw_chain_frames(const IcwK2Args &a, const IcwPr
             }
             if (k.iq0) { xt = d.lre; d.lre = d.lim; d.lim = xt; }
             if (k.iq1) { xt = d.rre; d.rre = d.rim; d.rim = xt; }
-            d.lre *= k.g0; d.lim *= k.g0;
-            d.rre *= k.g1; d.rim *= k.g1;
+            if (k.g0 != 1.0) { d.lre *= k.g0; d.lim *= k.g0; }
+            if (k.g1 != 1.0) { d.rre *= k.g1; d.rim *= k.g1; }
             if (k.mode == ICW_MODE_MASTER) {
                 lOut[r] = icw_master(k.tout0, d.lre, d.lim);
                 rOut[r] = icw_master(k.tout1, d.rre, d.rim);
@@ -944,22 +1051,38 @@ __device__ __forceinline__ void icw_chain_frames(const IcwK2Args &a, const IcwPr
                 if (k.act1) icw_rot(d.rre, d.rim, cs[r][1], sn[r][1], o.rre, o.rim);
             }
             prev[r] = o;
-            if (k.wb >= 0 && r < nv && t0 + r == T - 1) {
-                double *b = bus_s + k.wb * 4;
-                b[0] = o.lre; b[1] = o.lim; b[2] = o.rre; b[3] = o.rim;
-            }
+        }
+        if (k.mode != ICW_MODE_MASTER && k.wb >= 0 && has_last) {
+            double *b = bus_s + k.wb * 4;
+#pragma unroll
+            for (int r = 0; r < R; ++r)
+                if (r == lastr) { b[0] = prev[r].lre; b[1] = prev[r].lim; b[2] = prev[r].rre; b[3] = prev[r].rim; }
         }
     }
+    const IcwRenderK &rk = a.rk;
+    double q[R][2], lm_l = 0.0, lm_r = 0.0;
 #pragma unroll
     for (int r = 0; r < R; ++r) {
         dv[r][0] = dv[r][1] = 0;
+        q[r][0] = q[r][1] = 0.0;
         if (r < nv) {
             if (a.pre) {
                 double *p = a.pre + (size_t)s * a.pre_stride + (size_t)(t0 + r) * 2;
                 p[0] = lOut[r]; p[1] = rOut[r];
             }
-            dv[r][0] = icw_render_round(lOut[r], a.rk, clip_l, pk_l);
-            dv[r][1] = icw_render_round(rOut[r], a.rk, clip_r, pk_r);
+            dv[r][0] = icw_render_round_q(lOut[r], rk, q[r][0]);
+            dv[r][1] = icw_render_round_q(rOut[r], rk, q[r][1]);
+            lm_l = fmax(lm_l, fabs(q[r][0]));
+            lm_r = fmax(lm_r, fabs(q[r][1]));
+        }
+    }
+    pk_l = fmax(pk_l, lm_l);
+    pk_r = fmax(pk_r, lm_r);
+    if (fmax(lm_l, lm_r) >= rk.clip_abs) {
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            clip_l += (q[r][0] >= rk.hi ? 1u : 0u) + (q[r][0] <= rk.lo ? 1u : 0u);
+            clip_r += (q[r][1] >= rk.hi ? 1u : 0u) + (q[r][1] <= rk.lo ? 1u : 0u);
         }
     }
 }
@@ -1258,7 +1381,12 @@ __global__ __launch_bounds__(256, ICW_FIR_OCC) void icw_fir_graph(IcwFirArgs f, 
     __syncthreads();
     ICW_FIR_STAMP(3);
     double q[ICW_FIR_R], vi[ICW_FIR_R];
+#if ICW_FIR_CUT >= 2
+#pragma unroll
+    for (int r = 0; r < ICW_FIR_R; ++r) q[r] = 0.0;
+#else
     icw_fir_sums(lds + ch * px, gs, f.nt, ll, av, sh, c, q);
+#endif
     const int ix = 8 * av + 1;                               /* logical index of x[tt - c] */
 #pragma unroll
     for (int r = 0; r < ICW_FIR_R; ++r) vi[r] = lds[ch * px + icw_fir_phys(ICW_FIR_R * ll + r + ix)];
@@ -1266,6 +1394,16 @@ __global__ __launch_bounds__(256, ICW_FIR_OCC) void icw_fir_graph(IcwFirArgs f, 
     if (threadIdx.x == 0 && q[0] + vi[0] == 1.2345e300) icw_fir_stp[0] = 1;     /* the sums before stamp 4 */
 #endif
     ICW_FIR_STAMP(4);
+#if ICW_FIR_CUT
+    /* diagnostic build only (VALU accounting by phase): no graph, no render */
+    {
+        double acc = 0.0;
+#pragma unroll
+        for (int r = 0; r < ICW_FIR_R; ++r) acc += q[r] + vi[r];
+        if (acc == 1.2345e300) a.out[threadIdx.x] = 1;
+        return;
+    }
+#endif
 
     const IcwProg *P = a.prog;
     IcwRegFile Rf;
@@ -1290,7 +1428,14 @@ __global__ __launch_bounds__(256, ICW_FIR_OCC) void icw_fir_graph(IcwFirArgs f, 
         const int fr0 = ICW_FIR_R * ll + h;
         if (ICW_CHAIN4 && P->chain && (TAB || !TRIG) && !a.iq_out && a.do_render) {
             /* chain program, factors from the table (or none): the four frames op by op, two per
-             * pass (four at once spill at 128 VGPRs), each pass's I / Q exchange just before it */
+             * pass (four at once spill at 128 VGPRs), each pass's I / Q exchange just before it.
+             * Frame tt + fr0 + hh + j (tt a multiple of 8, fr0 = 8 ll + h) sits in table row
+             * (h + hh + j) q + tt / 8 + ll (icw_trig_index, q = trig_perm_q): a per-lane part and a
+             * uniform one.  The last tile of a launch block keeps the clamped index (frames past
+             * the block would point past the table). */
+            const bool rowp = TRIG && tt + TF <= f.T;
+            const size_t pq = (size_t)a.trig_perm_q * a.trig_pitch;
+            const uint32_t tro_lane = (uint32_t)(((size_t)h * a.trig_perm_q + (size_t)(tt >> 3) + ll) * a.trig_pitch);
 #pragma unroll
             for (int hh = 0; hh < 4; hh += 2) {
                 IcwLR in2[2];
@@ -1303,8 +1448,12 @@ __global__ __launch_bounds__(256, ICW_FIR_OCC) void icw_fir_graph(IcwFirArgs f, 
                     in2[j].lre = xl; in2[j].lim = yl; in2[j].rre = xr; in2[j].rim = yr;
                 }
                 int dv2[2][2];
-                icw_chain_frames<TRIG, 2>(a, P, s, tt + fr0 + hh, min(2, max(nf - fr0 - hh, 0)), in2, clip_l, clip_r,
-                                          pk_l, pk_r, dv2);
+                if (rowp)
+                    icw_chain_frames<TRIG, 2, true>(a, P, s, tt + fr0 + hh, min(2, max(nf - fr0 - hh, 0)), in2, clip_l,
+                                                    clip_r, pk_l, pk_r, dv2, tro_lane, (size_t)hh * pq, pq);
+                else
+                    icw_chain_frames<TRIG, 2>(a, P, s, tt + fr0 + hh, min(2, max(nf - fr0 - hh, 0)), in2, clip_l, clip_r,
+                                              pk_l, pk_r, dv2);
                 dv[hh][0] = dv2[0][0]; dv[hh][1] = dv2[0][1];
                 dv[hh + 1][0] = dv2[1][0]; dv[hh + 1][1] = dv2[1][1];
             }
@@ -1373,6 +1522,10 @@ __global__ __launch_bounds__(256, ICW_FIR_OCC) void icw_fir_graph(IcwFirArgs f, 
         const int fr0 = ICW_FIR_R * ll;
         const bool b24 = a.rk.is24;
         unsigned w[ICW_FIR_R / 2 * 3];               /* packed output: 16-bit frames in w[0..8) */
+        /* table rows as in the stereo form: frame tt + 8 ll + hh + j at row (hh + j) q + tt / 8 + ll */
+        const bool rowp = TRIG && tt + TF <= f.T;
+        const size_t pq = (size_t)a.trig_perm_q * a.trig_pitch;
+        const uint32_t tro_lane = (uint32_t)(((size_t)(tt >> 3) + ll) * a.trig_pitch);
 #pragma unroll
         for (int hh = 0; hh < ICW_FIR_R; hh += 2) {
             IcwLR in2[2];
@@ -1382,8 +1535,12 @@ __global__ __launch_bounds__(256, ICW_FIR_OCC) void icw_fir_graph(IcwFirArgs f, 
                 in2[r].lim = in2[r].rim = q[hh + r];
             }
             int dv[2][2];
-            icw_chain_frames<TRIG, 2>(a, P, s, tt + fr0 + hh, min(2, max(nf - fr0 - hh, 0)), in2, clip_l, clip_r, pk_l,
-                                      pk_r, dv);
+            if (rowp)
+                icw_chain_frames<TRIG, 2, true>(a, P, s, tt + fr0 + hh, min(2, max(nf - fr0 - hh, 0)), in2, clip_l, clip_r,
+                                                pk_l, pk_r, dv, tro_lane, (size_t)hh * pq, pq);
+            else
+                icw_chain_frames<TRIG, 2>(a, P, s, tt + fr0 + hh, min(2, max(nf - fr0 - hh, 0)), in2, clip_l, clip_r, pk_l,
+                                          pk_r, dv);
             if (b24) {
                 const unsigned l0 = (unsigned)dv[0][0] & 0xffffffu, r0 = (unsigned)dv[0][1] & 0xffffffu;
                 const unsigned l1 = (unsigned)dv[1][0] & 0xffffffu, r1 = (unsigned)dv[1][1] & 0xffffffu;
@@ -2256,23 +2413,47 @@ struct IcwRowNs {
     double one;
 };
 
-/* one sample at unroll step J (0..ICW_MAX_NS_TAPS-1); rings of R slots, the newest at J mod R */
-template <int KIND, int NN, int R, int J>
+/* one sample at unroll step J (0..ICW_MAX_NS_TAPS-1); rings of R slots, the newest at J mod R.
+ *
+ * The integer never sits on the error-feedback chain.  The reference forms val = (int)q' + delta
+ * (q' the clipped q, sound_render.c:782-797) and feeds back ev = (double)val - input (:800).  q' lies
+ * in [lo + 1, hi - 1] (|q'| < 2^24) and delta is 0 or -1, so (double)val = trunc(q') + (double)delta
+ * exactly -- an integer-valued sum of two integers, no rounding; the trunc of a negative q' in (-1, 0)
+ * is -0.0, and -0.0 + 0.0 = +0.0 = (double)0, -0.0 + -1.0 = -1.0 = (double)-1.  A NaN q (only from a
+ * NaN input, which makes ev NaN either way) clamps to a number here; its stored value is fixed up in
+ * the flush from the staged q, as the reference's (int)NaN = INT_MIN (cvttsd2si) + delta 0.  The
+ * double val (vst) is converted to the integer off the chain, in the flush.
+ * MR: mid-riser (round_offset 0, sign_delta -1: sound_render_recalc, sound_render.c:527-540) -- the
+ * rounding add q + (+-0.0) changes nothing but a -0.0 (to +0.0), which neither the clip stage, the
+ * peak (fabs) nor trunc + delta can tell apart, so it is skipped and only delta's select remains,
+ * beside the clamp.  Mid-tread (round_offset 0.5, sign_delta 0): q +- 0.5 by the sign of q, both
+ * sums formed beside the compare, delta 0.
+ * The FIR shaper's first term 0.0 + c0 * ev (ns_fir, sound_render.c:420-427: the sum starts at 0.0)
+ * is one fma(c0, ev, +0.0): the exact product plus +0.0, rounded once, is round(c0 * ev) with a
+ * zero's sign made +, exactly what 0.0 + round(c0 * ev) gives.  On the chain per sample: the input
+ * and q, clamp (2), trunc, + delta, ev, the fma and the shaper's DPP sum -- 16 ops for MEW44 where
+ * the integer round trip and the rounding's compare / select / add made it 23. */
+template <int KIND, int NN, int R, int J, bool MR>
 __device__ __forceinline__ void icw_rrow_step(double x, double d, double &prev_err, double (&E)[R], double (&O)[R],
                                               double (&P)[R], double (&P2)[R], const IcwRowNs &c,
-                                              const IcwRenderK &k, double *qst, int *vst)
+                                              const IcwRenderK &k, double *qst, double *vst)
 {
     constexpr int S = J % R;
     const double input = (x * k.norm_mul) - prev_err;
     double q = input + d;
-    int delta;
-    q = icw_round_q(q, k.round_offset, k.sign_delta, delta);
+    double dd;                                         /* (double)delta */
+    if constexpr (MR) {
+        dd = q < 0.0 ? -1.0 : 0.0;
+    } else {
+        const double qa = q + 0.5, qb = q - 0.5;       /* q + round_offset, q - round_offset */
+        q = q < 0.0 ? qb : qa;
+        dd = 0.0;
+    }
     /* the clip stage as it reaches the integer (icw_clamp_int); clips and peak from the staged q */
-    const int vc = (int)fmax(fmin(q, k.hi - 1.0), k.lo + 1.0);
-    const int val = (isnan(q) ? (int)0x80000000 : vc) + delta;
+    const double vd = __builtin_trunc(fmax(fmin(q, k.hi - 1.0), k.lo + 1.0)) + dd;
     qst[J * 16] = q;
-    vst[J * 16] = val;                                 /* shifted by norm_shift when written out */
-    const double ev = (double)val - input;
+    vst[J * 16] = vd;                                  /* the integer (then shifted) in the flush */
+    const double ev = vd - input;
     double res = 0.0;
     /* the new products go out before this sample's sum, whose volatile fmac block then separates
      * them from their first DPP read in the next sample (a VALU write -> DPP read needs two
@@ -2281,7 +2462,7 @@ __device__ __forceinline__ void icw_rrow_step(double x, double d, double &prev_e
         E[S] = ev;
         P[S] = icw_rmul(c.pl, ev);
         if constexpr (NN > 17) P2[S] = icw_rmul(c.pl2, ev);
-        res = 0.0 + c.c0 * ev;
+        res = __builtin_fma(c.c0, ev, 0.0);
         res = icw_ns_row_sum<NN, R, S>(res, c.one, P, P2);
     } else if constexpr (KIND == 2) {
         E[S] = ev;
@@ -2299,30 +2480,30 @@ __device__ __forceinline__ void icw_rrow_step(double x, double d, double &prev_e
  * per-sample step is scalar arithmetic.  Without dither dn is icw_zero4 with pitch 0 (a branch per
  * load made the compiler copy the prefetch registers around every sample). */
 __device__ double icw_zero4[4];
-template <int KIND, int NN, int R, int J>
+template <int KIND, int NN, int R, int J, bool MR>
 __device__ __forceinline__ void icw_rrow_block(double (&xin)[ICW_MAX_NS_TAPS], double (&dv)[ICW_MAX_NS_TAPS],
                                                double &prev_err, double (&E)[R], double (&O)[R], double (&P)[R],
                                                double (&P2)[R], const IcwRowNs &c, const IcwRenderK &k, double *qst,
-                                               int *vst, const double *pn, const double *dn, size_t dpitch, int dl)
+                                               double *vst, const double *pn, const double *dn, size_t dpitch, int dl)
 {
     if constexpr (J < ICW_MAX_NS_TAPS) {
-        icw_rrow_step<KIND, NN, R, J>(xin[J], dv[J], prev_err, E, O, P, P2, c, k, qst, vst);
+        icw_rrow_step<KIND, NN, R, J, MR>(xin[J], dv[J], prev_err, E, O, P, P2, c, k, qst, vst);
         xin[J] = pn[(size_t)J * 2];
         dv[J] = dn[(size_t)J * dpitch + dl];
-        icw_rrow_block<KIND, NN, R, J + 1>(xin, dv, prev_err, E, O, P, P2, c, k, qst, vst, pn, dn, dpitch, dl);
+        icw_rrow_block<KIND, NN, R, J + 1, MR>(xin, dv, prev_err, E, O, P, P2, c, k, qst, vst, pn, dn, dpitch, dl);
     }
 }
 
-template <int KIND, int NN, int R, int J>
+template <int KIND, int NN, int R, int J, bool MR>
 __device__ __forceinline__ void icw_rrow_block_lim(const double (&xin)[ICW_MAX_NS_TAPS], const double (&dv)[ICW_MAX_NS_TAPS],
                                                    double &prev_err, double (&E)[R], double (&O)[R], double (&P)[R],
                                                    double (&P2)[R], const IcwRowNs &c, const IcwRenderK &k, double *qst,
-                                                   int *vst, int lim)
+                                                   double *vst, int lim)
 {
     if constexpr (J < ICW_MAX_NS_TAPS) {
         if (J < lim) {
-            icw_rrow_step<KIND, NN, R, J>(xin[J], dv[J], prev_err, E, O, P, P2, c, k, qst, vst);
-            icw_rrow_block_lim<KIND, NN, R, J + 1>(xin, dv, prev_err, E, O, P, P2, c, k, qst, vst, lim);
+            icw_rrow_step<KIND, NN, R, J, MR>(xin[J], dv[J], prev_err, E, O, P, P2, c, k, qst, vst);
+            icw_rrow_block_lim<KIND, NN, R, J + 1, MR>(xin, dv, prev_err, E, O, P, P2, c, k, qst, vst, lim);
         }
     }
 }
@@ -2330,7 +2511,7 @@ __device__ __forceinline__ void icw_rrow_block_lim(const double (&xin)[ICW_MAX_N
 /* End of a block of nf samples: clips and peak of the staged q (lane l: samples l, l + 16 of its
  * row), then the block's frames -- lanes 0-31 write stream A's (rows 0, 1), 32-63 stream B's. */
 __device__ __forceinline__ void icw_rrow_flush(const double (*qs)[ICW_MAX_NS_TAPS][16],
-                                               const int (*vs)[ICW_MAX_NS_TAPS][16], int r, int lr, int lane,
+                                               const double (*vs)[ICW_MAX_NS_TAPS][16], int r, int lr, int lane,
                                                int nf, const IcwRenderK &k, unsigned &clips, double &pk,
                                                unsigned char *o0, unsigned char *o1, int osz)
 {
@@ -2347,8 +2528,12 @@ __device__ __forceinline__ void icw_rrow_flush(const double (*qs)[ICW_MAX_NS_TAP
     const int sb = lane >> 5, f = lane & 31;
     unsigned char *o = sb ? o1 : o0;
     if (o && f < nf) {
-        const uint32_t l = (uint32_t)(vs[2 * sb][f][0] << k.norm_shift);
-        const uint32_t rr = (uint32_t)(vs[2 * sb + 1][f][0] << k.norm_shift);
+        /* val = (int)q' + delta, exact in the double; a NaN q gives (int)NaN = INT_MIN with delta 0
+         * (x86 cvttsd2si), as icw_render_round */
+        const int vl = isnan(qs[2 * sb][f][0]) ? (int)0x80000000 : (int)vs[2 * sb][f][0];
+        const int vr = isnan(qs[2 * sb + 1][f][0]) ? (int)0x80000000 : (int)vs[2 * sb + 1][f][0];
+        const uint32_t l = (uint32_t)(vl << k.norm_shift);
+        const uint32_t rr = (uint32_t)(vr << k.norm_shift);
         if (osz == 2) {
             *(uint32_t *)(o + (size_t)f * 4) = (l & 0xffffu) | (rr << 16);
         } else {
@@ -2361,14 +2546,14 @@ __device__ __forceinline__ void icw_rrow_flush(const double (*qs)[ICW_MAX_NS_TAP
     __builtin_amdgcn_wave_barrier();
 }
 
-template <int KIND, int NN>
+template <int KIND, int NN, bool MR>
 __global__ __launch_bounds__(64) void icw_render_row(IcwK3Args a)
 {
     constexpr int U = ICW_MAX_NS_TAPS;                 /* samples per unrolled block */
     constexpr int R = KIND == 1 ? U : (KIND == 2 ? 4 : 1);
     static_assert(U % R == 0, "ring period must divide the unroll");
     __shared__ double qs[4][U][16];                    /* q of each sample, every lane its own slot */
-    __shared__ int vs[4][U][16];                       /* the output values before the shift */
+    __shared__ double vs[4][U][16];                    /* the output values (exact integers) before the shift */
     const int lane = threadIdx.x, r = lane >> 4, lr = lane & 15;
     const int g0 = blockIdx.x * 4 + r;
     const bool valid = g0 < a.n_gen;
@@ -2417,7 +2602,7 @@ __global__ __launch_bounds__(64) void icw_render_row(IcwK3Args a)
     unsigned char *oA = 2 * sA < a.n_gen ? a.out + (size_t)sA * a.out_stride : nullptr;
     unsigned char *oB = 2 * sB < a.n_gen ? a.out + (size_t)sB * a.out_stride : nullptr;
     double *qst = &qs[r][0][lr];
-    int *vst = &vs[r][0][lr];
+    double *vst = &vs[r][0][lr];
     unsigned clips = 0;
     double pk = 0.0;
     const int T = a.T;
@@ -2432,7 +2617,7 @@ __global__ __launch_bounds__(64) void icw_render_row(IcwK3Args a)
         for (; t + U <= T; t += U) {
             /* look-ahead loads of the next block; the last full block re-reads a valid window */
             const int tn = t + 2 * U <= T ? t + U : T - U;
-            icw_rrow_block<KIND, NN, R, 0>(xin, dv, prev_err, E, O, P, P2, c, k, qst, vst, pp + (size_t)tn * 2,
+            icw_rrow_block<KIND, NN, R, 0, MR>(xin, dv, prev_err, E, O, P, P2, c, k, qst, vst, pp + (size_t)tn * 2,
                                            dp + (size_t)tn * dpitch, dpitch, dl);
             icw_rrow_flush(qs, vs, r, lr, lane, U, k, clips, pk, oA ? oA + (size_t)t * 2 * osz : nullptr,
                            oB ? oB + (size_t)t * 2 * osz : nullptr, osz);
@@ -2445,7 +2630,7 @@ __global__ __launch_bounds__(64) void icw_render_row(IcwK3Args a)
             xin[j] = j < rem ? pp[(size_t)(t + j) * 2] : 0.0;
             dv[j] = j < rem ? dp[(size_t)(t + j) * dpitch + dl] : 0.0;
         }
-        icw_rrow_block_lim<KIND, NN, R, 0>(xin, dv, prev_err, E, O, P, P2, c, k, qst, vst, rem);
+        icw_rrow_block_lim<KIND, NN, R, 0, MR>(xin, dv, prev_err, E, O, P, P2, c, k, qst, vst, rem);
         icw_rrow_flush(qs, vs, r, lr, lane, rem, k, clips, pk, oA ? oA + (size_t)t * 2 * osz : nullptr,
                        oB ? oB + (size_t)t * 2 * osz : nullptr, osz);
         /* back to the block-start mapping: rotate left by rem mod R */
@@ -2661,6 +2846,27 @@ extern "C" hipError_t icw_launch_dither_lane(const IcwK3Args *a, hipStream_t st)
     return hipGetLastError();
 }
 
+template <bool MR>
+static hipError_t icw_launch_render_row(const IcwK3Args *a, int rb, int nn, hipStream_t st)
+{
+    if (a->rk.ns_kind == 0) {
+        hipLaunchKernelGGL((icw_render_row<0, 0, MR>), dim3(rb), dim3(64), 0, st, *a);
+    } else if (a->rk.ns_kind == 1) {
+        switch (nn) {
+        case 5: hipLaunchKernelGGL((icw_render_row<1, 5, MR>), dim3(rb), dim3(64), 0, st, *a); break;
+        case 9: hipLaunchKernelGGL((icw_render_row<1, 9, MR>), dim3(rb), dim3(64), 0, st, *a); break;
+        case 15: hipLaunchKernelGGL((icw_render_row<1, 15, MR>), dim3(rb), dim3(64), 0, st, *a); break;
+        case 16: hipLaunchKernelGGL((icw_render_row<1, 16, MR>), dim3(rb), dim3(64), 0, st, *a); break;
+        case 20: hipLaunchKernelGGL((icw_render_row<1, 20, MR>), dim3(rb), dim3(64), 0, st, *a); break;
+        default: return hipErrorInvalidValue;
+        }
+    } else {
+        if (nn != 4) return hipErrorInvalidValue;
+        hipLaunchKernelGGL((icw_render_row<2, 4, MR>), dim3(rb), dim3(64), 0, st, *a);
+    }
+    return hipGetLastError();
+}
+
 extern "C" hipError_t icw_launch_render(const IcwK3Args *a, hipStream_t st)
 {
     const int blocks = (a->n_gen + 63) / 64;
@@ -2672,22 +2878,10 @@ extern "C" hipError_t icw_launch_render(const IcwK3Args *a, hipStream_t st)
     const int nn = a->rk.ns_n;
     if (a->row) {
         const int rb = (a->n_gen + 3) / 4;          /* four channels (two streams) per wave */
-        if (a->rk.ns_kind == 0) {
-            hipLaunchKernelGGL((icw_render_row<0, 0>), dim3(rb), dim3(64), 0, st, *a);
-        } else if (a->rk.ns_kind == 1) {
-            switch (nn) {
-            case 5: hipLaunchKernelGGL((icw_render_row<1, 5>), dim3(rb), dim3(64), 0, st, *a); break;
-            case 9: hipLaunchKernelGGL((icw_render_row<1, 9>), dim3(rb), dim3(64), 0, st, *a); break;
-            case 15: hipLaunchKernelGGL((icw_render_row<1, 15>), dim3(rb), dim3(64), 0, st, *a); break;
-            case 16: hipLaunchKernelGGL((icw_render_row<1, 16>), dim3(rb), dim3(64), 0, st, *a); break;
-            case 20: hipLaunchKernelGGL((icw_render_row<1, 20>), dim3(rb), dim3(64), 0, st, *a); break;
-            default: return hipErrorInvalidValue;
-            }
-        } else {
-            if (nn != 4) return hipErrorInvalidValue;
-            hipLaunchKernelGGL((icw_render_row<2, 4>), dim3(rb), dim3(64), 0, st, *a);
-        }
-        return hipGetLastError();
+        /* the quantiser as a template flag: mid-riser (sign_delta -1, round_offset 0) or mid-tread
+         * (sign_delta 0, round_offset 0.5) -- render_consts gives no other pair */
+        if (a->rk.sign_delta != 0 ? a->rk.round_offset != 0.0 : a->rk.round_offset != 0.5) return hipErrorInvalidValue;
+        return a->rk.sign_delta ? icw_launch_render_row<true>(a, rb, nn, st) : icw_launch_render_row<false>(a, rb, nn, st);
     }
     if (a->rk.ns_kind == 0) {
         hipLaunchKernelGGL((icw_render_serial<0, 1, 0>), dim3(blocks), dim3(64), 0, st, *a);
