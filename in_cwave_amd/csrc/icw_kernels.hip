@@ -631,13 +631,35 @@ __device__ __forceinline__ double icw_iir_out(const double *win, const double (&
     }
 }
 
+/* x / SQRT2 correctly rounded, as dsp_master divides (adv_modulator.c:498-501), in 3 FP64 operations
+ * instead of the 11 of a general division (div_scale x 2, rcp, 5 fma, mul, div_fmas, div_fixup):
+ *     q0 = RN(x r),  e = RN(x - q0 c) (one fma),  q = RN(q0 + e r) (one fma),  r = RN(1/c).
+ * Error: |q0 + e r - x/c| < 2^-51 ulp(x/c) for 2^-900 <= |x| <= DBL_MAX (q0 is within 2 ulp, e within
+ * one rounding of the exact remainder, r within half an ulp of 1/c), so q can differ from RN(x/c)
+ * only where x/c lies within 2^-51 ulp of a rounding midpoint.  With c = C 2^-52 (C odd) those
+ * are the significands X with (2M + 1) C - 2^53 X = k (X >= C) or (2M + 1) C - 2^54 X = k (X < C)
+ * for an odd |k| < 8 -- one residue class mod C each, a handful of X in [2^52, 2^53); every one of
+ * them, up to |k| <= 63, gives RN(x/c) here (tests/test_libm.py::test_div_sqrt2_hard_cases, which
+ * solves for them and checks this arithmetic in exact rationals).  Zeros (a -0.0 would come out
+ * +0.0), tiny values (a subnormal remainder or quotient), infinities and NaNs take the division. */
+__device__ __forceinline__ double icw_div_sqrt2(double x)
+{
+    constexpr double c = ICW_SQRT2;
+    constexpr double rc = 0x1.6a09e667f3bccp-1;          /* RN(1 / c) */
+    const double q0 = x * rc;
+    const double e = __builtin_fma(-q0, c, x);
+    double q = __builtin_fma(e, rc, q0);
+    if (!(fabs(x) >= 0x1p-900 && fabs(x) <= 0x1.fffffffffffffp+1023)) q = x / c;
+    return q;
+}
+
 __device__ __forceinline__ double icw_master(int tout, double re, double im)
 {
     switch (tout) {
     case ICW_S_RE: return re;
     case ICW_S_IM: return im;
-    case ICW_S_ADD_REIM: return (re + im) / ICW_SQRT2;
-    case ICW_S_SUB_REIM: return (re - im) / ICW_SQRT2;
+    case ICW_S_ADD_REIM: return icw_div_sqrt2(re + im);
+    case ICW_S_SUB_REIM: return icw_div_sqrt2(re - im);
     }
     return 0.0;
 }

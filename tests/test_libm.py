@@ -39,3 +39,46 @@ def test_checker_detects_variant_mix(tmp_path):
     assert r.returncode == 1
     n_sc, n_s = (int(v) for v in r.stdout.strip().split("\n")[-1].split()[1:3])
     assert n_sc == 0 and n_s > 0
+
+
+def test_div_sqrt2_hard_cases():
+    """icw_div_sqrt2 (icw_kernels.hip): dsp_master's x / SQRT2 (adv_modulator.c:498-501) as
+    q0 = RN(x r), e = RN(x - q0 c), q = RN(q0 + e r) with r = RN(1/c).  Its error is below 2^-51 ulp,
+    so it can miss RN(x/c) only where x/c is that close to a rounding midpoint: for c = C 2^-52
+    (C odd) those significands X solve (2M + 1) C - 2^s X = k, s = 53 (X >= C) or 54 (X < C), odd
+    |k| < 8 -- one residue class mod C each.  Every such X (|k| <= 63, several binades) must give
+    RN(x/c), computed here in exact rationals; plus random values."""
+    import math
+    import random
+    from fractions import Fraction as Fr
+    c = float("1.4142135623730950488016887242097")        # SQRT2, adv_modulator.c:43
+    r = float.fromhex("0x1.6a09e667f3bccp-1")
+    assert c == math.sqrt(2.0) and r == 1.0 / c
+    m, ex = math.frexp(c)
+    C = int(m * 2 ** 53)
+    assert C * 2.0 ** (ex - 53) == c and C % 2 == 1
+
+    def fast(x):
+        q0 = x * r
+        e = float(Fr(x) - Fr(q0) * Fr(c))                  # one fma: exact, then rounded
+        return float(Fr(q0) + Fr(e) * Fr(r))                # one fma
+
+    n = 0
+    for s in (53, 54):
+        inv = pow(2 ** s, -1, C)
+        lo, hi = (C, 2 ** 53) if s == 53 else (2 ** 52, C)
+        for k in range(-63, 64, 2):
+            X = (-k * inv) % C
+            while X < hi:
+                if X >= lo:
+                    for e2 in (-800, -60, -1, 0, 7, 300, 1000):
+                        x = X * 2.0 ** (e2 - 52)
+                        assert fast(x) == float(Fr(x) / Fr(c)), (s, k, X, e2)
+                        assert fast(-x) == float(Fr(-x) / Fr(c)), (s, k, X, e2)
+                        n += 1
+                X += C
+    assert n > 100
+    rng = random.Random(2)
+    for _ in range(20000):
+        x = rng.uniform(-1e5, 1e5) * 2.0 ** rng.randint(-800, 900)
+        assert fast(x) == float(Fr(x) / Fr(c)), x
