@@ -155,6 +155,9 @@ struct IcwProg {
     int32_t n_persist;             /* slots read before any write in the frame and never written */
     int32_t chain;                 /* register form where every op reads only `in` and / or the op just
                                       before it: values stay in registers (no LDS register file) */
+    int32_t sig;                   /* chain programs: op count | (mode | chain_in << 2) << (4 + 4 i), ops in
+                                      execution order; the fused FIR kernel runs a few of these straight
+                                      (ICW_SIG_*, icw_kernels.hip); 0: not a chain */
     int32_t persist_reg[ICW_MAX_REGS], persist_slot[ICW_MAX_REGS];
     IcwOp ops[ICW_MAX_OPS];
 };

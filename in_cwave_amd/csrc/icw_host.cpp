@@ -485,6 +485,11 @@ int compile_graph(const std::vector<icw_node> &nodes, int bypass, IcwProg &P)
         }
         P.ops[oi].chain_in = bits;
     }
+    P.sig = 0;
+    if (P.chain && n_ops <= 6) {
+        P.sig = n_ops;
+        for (int oi = 0; oi < n_ops; ++oi) P.sig |= ((P.ops[oi].mode & 3) | (P.ops[oi].chain_in << 2)) << (4 + 4 * oi);
+    }
     set_needs_omega(P);
     return ICW_OK;
 }
@@ -849,7 +854,7 @@ int apply_graph(icw_ctx *c, std::vector<icw_node> &nv, int bypass, const std::ve
     IcwProg P;
     int rc = build_prog(cfg, nv, P);
     if (rc) return rc;
-    if (!c->chain_ok) P.chain = 0;
+    if (!c->chain_ok) P.chain = P.sig = 0;
     const bool serial = needs_serial(cfg, c->rk, P);
     if (serial && (rc = ensure_render_state(c))) return rc;
     for (int slot : clears)
@@ -1001,7 +1006,7 @@ int icw_create(const icw_config *cfg, const icw_node *nodes, int n_nodes, int n_
         const char *che = getenv("ICW_CHAIN");
         if (che && !strcmp(che, "0")) {
             c->chain_ok = false;
-            c->prog.chain = 0;
+            c->prog.chain = c->prog.sig = 0;
             if (hipMemcpy(c->d_prog, &c->prog, sizeof(IcwProg), hipMemcpyHostToDevice) != hipSuccess) {
                 free_all(c);
                 delete c;

@@ -787,7 +787,17 @@ __device__ __forceinline__ double icw_omega(unsigned long long n0, long long t, 
  * cos / sin are glibc's own (icw_libm.h): the reference's cos + sin pair is one sincos() call in a
  * gcc build, PM's inner sin() is glibc's FMA variant -- so the factors, and everything after them,
  * are bit-identical to the CPU path. */
-__device__ __forceinline__ void icw_trig(const IcwOp &op, int c, double omega, double &cs, double &sn)
+/* The compiled DSP program is read through the constant address space: its fields are wave-uniform
+ * and the kernels never write it, so they come in by scalar loads into SGPRs.  Through a plain
+ * pointer the compiler could not prove the kernel's own stores (output, bus, pre-render) leave it
+ * alone, and every op field became a vector load, a full vmcnt(0) wait and a v_readfirstlane per
+ * use -- in KF2's graph phase ~half of its 1 050 VALU instructions per wave (c2fir SQ pass,
+ * profiles/r04_c2fir_phases.json). */
+typedef const __attribute__((address_space(4))) IcwProg icw_cprog;
+typedef const __attribute__((address_space(4))) IcwOp icw_cop;
+__device__ __forceinline__ icw_cprog *icw_prog_c(const IcwProg *p) { return (icw_cprog *)p; }
+
+__device__ __forceinline__ void icw_trig(icw_cop &op, int c, double omega, double &cs, double &sn)
 {
     const double ph = fmod(omega * op.f[c], 2.0 * ICW_PI);
     if (op.mode == ICW_MODE_SHIFT) {
@@ -802,7 +812,7 @@ __device__ __forceinline__ void icw_trig(const IcwOp &op, int c, double omega, d
 /* icw_trig out of line, for the per-stream fallback of K2 / K4 (a stream whose frame counter is
  * not stream 0's): inlined, glibc's sincos path added ~45 VGPRs to K2 and cost it a wave per SIMD
  * (141 -> 3 waves) although the per-frame rotation table serves every stream in step. */
-__device__ __noinline__ double2 icw_trig_call(const IcwOp &op, int c, double omega)
+__device__ __noinline__ double2 icw_trig_call(icw_cop &op, int c, double omega)
 {
     double cs, sn;
     icw_trig(op, c, omega, cs, sn);
@@ -813,7 +823,7 @@ __device__ __noinline__ double2 icw_trig_call(const IcwOp &op, int c, double ome
  * gains, then Master (-> lOut/rOut) or Shift / PM / Mix (-> o, returns true).  trow: this frame's
  * row of the rotation table (nullable: compute the factors inline). */
 template <bool TRIG = true, bool TAB = false>
-__device__ __forceinline__ bool icw_exec_op(const IcwOp &op, IcwLR d, double omega, IcwLR &o, double &lOut,
+__device__ __forceinline__ bool icw_exec_op(icw_cop &op, IcwLR d, double omega, IcwLR &o, double &lOut,
                                             double &rOut, const double *trow = nullptr)
 {
     double xt;
@@ -866,7 +876,7 @@ __device__ __forceinline__ bool icw_exec_op(const IcwOp &op, IcwLR d, double ome
  * doubles and the elementwise ROUND render with the meters' per-thread parts. */
 /* DEFER: the rendered integers go to dv[0..1] instead of the output row (KF2 stores 4 frames at once) */
 template <bool TRIG, bool TAB = false, bool DEFER = false>
-__device__ __forceinline__ void icw_frame_graph(const IcwK2Args &a, const IcwProg *P, const IcwRegFile &R, int s,
+__device__ __forceinline__ void icw_frame_graph(const IcwK2Args &a, icw_cprog *P, const IcwRegFile &R, int s,
                                                 int t, const IcwLR &in, bool use_tab, unsigned &clip_l,
                                                 unsigned &clip_r, double &pk_l, double &pk_r, int *dv = nullptr)
 {
@@ -890,7 +900,7 @@ __device__ __forceinline__ void icw_frame_graph(const IcwK2Args &a, const IcwPro
             /* chain program: `in` and the previous op's output in registers, no register file */
             IcwLR prev = in;
             for (int oi = 0; oi < P->n_ops; ++oi) {
-                const IcwOp &op = P->ops[oi];
+                icw_cop &op = P->ops[oi];
                 IcwLR d;
                 if (P->bypass) {
                     d = in;
@@ -911,7 +921,7 @@ __device__ __forceinline__ void icw_frame_graph(const IcwK2Args &a, const IcwPro
         } else {
         R.set(0, in);
         for (int oi = 0; oi < P->n_ops; ++oi) {
-            const IcwOp &op = P->ops[oi];
+            icw_cop &op = P->ops[oi];
             IcwLR d;
             if (P->bypass) {
                 d = in;
@@ -967,7 +977,7 @@ struct IcwOpK {
     double g0, g1;
 };
 
-__device__ __forceinline__ IcwOpK icw_op_k(const IcwOp &op)
+__device__ __forceinline__ IcwOpK icw_op_k(icw_cop &op)
 {
     IcwOpK k;
     k.mode = op.mode; k.chain_in = op.chain_in; k.xch = op.xch;
@@ -995,8 +1005,109 @@ __device__ __forceinline__ IcwOpK icw_op_k(const IcwOp &op)
  * counters take one compare per call -- a clip needs |q| >= min(hi, -lo) (clip_abs), so only a call
  * whose largest |q| reaches that counts its samples one by one (a NaN q clips nothing, and fmax
  * passes it over, as the per-sample compares did). */
-template <bool TRIG, int R, bool ROWP = false>
-__device__ __forceinline__ void icw_chain_frames(const IcwK2Args &a, const IcwProg *P, int s, int t0, int nv,
+/* One op of a chain program over the R frames (the body of icw_chain_frames).  MODE / CIN >= 0: the
+ * op's mode and chain inputs known at compile time (a specialised signature, ICW_SIG_*), so the
+ * compiler keeps only that op's arithmetic and no merges between the modes' results; -1: read from
+ * the program (the generic loop).  The other fields are wave-uniform scalars either way. */
+template <bool TRIG, int R, bool ROWP, int MODE, int CIN>
+__device__ __forceinline__ void icw_chain_op(const IcwK2Args &a, icw_cop &op, bool bypass, int t0, int T,
+                                             const IcwLR (&in)[R], IcwLR (&prev)[R], double (&lOut)[R],
+                                             double (&rOut)[R], double *bus_s, bool has_last, int lastr,
+                                             uint32_t tro_lane, size_t tro_u, size_t tro_step)
+{
+    const IcwOpK k = icw_op_k(op);
+    const int mode = MODE >= 0 ? MODE : k.mode;
+    const int cin = CIN >= 0 ? CIN : k.chain_in;
+    const bool rot = TRIG && (mode == ICW_MODE_SHIFT || mode == ICW_MODE_PM);
+    double cs[R][2], sn[R][2];
+    if (rot) {
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            /* (cos, sin) of a channel: one 16-byte load (rows and columns are 16-byte aligned) */
+            const double *trow = ROWP ? a.trig_tab + tro_u + (size_t)r * tro_step + tro_lane
+                                      : a.trig_tab + icw_trig_index(min(t0 + r, T - 1), a.trig_perm_q) * a.trig_pitch;
+            const double2 f0 = k.act0 ? *(const double2 *)(trow + k.ts0 * 2) : make_double2(0.0, 0.0);
+            const double2 f1 = k.act1 ? *(const double2 *)(trow + k.ts1 * 2) : make_double2(0.0, 0.0);
+            cs[r][0] = f0.x; sn[r][0] = f0.y;
+            cs[r][1] = f1.x; sn[r][1] = f1.y;
+        }
+    }
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        IcwLR d;
+        if (bypass) {
+            d = in[r];
+        } else {
+            d.lre = d.lim = d.rre = d.rim = 0.0;
+            if (cin & 1) { d.lre += in[r].lre; d.lim += in[r].lim; d.rre += in[r].rre; d.rim += in[r].rim; }
+            if (cin & 2) { d.lre += prev[r].lre; d.lim += prev[r].lim; d.rre += prev[r].rre; d.rim += prev[r].rim; }
+        }
+        double xt;
+        switch (k.xch) {
+        case ICW_XCH_SWAP:
+            xt = d.lre; d.lre = d.rre; d.rre = xt;
+            xt = d.lim; d.lim = d.rim; d.rim = xt;
+            break;
+        case ICW_XCH_LEFTONLY: d.rre = d.lre; d.rim = d.lim; break;
+        case ICW_XCH_RIGHTONLY: d.lre = d.rre; d.lim = d.rim; break;
+        case ICW_XCH_MIXLR:
+            d.lre = d.rre = (d.lre + d.rre) / 2.0;
+            d.lim = d.rim = (d.lim + d.rim) / 2.0;
+            break;
+        default: break;
+        }
+        if (k.iq0) { xt = d.lre; d.lre = d.lim; d.lim = xt; }
+        if (k.iq1) { xt = d.rre; d.rre = d.rim; d.rim = xt; }
+        if (k.g0 != 1.0) { d.lre *= k.g0; d.lim *= k.g0; }
+        if (k.g1 != 1.0) { d.rre *= k.g1; d.rim *= k.g1; }
+        if (mode == ICW_MODE_MASTER) {
+            lOut[r] = icw_master(k.tout0, d.lre, d.lim);
+            rOut[r] = icw_master(k.tout1, d.rre, d.rim);
+            continue;
+        }
+        IcwLR o = d;
+        if (rot) {
+            if (k.act0) icw_rot(d.lre, d.lim, cs[r][0], sn[r][0], o.lre, o.lim);
+            if (k.act1) icw_rot(d.rre, d.rim, cs[r][1], sn[r][1], o.rre, o.rim);
+        }
+        prev[r] = o;
+    }
+    if (mode != ICW_MODE_MASTER && k.wb >= 0 && has_last) {
+        double *b = bus_s + k.wb * 4;
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+            if (r == lastr) { b[0] = prev[r].lre; b[1] = prev[r].lim; b[2] = prev[r].rre; b[3] = prev[r].rim; }
+    }
+}
+
+/* Chain-program signatures compiled straight (IcwProg.sig, the host's encoding: the op count in bits
+ * 0-3, then per op in execution order (tail first) 4 bits: mode | chain_in << 2).  Each is one of
+ * the BASELINE graphs: Master on `in` (C3 / C5), Shift -> Master (C1 / C2), PM -> Shift ->
+ * Mix(in + B) -> Master (C4).  Any other chain runs the generic op loop. */
+#define ICW_SIG_M    0x41
+#define ICW_SIG_SM   0x852
+#define ICW_SIG_PSXM 0x8F964
+template <int SIG, int I>
+struct icw_sig_op {
+    static constexpr int mode = (SIG >> (4 + 4 * I)) & 3;
+    static constexpr int cin = (SIG >> (6 + 4 * I)) & 3;
+};
+
+template <bool TRIG, int R, bool ROWP, int SIG, int I>
+__device__ __forceinline__ void icw_chain_sig(const IcwK2Args &a, icw_cprog *P, int t0, int T, const IcwLR (&in)[R],
+                                              IcwLR (&prev)[R], double (&lOut)[R], double (&rOut)[R], double *bus_s,
+                                              bool has_last, int lastr, uint32_t tro_lane, size_t tro_u, size_t tro_step)
+{
+    if constexpr (I < (SIG & 15)) {
+        icw_chain_op<TRIG, R, ROWP, icw_sig_op<SIG, I>::mode, icw_sig_op<SIG, I>::cin>(
+            a, P->ops[I], false, t0, T, in, prev, lOut, rOut, bus_s, has_last, lastr, tro_lane, tro_u, tro_step);
+        icw_chain_sig<TRIG, R, ROWP, SIG, I + 1>(a, P, t0, T, in, prev, lOut, rOut, bus_s, has_last, lastr, tro_lane,
+                                                 tro_u, tro_step);
+    }
+}
+
+template <bool TRIG, int R, bool ROWP = false, int SIG = 0>
+__device__ __forceinline__ void icw_chain_frames(const IcwK2Args &a, icw_cprog *P, int s, int t0, int nv,
                                                  const IcwLR (&in)[R], unsigned &clip_l, unsigned &clip_r,
                                                  double &pk_l, double &pk_r, int (&dv)[R][2], uint32_t tro_lane = 0,
                                                  size_t tro_u = 0, size_t tro_step = 0)
@@ -1017,69 +1128,15 @@ __device__ __forceinline__ void icw_chain_frames(const IcwK2Args &a, const IcwPr
         for (int r = 0; r < R; ++r)
             if (r == lastr) { bus_s[0] = in[r].lre; bus_s[1] = in[r].lim; bus_s[2] = in[r].rre; bus_s[3] = in[r].rim; }
     }
-    const bool bypass = P->bypass != 0;
-    for (int oi = 0; oi < P->n_ops; ++oi) {
-        const IcwOpK k = icw_op_k(P->ops[oi]);
-        const bool rot = TRIG && (k.mode == ICW_MODE_SHIFT || k.mode == ICW_MODE_PM);
-        double cs[R][2], sn[R][2];
-        if (rot) {
-#pragma unroll
-            for (int r = 0; r < R; ++r) {
-                /* (cos, sin) of a channel: one 16-byte load (rows and columns are 16-byte aligned) */
-                const double *trow = ROWP ? a.trig_tab + tro_u + (size_t)r * tro_step + tro_lane
-                                          : a.trig_tab + icw_trig_index(min(t0 + r, T - 1), a.trig_perm_q) * a.trig_pitch;
-                const double2 f0 = k.act0 ? *(const double2 *)(trow + k.ts0 * 2) : make_double2(0.0, 0.0);
-                const double2 f1 = k.act1 ? *(const double2 *)(trow + k.ts1 * 2) : make_double2(0.0, 0.0);
-                cs[r][0] = f0.x; sn[r][0] = f0.y;
-                cs[r][1] = f1.x; sn[r][1] = f1.y;
-            }
-        }
-#pragma unroll
-        for (int r = 0; r < R; ++r) {
-            IcwLR d;
-            if (bypass) {
-                d = in[r];
-            } else {
-                d.lre = d.lim = d.rre = d.rim = 0.0;
-                if (k.chain_in & 1) { d.lre += in[r].lre; d.lim += in[r].lim; d.rre += in[r].rre; d.rim += in[r].rim; }
-                if (k.chain_in & 2) { d.lre += prev[r].lre; d.lim += prev[r].lim; d.rre += prev[r].rre; d.rim += prev[r].rim; }
-            }
-            double xt;
-            switch (k.xch) {
-            case ICW_XCH_SWAP:
-                xt = d.lre; d.lre = d.rre; d.rre = xt;
-                xt = d.lim; d.lim = d.rim; d.rim = xt;
-                break;
-            case ICW_XCH_LEFTONLY: d.rre = d.lre; d.rim = d.lim; break;
-            case ICW_XCH_RIGHTONLY: d.lre = d.rre; d.lim = d.rim; break;
-            case ICW_XCH_MIXLR:
-                d.lre = d.rre = (d.lre + d.rre) / 2.0;
-                d.lim = d.rim = (d.lim + d.rim) / 2.0;
-                break;
-            default: break;
-            }
-            if (k.iq0) { xt = d.lre; d.lre = d.lim; d.lim = xt; }
-            if (k.iq1) { xt = d.rre; d.rre = d.rim; d.rim = xt; }
-            if (k.g0 != 1.0) { d.lre *= k.g0; d.lim *= k.g0; }
-            if (k.g1 != 1.0) { d.rre *= k.g1; d.rim *= k.g1; }
-            if (k.mode == ICW_MODE_MASTER) {
-                lOut[r] = icw_master(k.tout0, d.lre, d.lim);
-                rOut[r] = icw_master(k.tout1, d.rre, d.rim);
-                continue;
-            }
-            IcwLR o = d;
-            if (rot) {
-                if (k.act0) icw_rot(d.lre, d.lim, cs[r][0], sn[r][0], o.lre, o.lim);
-                if (k.act1) icw_rot(d.rre, d.rim, cs[r][1], sn[r][1], o.rre, o.rim);
-            }
-            prev[r] = o;
-        }
-        if (k.mode != ICW_MODE_MASTER && k.wb >= 0 && has_last) {
-            double *b = bus_s + k.wb * 4;
-#pragma unroll
-            for (int r = 0; r < R; ++r)
-                if (r == lastr) { b[0] = prev[r].lre; b[1] = prev[r].lim; b[2] = prev[r].rre; b[3] = prev[r].rim; }
-        }
+    if constexpr (SIG != 0) {
+        /* a signature has no bypass: a bypassed list is the Master alone reading nothing (chain_in 0) */
+        icw_chain_sig<TRIG, R, ROWP, SIG, 0>(a, P, t0, T, in, prev, lOut, rOut, bus_s, has_last, lastr, tro_lane, tro_u,
+                                             tro_step);
+    } else {
+        const bool bypass = P->bypass != 0;
+        for (int oi = 0; oi < P->n_ops; ++oi)
+            icw_chain_op<TRIG, R, ROWP, -1, -1>(a, P->ops[oi], bypass, t0, T, in, prev, lOut, rOut, bus_s, has_last, lastr,
+                                                tro_lane, tro_u, tro_step);
     }
     const IcwRenderK &rk = a.rk;
     double q[R][2], lm_l = 0.0, lm_r = 0.0;
@@ -1106,6 +1163,32 @@ __device__ __forceinline__ void icw_chain_frames(const IcwK2Args &a, const IcwPr
             clip_l += (q[r][0] >= rk.hi ? 1u : 0u) + (q[r][0] <= rk.lo ? 1u : 0u);
             clip_r += (q[r][1] >= rk.hi ? 1u : 0u) + (q[r][1] <= rk.lo ? 1u : 0u);
         }
+    }
+}
+
+/* the chain frames of one call through the program's signature when it is a specialised one */
+template <bool TRIG, int R>
+__device__ __forceinline__ void icw_chain_frames_rowp(const IcwK2Args &a, icw_cprog *P, int sig, int s, int t0, int nv,
+                                                      const IcwLR (&in)[R], unsigned &clip_l, unsigned &clip_r,
+                                                      double &pk_l, double &pk_r, int (&dv)[R][2], uint32_t tro_lane,
+                                                      size_t tro_u, size_t tro_step)
+{
+    switch (sig) {
+    case ICW_SIG_M:
+        icw_chain_frames<TRIG, R, true, ICW_SIG_M>(a, P, s, t0, nv, in, clip_l, clip_r, pk_l, pk_r, dv, tro_lane, tro_u,
+                                                   tro_step);
+        break;
+    case ICW_SIG_SM:
+        icw_chain_frames<TRIG, R, true, ICW_SIG_SM>(a, P, s, t0, nv, in, clip_l, clip_r, pk_l, pk_r, dv, tro_lane, tro_u,
+                                                    tro_step);
+        break;
+    case ICW_SIG_PSXM:
+        icw_chain_frames<TRIG, R, true, ICW_SIG_PSXM>(a, P, s, t0, nv, in, clip_l, clip_r, pk_l, pk_r, dv, tro_lane, tro_u,
+                                                      tro_step);
+        break;
+    default:
+        icw_chain_frames<TRIG, R, true>(a, P, s, t0, nv, in, clip_l, clip_r, pk_l, pk_r, dv, tro_lane, tro_u, tro_step);
+        break;
     }
 }
 
@@ -1139,7 +1222,7 @@ __device__ __forceinline__ void icw_meters_wg(const IcwK2Args &a, int s, unsigne
  * window, w[c][N] the state after the frame), the de-subnorm counts, the fs/4 un-mix, then the
  * frame graph.  dup: mono input with bit-identical converters, chains 2-3 are copies of 0-1. */
 template <int N, bool KAHAN, bool TRIG, bool FCK>
-__device__ __forceinline__ void icw_output_frame(const IcwK2Args &a, const IcwProg *P, const IcwRegFile &R, int s,
+__device__ __forceinline__ void icw_output_frame(const IcwK2Args &a, icw_cprog *P, const IcwRegFile &R, int s,
                                                  int t, const double *const (&w)[4], bool dup, const double *lc,
                                                  IcwFes (&fes)[2], bool count_sn, unsigned (&sn)[4], bool use_tab,
                                                  unsigned &clip_l, unsigned &clip_r, double &pk_l, double &pk_r)
@@ -1266,7 +1349,7 @@ __device__ __forceinline__ void icw_output_body(const IcwK2Args &a, int bx, int 
         __syncthreads();
     }
 
-    const IcwProg *P = a.prog;
+    icw_cprog *P = icw_prog_c(a.prog);
     IcwRegFile R;
     R.base = lregs + tl;
     /* slots read but never written in the frame hold their block-start values */
@@ -1427,7 +1510,7 @@ __global__ __launch_bounds__(256, ICW_FIR_OCC) void icw_fir_graph(IcwFirArgs f, 
     }
 #endif
 
-    const IcwProg *P = a.prog;
+    icw_cprog *P = icw_prog_c(a.prog);
     IcwRegFile Rf;
     Rf.base = lregs + threadIdx.x;
     for (int r = 0; r < P->n_persist; ++r) {
@@ -1455,7 +1538,8 @@ __global__ __launch_bounds__(256, ICW_FIR_OCC) void icw_fir_graph(IcwFirArgs f, 
              * (h + hh + j) q + tt / 8 + ll (icw_trig_index, q = trig_perm_q): a per-lane part and a
              * uniform one.  The last tile of a launch block keeps the clamped index (frames past
              * the block would point past the table). */
-            const bool rowp = TRIG && tt + TF <= f.T;
+            const bool rowp = (TRIG || P->sig) && tt + TF <= f.T;
+            const int sig = P->sig;
             const size_t pq = (size_t)a.trig_perm_q * a.trig_pitch;
             const uint32_t tro_lane = (uint32_t)(((size_t)h * a.trig_perm_q + (size_t)(tt >> 3) + ll) * a.trig_pitch);
 #pragma unroll
@@ -1471,8 +1555,8 @@ __global__ __launch_bounds__(256, ICW_FIR_OCC) void icw_fir_graph(IcwFirArgs f, 
                 }
                 int dv2[2][2];
                 if (rowp)
-                    icw_chain_frames<TRIG, 2, true>(a, P, s, tt + fr0 + hh, min(2, max(nf - fr0 - hh, 0)), in2, clip_l,
-                                                    clip_r, pk_l, pk_r, dv2, tro_lane, (size_t)hh * pq, pq);
+                    icw_chain_frames_rowp<TRIG, 2>(a, P, sig, s, tt + fr0 + hh, min(2, max(nf - fr0 - hh, 0)), in2, clip_l,
+                                                   clip_r, pk_l, pk_r, dv2, tro_lane, (size_t)hh * pq, pq);
                 else
                     icw_chain_frames<TRIG, 2>(a, P, s, tt + fr0 + hh, min(2, max(nf - fr0 - hh, 0)), in2, clip_l, clip_r,
                                               pk_l, pk_r, dv2);
@@ -1545,7 +1629,8 @@ __global__ __launch_bounds__(256, ICW_FIR_OCC) void icw_fir_graph(IcwFirArgs f, 
         const bool b24 = a.rk.is24;
         unsigned w[ICW_FIR_R / 2 * 3];               /* packed output: 16-bit frames in w[0..8) */
         /* table rows as in the stereo form: frame tt + 8 ll + hh + j at row (hh + j) q + tt / 8 + ll */
-        const bool rowp = TRIG && tt + TF <= f.T;
+        const bool rowp = (TRIG || P->sig) && tt + TF <= f.T;
+        const int sig = P->sig;
         const size_t pq = (size_t)a.trig_perm_q * a.trig_pitch;
         const uint32_t tro_lane = (uint32_t)(((size_t)(tt >> 3) + ll) * a.trig_pitch);
 #pragma unroll
@@ -1558,8 +1643,8 @@ __global__ __launch_bounds__(256, ICW_FIR_OCC) void icw_fir_graph(IcwFirArgs f, 
             }
             int dv[2][2];
             if (rowp)
-                icw_chain_frames<TRIG, 2, true>(a, P, s, tt + fr0 + hh, min(2, max(nf - fr0 - hh, 0)), in2, clip_l, clip_r,
-                                                pk_l, pk_r, dv, tro_lane, (size_t)hh * pq, pq);
+                icw_chain_frames_rowp<TRIG, 2>(a, P, sig, s, tt + fr0 + hh, min(2, max(nf - fr0 - hh, 0)), in2, clip_l,
+                                               clip_r, pk_l, pk_r, dv, tro_lane, (size_t)hh * pq, pq);
             else
                 icw_chain_frames<TRIG, 2>(a, P, s, tt + fr0 + hh, min(2, max(nf - fr0 - hh, 0)), in2, clip_l, clip_r, pk_l,
                                           pk_r, dv);
@@ -1623,11 +1708,11 @@ __global__ __launch_bounds__(256, ICW_FIR_OCC) void icw_fir_graph(IcwFirArgs f, 
  * the inline path); K2 reads the row instead of running fmod / sin / sincos per stream. */
 __device__ __forceinline__ void icw_trig_row(const IcwTrigArgs &a, int t)
 {
-    const IcwProg *P = a.prog;
+    icw_cprog *P = icw_prog_c(a.prog);
     const double omega = icw_omega(a.n_frame[0], a.t0 + t, a.scaled, a.ssr, a.sample_rate);
     double *row = a.tab + icw_trig_index(t, a.perm_q) * a.trig_pitch;
     for (int oi = 0; oi < P->n_ops; ++oi) {
-        const IcwOp &op = P->ops[oi];
+        icw_cop &op = P->ops[oi];
         if (op.mode != ICW_MODE_SHIFT && op.mode != ICW_MODE_PM) continue;
         for (int c = 0; c < 2; ++c) {
             if (!op.act[c]) continue;
@@ -1659,7 +1744,7 @@ __global__ __launch_bounds__(64) void icw_graph_serial(IcwK4Args a)
     if (s >= a.n_streams) return;
     double *gb = a.bus + (size_t)s * ICW_N_INPUTS * 4;
     for (int k = 0; k < ICW_N_INPUTS * 4; ++k) bus[k][lane] = gb[k];
-    const IcwProg *P = a.prog;
+    icw_cprog *P = icw_prog_c(a.prog);
     const unsigned long long n0 = a.n_frame[s];
     const double *iq = a.iq + (size_t)s * a.T * 4;
     double *pre = a.pre + (size_t)s * a.pre_stride;
@@ -1671,7 +1756,7 @@ __global__ __launch_bounds__(64) void icw_graph_serial(IcwK4Args a)
         bus[3][lane] = iq[(size_t)t * 4 + 3];
         double lOut = 0.0, rOut = 0.0;
         for (int oi = 0; oi < P->n_ops; ++oi) {
-            const IcwOp &op = P->ops[oi];
+            icw_cop &op = P->ops[oi];
             IcwLR d;
             if (P->bypass) {
                 d.lre = bus[0][lane]; d.lim = bus[1][lane]; d.rre = bus[2][lane]; d.rim = bus[3][lane];
@@ -1757,7 +1842,7 @@ __device__ __forceinline__ void icw_s1_overlapped(const IcwS1Args &a, double *lr
         icw_iir_row_body<N, true>(a.k1, tid, rows, a.lpitch, prog);
     } else {
         const int k = tid - 128, w2 = k >> 6, lane = k & 63;
-        const IcwProg *P = a2.prog;
+        icw_cprog *P = icw_prog_c(a2.prog);
         IcwRegFile R;
         R.base = lregs + tid;
         for (int r = 0; r < P->n_persist; ++r) {

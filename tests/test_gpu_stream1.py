@@ -157,3 +157,24 @@ def test_stream1_overlapped_output_phase(oracle, icw, ovl, kind, ch, monkeypatch
                  "long_chain": graph.graph_long_chain}[kind]()
     lens = [576, 1, 19, 38, 63, 64, 65, 128, 129, 2048, 2500, 576]
     calls(oracle, icw, cfg, nodes, lens, monkeypatch, True)
+
+
+def test_prepare_leaves_fresh_state(oracle, icw):
+    """icw_prepare (the drop-in's warm-up, called by icw_mod_context_create): one call of silence, then
+    the fresh state back -- the first real call equals the oracle's from a fresh stream, meters and
+    frame counter included; a second icw_prepare, after a call, is refused"""
+    cfg = graph.default_config(44100)
+    nodes = graph.graph_pm_shift_mix()
+    ctx = icw.Context(cfg, nodes, 1)
+    ctx.prepare(576)
+    ref = oracle.Stream(cfg, nodes)
+    raw = synth.batch_pcm(1, 576 * 3, 44100, first=21)
+    for b in range(3):
+        seg = np.ascontiguousarray(raw[:, b * 576 * 4:(b + 1) * 576 * 4])
+        out, _ = ctx.process(seg, 576)
+        ro, _ = ref.process(seg[0], 576)
+        assert np.array_equal(out[0], ro), b
+    assert ctx.meters(0) == ref.meters() and ctx.n_frame(0) == ref.n_frame()
+    with pytest.raises(icw.IcwError):
+        ctx.prepare(576)
+    ctx.close()
