@@ -875,6 +875,18 @@ __device__ __forceinline__ bool icw_exec_op(icw_cop &op, IcwLR d, double omega, 
  * hand-off, or the DSP list (adv_modulator.c:637-751) on the LDS register file, the pre-render
  * doubles and the elementwise ROUND render with the meters' per-thread parts. */
 /* DEFER: the rendered integers go to dv[0..1] instead of the output row (KF2 stores 4 frames at once) */
+/* Chain-program signatures compiled straight (IcwProg.sig, the host's encoding: the op count in bits
+ * 0-3, then per op in execution order (tail first) 4 bits: mode | chain_in << 2).  Each is one of
+ * the BASELINE graphs: Master on `in` (C3 / C5), Shift -> Master (C1 / C2), PM -> Shift ->
+ * Mix(in + B) -> Master (C4).  Any other chain runs the generic op loop.  (icw_chain_sig below.) */
+#define ICW_SIG_M    0x41
+#define ICW_SIG_SM   0x852
+#define ICW_SIG_PSXM 0x8F964
+template <bool TRIG, int R, bool ROWP, int SIG, int I>
+__device__ __forceinline__ void icw_chain_sig(const IcwK2Args &a, icw_cprog *P, int t0, int T, const IcwLR (&in)[R],
+                                              IcwLR (&prev)[R], double (&lOut)[R], double (&rOut)[R], double *bus_s,
+                                              bool has_last, int lastr, uint32_t tro_lane, size_t tro_u, size_t tro_step);
+
 template <bool TRIG, bool TAB = false, bool DEFER = false>
 __device__ __forceinline__ void icw_frame_graph(const IcwK2Args &a, icw_cprog *P, const IcwRegFile &R, int s,
                                                 int t, const IcwLR &in, bool use_tab, unsigned &clip_l,
@@ -896,7 +908,21 @@ __device__ __forceinline__ void icw_frame_graph(const IcwK2Args &a, icw_cprog *P
         double *bus_s = a.bus + (size_t)s * ICW_N_INPUTS * 4;
         if (last) { bus_s[0] = in.lre; bus_s[1] = in.lim; bus_s[2] = in.rre; bus_s[3] = in.rim; }
         double lOut = 0.0, rOut = 0.0;
-        if (P->chain) {
+        const int sig = P->sig;
+        if (P->chain && (sig == ICW_SIG_M || sig == ICW_SIG_SM || sig == ICW_SIG_PSXM) && (!TRIG || use_tab)) {
+            /* a specialised chain signature, factors from the table (or none): the ops straight */
+            IcwLR inr[1] = {in}, pv[1] = {in};
+            double lo[1] = {0.0}, ro[1] = {0.0};
+            const uint32_t tro = TRIG ? (uint32_t)(icw_trig_index(t, a.trig_perm_q) * a.trig_pitch) : 0u;
+            if (sig == ICW_SIG_M)
+                icw_chain_sig<TRIG, 1, true, ICW_SIG_M, 0>(a, P, t, T, inr, pv, lo, ro, bus_s, last, 0, tro, 0, 0);
+            else if (sig == ICW_SIG_SM)
+                icw_chain_sig<TRIG, 1, true, ICW_SIG_SM, 0>(a, P, t, T, inr, pv, lo, ro, bus_s, last, 0, tro, 0, 0);
+            else
+                icw_chain_sig<TRIG, 1, true, ICW_SIG_PSXM, 0>(a, P, t, T, inr, pv, lo, ro, bus_s, last, 0, tro, 0, 0);
+            lOut = lo[0];
+            rOut = ro[0];
+        } else if (P->chain) {
             /* chain program: `in` and the previous op's output in registers, no register file */
             IcwLR prev = in;
             for (int oi = 0; oi < P->n_ops; ++oi) {
@@ -1080,13 +1106,7 @@ __device__ __forceinline__ void icw_chain_op(const IcwK2Args &a, icw_cop &op, bo
     }
 }
 
-/* Chain-program signatures compiled straight (IcwProg.sig, the host's encoding: the op count in bits
- * 0-3, then per op in execution order (tail first) 4 bits: mode | chain_in << 2).  Each is one of
- * the BASELINE graphs: Master on `in` (C3 / C5), Shift -> Master (C1 / C2), PM -> Shift ->
- * Mix(in + B) -> Master (C4).  Any other chain runs the generic op loop. */
-#define ICW_SIG_M    0x41
-#define ICW_SIG_SM   0x852
-#define ICW_SIG_PSXM 0x8F964
+/* op I of signature SIG (ICW_SIG_*, above) */
 template <int SIG, int I>
 struct icw_sig_op {
     static constexpr int mode = (SIG >> (4 + 4 * I)) & 3;
