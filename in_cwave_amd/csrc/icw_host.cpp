@@ -485,8 +485,17 @@ int compile_graph(const std::vector<icw_node> &nodes, int bypass, IcwProg &P)
         }
         P.ops[oi].chain_in = bits;
     }
+    /* the signature of a chain of plain ops (the device runs it straight, icw_chain_sig): no channel
+     * exchange or I/Q swap, both channels of a Shift / PM rotating, a Master summing re + im */
     P.sig = 0;
-    if (P.chain && n_ops <= 6) {
+    bool plain = P.chain && n_ops <= 6;
+    for (int oi = 0; oi < n_ops && plain; ++oi) {
+        const IcwOp &op = P.ops[oi];
+        plain = op.xch == ICW_XCH_NORMAL && !op.iqinv[0] && !op.iqinv[1];
+        if (op.mode == ICW_MODE_MASTER) plain &= op.tout[0] == ICW_S_ADD_REIM && op.tout[1] == ICW_S_ADD_REIM;
+        else if (op.mode != ICW_MODE_MIX) plain &= op.act[0] && op.act[1];
+    }
+    if (plain) {
         P.sig = n_ops;
         for (int oi = 0; oi < n_ops; ++oi) P.sig |= ((P.ops[oi].mode & 3) | (P.ops[oi].chain_in << 2)) << (4 + 4 * oi);
     }

@@ -233,6 +233,9 @@ __global__ __launch_bounds__(256) void icw_unpack_frames(IcwK0Args a)
 #ifndef ICW_FIR_CUT
 #define ICW_FIR_CUT 0                                /* diagnostic: 1 no graph, 2 no sums either (VALU by phase) */
 #endif
+#ifndef ICW_FIR_DIAG
+#define ICW_FIR_DIAG 0                               /* diagnostic, not exact: 1 no division slow path, 2 no render */
+#endif
 #ifndef ICW_FIR_STAMPS
 #define ICW_FIR_STAMPS 0                             /* diagnostic: KF2 phase stamps (tools/fir_phases.py) */
 #endif
@@ -642,14 +645,30 @@ __device__ __forceinline__ double icw_iir_out(const double *win, const double (&
  * them, up to |k| <= 63, gives RN(x/c) here (tests/test_libm.py::test_div_sqrt2_hard_cases, which
  * solves for them and checks this arithmetic in exact rationals).  Zeros (a -0.0 would come out
  * +0.0), tiny values (a subnormal remainder or quotient), infinities and NaNs take the division. */
-__device__ __forceinline__ double icw_div_sqrt2(double x)
+/* The range test is on the result: |q| >= 2^-900 holds for no NaN (an infinite x gives a NaN q) and
+ * implies |x| >= 2^-899.5 (q is within a few ulp of x / c wherever it is not a NaN), so it keeps q
+ * only inside the range above, in one compare. */
+__device__ __forceinline__ double icw_div_sqrt2_fast(double x)
 {
-    constexpr double c = ICW_SQRT2;
     constexpr double rc = 0x1.6a09e667f3bccp-1;          /* RN(1 / c) */
     const double q0 = x * rc;
-    const double e = __builtin_fma(-q0, c, x);
-    double q = __builtin_fma(e, rc, q0);
-    if (!(fabs(x) >= 0x1p-900 && fabs(x) <= 0x1.fffffffffffffp+1023)) q = x / c;
+    const double e = __builtin_fma(-q0, ICW_SQRT2, x);
+    return __builtin_fma(e, rc, q0);
+}
+
+__device__ __forceinline__ bool icw_div_sqrt2_ok(double q)
+{
+#if ICW_FIR_DIAG & 1
+    return true;
+#else
+    return fabs(q) >= 0x1p-900;
+#endif
+}
+
+__device__ __forceinline__ double icw_div_sqrt2(double x)
+{
+    double q = icw_div_sqrt2_fast(x);
+    if (!icw_div_sqrt2_ok(q)) q = x / ICW_SQRT2;
     return q;
 }
 
@@ -1041,10 +1060,12 @@ __device__ __forceinline__ void icw_chain_op(const IcwK2Args &a, icw_cop &op, bo
                                              double (&rOut)[R], double *bus_s, bool has_last, int lastr,
                                              uint32_t tro_lane, size_t tro_u, size_t tro_step)
 {
+    constexpr bool plain = MODE >= 0;   /* a signature op: plain fields (compile_graph, IcwProg.sig) */
     const IcwOpK k = icw_op_k(op);
     const int mode = MODE >= 0 ? MODE : k.mode;
     const int cin = CIN >= 0 ? CIN : k.chain_in;
     const bool rot = TRIG && (mode == ICW_MODE_SHIFT || mode == ICW_MODE_PM);
+    const bool act0 = plain || k.act0, act1 = plain || k.act1;
     double cs[R][2], sn[R][2];
     if (rot) {
 #pragma unroll
@@ -1052,8 +1073,8 @@ __device__ __forceinline__ void icw_chain_op(const IcwK2Args &a, icw_cop &op, bo
             /* (cos, sin) of a channel: one 16-byte load (rows and columns are 16-byte aligned) */
             const double *trow = ROWP ? a.trig_tab + tro_u + (size_t)r * tro_step + tro_lane
                                       : a.trig_tab + icw_trig_index(min(t0 + r, T - 1), a.trig_perm_q) * a.trig_pitch;
-            const double2 f0 = k.act0 ? *(const double2 *)(trow + k.ts0 * 2) : make_double2(0.0, 0.0);
-            const double2 f1 = k.act1 ? *(const double2 *)(trow + k.ts1 * 2) : make_double2(0.0, 0.0);
+            const double2 f0 = act0 ? *(const double2 *)(trow + k.ts0 * 2) : make_double2(0.0, 0.0);
+            const double2 f1 = act1 ? *(const double2 *)(trow + k.ts1 * 2) : make_double2(0.0, 0.0);
             cs[r][0] = f0.x; sn[r][0] = f0.y;
             cs[r][1] = f1.x; sn[r][1] = f1.y;
         }
@@ -1069,32 +1090,34 @@ __device__ __forceinline__ void icw_chain_op(const IcwK2Args &a, icw_cop &op, bo
             if (cin & 2) { d.lre += prev[r].lre; d.lim += prev[r].lim; d.rre += prev[r].rre; d.rim += prev[r].rim; }
         }
         double xt;
-        switch (k.xch) {
-        case ICW_XCH_SWAP:
-            xt = d.lre; d.lre = d.rre; d.rre = xt;
-            xt = d.lim; d.lim = d.rim; d.rim = xt;
-            break;
-        case ICW_XCH_LEFTONLY: d.rre = d.lre; d.rim = d.lim; break;
-        case ICW_XCH_RIGHTONLY: d.lre = d.rre; d.lim = d.rim; break;
-        case ICW_XCH_MIXLR:
-            d.lre = d.rre = (d.lre + d.rre) / 2.0;
-            d.lim = d.rim = (d.lim + d.rim) / 2.0;
-            break;
-        default: break;
+        if (!plain) {
+            switch (k.xch) {
+            case ICW_XCH_SWAP:
+                xt = d.lre; d.lre = d.rre; d.rre = xt;
+                xt = d.lim; d.lim = d.rim; d.rim = xt;
+                break;
+            case ICW_XCH_LEFTONLY: d.rre = d.lre; d.rim = d.lim; break;
+            case ICW_XCH_RIGHTONLY: d.lre = d.rre; d.lim = d.rim; break;
+            case ICW_XCH_MIXLR:
+                d.lre = d.rre = (d.lre + d.rre) / 2.0;
+                d.lim = d.rim = (d.lim + d.rim) / 2.0;
+                break;
+            default: break;
+            }
+            if (k.iq0) { xt = d.lre; d.lre = d.lim; d.lim = xt; }
+            if (k.iq1) { xt = d.rre; d.rre = d.rim; d.rim = xt; }
         }
-        if (k.iq0) { xt = d.lre; d.lre = d.lim; d.lim = xt; }
-        if (k.iq1) { xt = d.rre; d.rre = d.rim; d.rim = xt; }
         if (k.g0 != 1.0) { d.lre *= k.g0; d.lim *= k.g0; }
         if (k.g1 != 1.0) { d.rre *= k.g1; d.rim *= k.g1; }
         if (mode == ICW_MODE_MASTER) {
-            lOut[r] = icw_master(k.tout0, d.lre, d.lim);
-            rOut[r] = icw_master(k.tout1, d.rre, d.rim);
+            lOut[r] = icw_master(plain ? ICW_S_ADD_REIM : k.tout0, d.lre, d.lim);
+            rOut[r] = icw_master(plain ? ICW_S_ADD_REIM : k.tout1, d.rre, d.rim);
             continue;
         }
         IcwLR o = d;
         if (rot) {
-            if (k.act0) icw_rot(d.lre, d.lim, cs[r][0], sn[r][0], o.lre, o.lim);
-            if (k.act1) icw_rot(d.rre, d.rim, cs[r][1], sn[r][1], o.rre, o.rim);
+            if (act0) icw_rot(d.lre, d.lim, cs[r][0], sn[r][0], o.lre, o.lim);
+            if (act1) icw_rot(d.rre, d.rim, cs[r][1], sn[r][1], o.rre, o.rim);
         }
         prev[r] = o;
     }
@@ -1126,6 +1149,172 @@ __device__ __forceinline__ void icw_chain_sig(const IcwK2Args &a, icw_cprog *P, 
     }
 }
 
+/* The render-only form of a signature pass (no pre-render doubles requested, no lane holding the
+ * block's last frame): the same rendered integers and meters in about a third of the instructions.
+ *  - An op's input is the sum in + prev without the reference's leading 0.0 + (adv_modulator.c:655-665).
+ *    0.0 + x differs from x only for x = -0.0, and in this arithmetic (products, sums, the division by
+ *    SQRT2 -- no reciprocal, no sign test) a zero's sign changes nothing but zero signs downstream.
+ *    The render cannot see one (below), so the integers and meters are the exact pass's; the pre-render
+ *    doubles and the bus state can, which is why those calls and frames take icw_chain_frames' path.
+ *  - A gain of 1.0 is branched over (the compiler had turned the uniform test into a multiply and
+ *    two selects per double).
+ *  - The division by SQRT2: icw_div_sqrt2's three operations for every value, then one test per value
+ *    and one divergent branch per op for those outside its range.
+ *  - The render (sound_render_value, ROUND + flat shaper, sound_render.c:747-797): q = x * norm_mul +
+ *    copysign(round_offset, x) -- for the mid-riser (offset 0) x + +-0 with x's own sign is x exactly,
+ *    for the mid-tread it is the reference's x +- 0.5 except at x = -0.0, where -0.5 and +0.5 both
+ *    truncate to 0 and have the same magnitude for the peak and the clip tests; the clip stage and the
+ *    truncation as v_cvt_i32_f64 (it saturates out-of-range values) + v_med3_i32 into [lo + 1, hi - 1]
+ *    (the same integer as min(q, hi - 1), max(., lo + 1), then (int), for every q that is not a NaN);
+ *    a NaN q -- INT_MIN, as x86's cvttsd2si gives -- takes a divergent branch of its own. */
+__device__ __forceinline__ int icw_cvt_sat_i32(double q)
+{
+    int v;
+    asm("v_cvt_i32_f64_e32 %0, %1" : "=v"(v) : "v"(q));
+    return v;
+}
+
+__device__ __forceinline__ int icw_med3_i32(int x, int lo, int hi)
+{
+    int v;
+    asm("v_med3_i32 %0, %1, %2, %3" : "=v"(v) : "v"(x), "v"(lo), "v"(hi));
+    return v;
+}
+
+template <bool TRIG, int R, int SIG, int I>
+__device__ __forceinline__ void icw_sig_fast_ops(const IcwK2Args &a, icw_cprog *P, const IcwLR (&in)[R],
+                                                 IcwLR (&prev)[R], double (&lOut)[R], double (&rOut)[R],
+                                                 uint32_t tro_lane, size_t tro_u, size_t tro_step)
+{
+    if constexpr (I < (SIG & 15)) {
+        constexpr int mode = icw_sig_op<SIG, I>::mode, cin = icw_sig_op<SIG, I>::cin;
+        constexpr bool rot = TRIG && (mode == ICW_MODE_SHIFT || mode == ICW_MODE_PM);
+        icw_cop &op = P->ops[I];
+        double cs[R][2], sn[R][2];
+        if constexpr (rot) {
+            const int ts0 = op.tslot[0], ts1 = op.tslot[1];
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                const double *trow = a.trig_tab + tro_u + (size_t)r * tro_step + tro_lane;
+                const double2 f0 = *(const double2 *)(trow + ts0 * 2);
+                const double2 f1 = *(const double2 *)(trow + ts1 * 2);
+                cs[r][0] = f0.x; sn[r][0] = f0.y;
+                cs[r][1] = f1.x; sn[r][1] = f1.y;
+            }
+        }
+        IcwLR d[R];
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            if constexpr (cin == 1) d[r] = in[r];
+            else if constexpr (cin == 2) d[r] = prev[r];
+            else if constexpr (cin == 3) {
+                d[r].lre = in[r].lre + prev[r].lre; d[r].lim = in[r].lim + prev[r].lim;
+                d[r].rre = in[r].rre + prev[r].rre; d[r].rim = in[r].rim + prev[r].rim;
+            } else {
+                d[r].lre = d[r].lim = d[r].rre = d[r].rim = 0.0;
+            }
+        }
+        const double g0 = op.gain[0], g1 = op.gain[1];
+        if (g0 != 1.0) {
+            asm volatile("");
+#pragma unroll
+            for (int r = 0; r < R; ++r) { d[r].lre *= g0; d[r].lim *= g0; }
+        }
+        if (g1 != 1.0) {
+            asm volatile("");
+#pragma unroll
+            for (int r = 0; r < R; ++r) { d[r].rre *= g1; d[r].rim *= g1; }
+        }
+        if constexpr (mode == ICW_MODE_MASTER) {
+            double x[R][2];
+            bool slow = false;
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                x[r][0] = d[r].lre + d[r].lim;
+                x[r][1] = d[r].rre + d[r].rim;
+                lOut[r] = icw_div_sqrt2_fast(x[r][0]);
+                rOut[r] = icw_div_sqrt2_fast(x[r][1]);
+                slow |= !icw_div_sqrt2_ok(lOut[r]) || !icw_div_sqrt2_ok(rOut[r]);
+            }
+            if (slow) {
+#pragma unroll
+                for (int r = 0; r < R; ++r) {
+                    if (!icw_div_sqrt2_ok(lOut[r])) lOut[r] = x[r][0] / ICW_SQRT2;
+                    if (!icw_div_sqrt2_ok(rOut[r])) rOut[r] = x[r][1] / ICW_SQRT2;
+                }
+            }
+        } else {
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                if constexpr (rot) {
+                    icw_rot(d[r].lre, d[r].lim, cs[r][0], sn[r][0], prev[r].lre, prev[r].lim);
+                    icw_rot(d[r].rre, d[r].rim, cs[r][1], sn[r][1], prev[r].rre, prev[r].rim);
+                } else {
+                    prev[r] = d[r];
+                }
+            }
+        }
+        icw_sig_fast_ops<TRIG, R, SIG, I + 1>(a, P, in, prev, lOut, rOut, tro_lane, tro_u, tro_step);
+    }
+}
+
+template <bool TRIG, int R, int SIG>
+__device__ __forceinline__ void icw_sig_fast(const IcwK2Args &a, icw_cprog *P, const IcwLR (&in)[R], unsigned &clip_l,
+                                             unsigned &clip_r, double &pk_l, double &pk_r, int (&dv)[R][2],
+                                             uint32_t tro_lane, size_t tro_u, size_t tro_step)
+{
+    IcwLR prev[R];
+    double lOut[R], rOut[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        prev[r] = in[r];
+        lOut[r] = rOut[r] = 0.0;
+    }
+    icw_sig_fast_ops<TRIG, R, SIG, 0>(a, P, in, prev, lOut, rOut, tro_lane, tro_u, tro_step);
+    const IcwRenderK &rk = a.rk;
+    double x[R][2], q[R][2];
+#pragma unroll
+    for (int r = 0; r < R; ++r) { x[r][0] = lOut[r]; x[r][1] = rOut[r]; }
+    if (rk.norm_mul != 1.0) {
+        asm volatile("");
+#pragma unroll
+        for (int r = 0; r < R; ++r) { x[r][0] *= rk.norm_mul; x[r][1] *= rk.norm_mul; }
+    }
+    const int lo1 = (int)rk.lo + 1, hi1 = (int)rk.hi - 1;
+    int del[R][2];
+    bool nan = false;
+    double lm_l = 0.0, lm_r = 0.0;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+            q[r][c] = x[r][c] + __builtin_copysign(rk.round_offset, x[r][c]);
+            del[r][c] = x[r][c] < 0.0 ? rk.sign_delta : 0;
+            const int v = icw_med3_i32(icw_cvt_sat_i32(q[r][c]), lo1, hi1);
+            dv[r][c] = (v + del[r][c]) << rk.norm_shift;
+            nan |= q[r][c] != q[r][c];
+        }
+        lm_l = fmax(lm_l, fabs(q[r][0]));
+        lm_r = fmax(lm_r, fabs(q[r][1]));
+    }
+    if (nan) {
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+#pragma unroll
+            for (int c = 0; c < 2; ++c)
+                if (q[r][c] != q[r][c]) dv[r][c] = ((int)0x80000000 + del[r][c]) << rk.norm_shift;
+    }
+    pk_l = fmax(pk_l, lm_l);
+    pk_r = fmax(pk_r, lm_r);
+    if (fmax(lm_l, lm_r) >= rk.clip_abs) {
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            clip_l += (q[r][0] >= rk.hi ? 1u : 0u) + (q[r][0] <= rk.lo ? 1u : 0u);
+            clip_r += (q[r][1] >= rk.hi ? 1u : 0u) + (q[r][1] <= rk.lo ? 1u : 0u);
+        }
+    }
+}
+
 template <bool TRIG, int R, bool ROWP = false, int SIG = 0>
 __device__ __forceinline__ void icw_chain_frames(const IcwK2Args &a, icw_cprog *P, int s, int t0, int nv,
                                                  const IcwLR (&in)[R], unsigned &clip_l, unsigned &clip_r,
@@ -1136,6 +1325,13 @@ __device__ __forceinline__ void icw_chain_frames(const IcwK2Args &a, icw_cprog *
     double *bus_s = a.bus + (size_t)s * ICW_N_INPUTS * 4;
     const int lastr = T - 1 - t0;                    /* the block's last frame is frame lastr here */
     const bool has_last = lastr >= 0 && lastr < nv;
+    if constexpr (SIG != 0 && ROWP) {
+        /* the render-only form when no lane of the wave needs the exact doubles */
+        if (!a.pre && __all(nv == R && !has_last)) {
+            icw_sig_fast<TRIG, R, SIG>(a, P, in, clip_l, clip_r, pk_l, pk_r, dv, tro_lane, tro_u, tro_step);
+            return;
+        }
+    }
     IcwLR prev[R];
     double lOut[R], rOut[R];
 #pragma unroll
@@ -1169,8 +1365,13 @@ __device__ __forceinline__ void icw_chain_frames(const IcwK2Args &a, icw_cprog *
                 double *p = a.pre + (size_t)s * a.pre_stride + (size_t)(t0 + r) * 2;
                 p[0] = lOut[r]; p[1] = rOut[r];
             }
+#if ICW_FIR_DIAG & 2
+            q[r][0] = lOut[r]; q[r][1] = rOut[r];
+            dv[r][0] = (int)lOut[r]; dv[r][1] = (int)rOut[r];
+#else
             dv[r][0] = icw_render_round_q(lOut[r], rk, q[r][0]);
             dv[r][1] = icw_render_round_q(rOut[r], rk, q[r][1]);
+#endif
             lm_l = fmax(lm_l, fabs(q[r][0]));
             lm_r = fmax(lm_r, fabs(q[r][1]));
         }

@@ -1,0 +1,79 @@
+"""GPU parity of the render-only form of the specialised chain programs (icw_sig_fast in
+icw_kernels.hip): calls that ask for no pre-render doubles run the BASELINE graphs' signatures
+without the reference's leading `0.0 +` per op input, with the division by SQRT2 tested once per op
+and the render's clip stage as a saturating conversion + integer clamp.  Its rendered bytes and
+meters must be the oracle's, and the exact form's (the same call asking for the doubles), for both
+quantizers, 16- and 24-bit output, a norm_mul other than 1.0, gains of 1.0 and not, stereo and mono,
+and float input carrying NaN, infinities, -0.0 runs and values far past full scale."""
+import numpy as np
+import pytest
+
+from in_cwave_amd import abi, graph, synth
+
+pytestmark = pytest.mark.gpu
+
+ORDER, BETA = 254, 8.0
+N = 5000            # four full 1024-frame tiles (the render-only form) and a partial one (the exact form)
+
+
+def graphs():
+    sm_gains = graph.graph_shift_master()
+    sm_gains[0].gain[0] = sm_gains[0].gain[1] = 1.0      # Master gain 1.0
+    sm_gains[1].gain[0] = 0.5                            # Shift L gain 0.5, R 1.0
+    return {"master": graph.graph_master_only(), "shift_master": graph.graph_shift_master(),
+            "pm_shift_mix": graph.graph_pm_shift_mix(), "shift_master_gains": sm_gains}
+
+
+def special_f32(n_streams, n, ch, seed):
+    """loud float input (up to 4x full scale) with NaN, +-inf, -0.0 runs and huge values"""
+    rng = np.random.default_rng(seed)
+    x = (rng.standard_normal((n_streams, n, ch)) * 1.5).astype(np.float32)
+    x[:, 300:700] = -0.0                                  # a silent run of negative zeros
+    x[:, 1500:1540] = 0.0
+    for s in range(n_streams):
+        for v in (np.nan, np.inf, -np.inf, 3e38, -3e38, 1e-40, -1e-40):
+            idx = rng.integers(0, n, 3)
+            x[s, idx, rng.integers(0, ch)] = v
+    return x.reshape(n_streams, -1).view(np.uint8)
+
+
+def run(oracle, icw, cfg, nodes, raw, n, want_pre):
+    S = raw.shape[0]
+    ctx = icw.Context(cfg, nodes, S)
+    ctx.set_fir_hilbert(ORDER, BETA)
+    out, _ = ctx.process(raw, n, want_pre=want_pre)
+    meters = [ctx.meters(s) for s in range(S)]
+    ctx.close()
+    return out, meters
+
+
+@pytest.mark.parametrize("gname", ["master", "shift_master", "pm_shift_mix", "shift_master_gains"])
+@pytest.mark.parametrize("quantz", [abi.QUANTZ_MID_RISER, abi.QUANTZ_MID_TREAD])
+@pytest.mark.parametrize("b24,sign16", [(False, 16), (False, 11), (True, 16)])
+@pytest.mark.parametrize("fmt,ch", [(abi.FMT_I16, 2), (abi.FMT_F32, 2), (abi.FMT_F32, 1)])
+def test_sig_fast_render(oracle, icw, gname, quantz, b24, sign16, fmt, ch, monkeypatch):
+    monkeypatch.setenv("ICW_FIR_FUSED", "1")
+    cfg = graph.default_config(48000, fmt=fmt, channels=ch, need24bits=b24)
+    cfg.render.quantz_type = quantz
+    cfg.render.sign_bits16 = sign16
+    nodes = graphs()[gname]
+    S = 2
+    if fmt == abi.FMT_F32:
+        raw = special_f32(S, N, ch, seed=hash((gname, quantz, b24, sign16, ch)) & 0xffff)
+    else:
+        raw = synth.batch_pcm(S, N, 48000, channels=ch, fmt=fmt, first=3)
+        # past full scale: the clip counters and the clamp
+        v = raw.view(np.int16).copy()
+        v[:, 4000:4400] = np.where(v[:, 4000:4400] >= 0, 32767, -32768)
+        raw = v.view(np.uint8)
+    out, meters = run(oracle, icw, cfg, nodes, raw, N, want_pre=False)
+    out_x, meters_x = run(oracle, icw, cfg, nodes, raw, N, want_pre=True)
+    assert np.array_equal(out, out_x)
+    assert meters == meters_x
+    for s in range(S):
+        st = oracle.Stream(cfg, nodes)
+        st.set_fir(ORDER, BETA)
+        ro, _ = st.process(raw[s], N)
+        bad = np.flatnonzero(out[s] != ro)
+        assert bad.size == 0, (s, bad[:8])
+        assert meters[s] == st.meters(), (s, meters[s], st.meters())
