@@ -1591,6 +1591,13 @@ int icw_process_streams(icw_ctx *c, int first, int count, const void *in, size_t
             sR = cs->render;
             if (c->fill_drain) sF = c->stream2;
         }
+    } else {
+        /* complex input or the FIR converter: no recurrence kernel, so the dither generator runs after
+         * the converter / output kernel on sA, beside the serial render of the previous block on sR.
+         * On its own stream it shared a hardware queue with the render (4 queues per process,
+         * GPU_MAX_HW_QUEUES, streams dealt round-robin): K3a of block b + 1 waited for K3r of block b,
+         * 1.2 of every 6.7 ms per c5fir block (profiles/r04_c5fir_timeline.txt) */
+        sD = sA;
     }
     hipStream_t sC = pipe_io ? c->stream_io : nullptr;
     if (pipe_io && (int)c->ev_io.size() < n_blocks) {

@@ -2764,7 +2764,7 @@ struct IcwRowNs {
 template <int KIND, int NN, int R, int J, bool MR>
 __device__ __forceinline__ void icw_rrow_step(double x, double d, double &prev_err, double (&E)[R], double (&O)[R],
                                               double (&P)[R], double (&P2)[R], const IcwRowNs &c,
-                                              const IcwRenderK &k, double *qst, double *vst)
+                                              const IcwRenderK &k, double *qst)
 {
     constexpr int S = J % R;
     const double input = (x * k.norm_mul) - prev_err;
@@ -2779,8 +2779,7 @@ __device__ __forceinline__ void icw_rrow_step(double x, double d, double &prev_e
     }
     /* the clip stage as it reaches the integer (icw_clamp_int); clips and peak from the staged q */
     const double vd = __builtin_trunc(fmax(fmin(q, k.hi - 1.0), k.lo + 1.0)) + dd;
-    qst[J * 16] = q;
-    vst[J * 16] = vd;                                  /* the integer (then shifted) in the flush */
+    qst[J * 16] = q;                                   /* the integer is the flush's, from q */
     const double ev = vd - input;
     double res = 0.0;
     /* the new products go out before this sample's sum, whose volatile fmac block then separates
@@ -2803,22 +2802,20 @@ __device__ __forceinline__ void icw_rrow_step(double x, double d, double &prev_e
     prev_err = res;
 }
 
-/* look-ahead loads: pn is the lane's pre-render row at the next block; the dither rows are
- * time-major, so their address is a wave-uniform base dn plus the row's channel offset dl -- the
- * per-sample step is scalar arithmetic.  Without dither dn is icw_zero4 with pitch 0 (a branch per
- * load made the compiler copy the prefetch registers around every sample). */
-__device__ double icw_zero4[4];
+/* look-ahead reads: the next block's inputs and dither values of the row's channel, staged in LDS
+ * (icw_rrow_stage_*): sample J of this block reads sample J of the next -- a whole block ahead of
+ * its use, at an immediate offset (no address arithmetic per sample, no wait on global memory) */
 template <int KIND, int NN, int R, int J, bool MR>
 __device__ __forceinline__ void icw_rrow_block(double (&xin)[ICW_MAX_NS_TAPS], double (&dv)[ICW_MAX_NS_TAPS],
                                                double &prev_err, double (&E)[R], double (&O)[R], double (&P)[R],
                                                double (&P2)[R], const IcwRowNs &c, const IcwRenderK &k, double *qst,
-                                               double *vst, const double *pn, const double *dn, size_t dpitch, int dl)
+                                               const double *xn, const double *dn)
 {
     if constexpr (J < ICW_MAX_NS_TAPS) {
-        icw_rrow_step<KIND, NN, R, J, MR>(xin[J], dv[J], prev_err, E, O, P, P2, c, k, qst, vst);
-        xin[J] = pn[(size_t)J * 2];
-        dv[J] = dn[(size_t)J * dpitch + dl];
-        icw_rrow_block<KIND, NN, R, J + 1, MR>(xin, dv, prev_err, E, O, P, P2, c, k, qst, vst, pn, dn, dpitch, dl);
+        icw_rrow_step<KIND, NN, R, J, MR>(xin[J], dv[J], prev_err, E, O, P, P2, c, k, qst);
+        xin[J] = xn[J];
+        dv[J] = dn[J];
+        icw_rrow_block<KIND, NN, R, J + 1, MR>(xin, dv, prev_err, E, O, P, P2, c, k, qst, xn, dn);
     }
 }
 
@@ -2826,20 +2823,64 @@ template <int KIND, int NN, int R, int J, bool MR>
 __device__ __forceinline__ void icw_rrow_block_lim(const double (&xin)[ICW_MAX_NS_TAPS], const double (&dv)[ICW_MAX_NS_TAPS],
                                                    double &prev_err, double (&E)[R], double (&O)[R], double (&P)[R],
                                                    double (&P2)[R], const IcwRowNs &c, const IcwRenderK &k, double *qst,
-                                                   double *vst, int lim)
+                                                   int lim)
 {
     if constexpr (J < ICW_MAX_NS_TAPS) {
         if (J < lim) {
-            icw_rrow_step<KIND, NN, R, J, MR>(xin[J], dv[J], prev_err, E, O, P, P2, c, k, qst, vst);
-            icw_rrow_block_lim<KIND, NN, R, J + 1, MR>(xin, dv, prev_err, E, O, P, P2, c, k, qst, vst, lim);
+            icw_rrow_step<KIND, NN, R, J, MR>(xin[J], dv[J], prev_err, E, O, P, P2, c, k, qst);
+            icw_rrow_block_lim<KIND, NN, R, J + 1, MR>(xin, dv, prev_err, E, O, P, P2, c, k, qst, lim);
         }
     }
 }
 
+/* The staging of one block's inputs (frames t0 .. t0 + U - 1 of the wave's two streams, both
+ * channels: lanes 0-19 / 32-51 load frame i of stream A / B, L and R in 16 bytes) and dither values
+ * (its four channels: lanes 0-39 half a dither row each, 16 bytes); frames past T, streams past the
+ * batch and channels past n_gen load nothing.  A block is loaded one block before it is stored to
+ * LDS and stored one block before it is read, so no per-sample wait reaches global memory -- the
+ * per-sample loads they replace ended each block in a full drain (s_waitcnt vmcnt(0)). */
+struct IcwRowStage {
+    double2 x, d;
+};
+
+__device__ __forceinline__ void icw_rrow_stage_load(const IcwK3Args &a, int t0, int lane, IcwRowStage &st)
+{
+    constexpr int U = ICW_MAX_NS_TAPS;
+    const int sb = lane >> 5, i = lane & 31;
+    const int s = blockIdx.x * 2 + sb;
+    st.x = make_double2(0.0, 0.0);
+    st.d = make_double2(0.0, 0.0);
+    if (i < U && t0 + i < a.T && 2 * s < a.n_gen)
+        st.x = *(const double2 *)(a.pre + (size_t)s * a.pre_stride + (size_t)(t0 + i) * 2);
+    const int tt = lane >> 1, h = lane & 1;
+    if (a.dith && lane < 2 * U && t0 + tt < a.T && (int)blockIdx.x * 4 + 2 * h < a.n_gen)
+        st.d = *(const double2 *)(a.dith + (size_t)(t0 + tt) * a.dith_pitch + blockIdx.x * 4 + 2 * h);
+}
+
+__device__ __forceinline__ void icw_rrow_stage_store(double (*xs)[ICW_MAX_NS_TAPS], double (*ds)[ICW_MAX_NS_TAPS],
+                                                     int lane, const IcwRowStage &st)
+{
+    constexpr int U = ICW_MAX_NS_TAPS;
+    const int sb = lane >> 5, i = lane & 31;
+    if (i < U) { xs[2 * sb][i] = st.x.x; xs[2 * sb + 1][i] = st.x.y; }
+    const int tt = lane >> 1, h = lane & 1;
+    if (lane < 2 * U) { ds[2 * h][tt] = st.d.x; ds[2 * h + 1][tt] = st.d.y; }
+}
+
 /* End of a block of nf samples: clips and peak of the staged q (lane l: samples l, l + 16 of its
- * row), then the block's frames -- lanes 0-31 write stream A's (rows 0, 1), 32-63 stream B's. */
-__device__ __forceinline__ void icw_rrow_flush(const double (*qs)[ICW_MAX_NS_TAPS][16],
-                                               const double (*vs)[ICW_MAX_NS_TAPS][16], int r, int lr, int lane,
+ * row), then the block's frames -- lanes 0-31 write stream A's (rows 0, 1), 32-63 stream B's.  The
+ * integer is the chain's trunc(q') + delta formed again from q, off the chain: the saturating
+ * conversion, the clamp into [lo + 1, hi - 1] and the mid-riser's delta (q < 0); a NaN q gives
+ * (int)NaN = INT_MIN (x86 cvttsd2si) with delta 0, as icw_render_round. */
+template <bool MR>
+__device__ __forceinline__ int icw_rrow_val(double q, int lo1, int hi1)
+{
+    const int v = icw_med3_i32(icw_cvt_sat_i32(q), lo1, hi1) + (MR && q < 0.0 ? -1 : 0);
+    return q != q ? (int)0x80000000 : v;
+}
+
+template <bool MR>
+__device__ __forceinline__ void icw_rrow_flush(const double (*qs)[ICW_MAX_NS_TAPS][16], int r, int lr, int lane,
                                                int nf, const IcwRenderK &k, unsigned &clips, double &pk,
                                                unsigned char *o0, unsigned char *o1, int osz)
 {
@@ -2856,10 +2897,9 @@ __device__ __forceinline__ void icw_rrow_flush(const double (*qs)[ICW_MAX_NS_TAP
     const int sb = lane >> 5, f = lane & 31;
     unsigned char *o = sb ? o1 : o0;
     if (o && f < nf) {
-        /* val = (int)q' + delta, exact in the double; a NaN q gives (int)NaN = INT_MIN with delta 0
-         * (x86 cvttsd2si), as icw_render_round */
-        const int vl = isnan(qs[2 * sb][f][0]) ? (int)0x80000000 : (int)vs[2 * sb][f][0];
-        const int vr = isnan(qs[2 * sb + 1][f][0]) ? (int)0x80000000 : (int)vs[2 * sb + 1][f][0];
+        const int lo1 = (int)k.lo + 1, hi1 = (int)k.hi - 1;
+        const int vl = icw_rrow_val<MR>(qs[2 * sb][f][0], lo1, hi1);
+        const int vr = icw_rrow_val<MR>(qs[2 * sb + 1][f][0], lo1, hi1);
         const uint32_t l = (uint32_t)(vl << k.norm_shift);
         const uint32_t rr = (uint32_t)(vr << k.norm_shift);
         if (osz == 2) {
@@ -2881,12 +2921,10 @@ __global__ __launch_bounds__(64) void icw_render_row(IcwK3Args a)
     constexpr int R = KIND == 1 ? U : (KIND == 2 ? 4 : 1);
     static_assert(U % R == 0, "ring period must divide the unroll");
     __shared__ double qs[4][U][16];                    /* q of each sample, every lane its own slot */
-    __shared__ double vs[4][U][16];                    /* the output values (exact integers) before the shift */
     const int lane = threadIdx.x, r = lane >> 4, lr = lane & 15;
     const int g0 = blockIdx.x * 4 + r;
     const bool valid = g0 < a.n_gen;
-    const int g = valid ? g0 : a.n_gen - 1;            /* spare rows run a copy, store nothing */
-    const int s = g >> 1, ch = g & 1;
+    const int g = valid ? g0 : a.n_gen - 1;            /* spare rows run on zeros, store nothing */
     const IcwRenderK &k = a.rk;
     double *rs = a.rs + (size_t)g * ICW_RSTATE;
     double prev_err = rs[1];
@@ -2920,47 +2958,46 @@ __global__ __launch_bounds__(64) void icw_render_row(IcwK3Args a)
     }
     asm volatile("s_nop 1");                           /* VALU write -> DPP read of P / P2 */
     const int osz = k.is24 ? 3 : 2;
-    const double *pp = a.pre + (size_t)s * a.pre_stride + ch;
-    /* dither rows, time-major [t][dith_pitch]; ROUND: rnd * dth_mul == 0.0 * dth_mul, all zeros */
-    const double *dp = a.dith ? a.dith + blockIdx.x * 4 : icw_zero4;
-    const int dl = g - blockIdx.x * 4;                 /* this row's channel in the wave's four */
-    const size_t dpitch = a.dith ? a.dith_pitch : 0;
     /* the wave's two streams (channels 4b..4b+3); a stream past the batch writes nothing */
     const int sA = blockIdx.x * 2, sB = sA + 1;
     unsigned char *oA = 2 * sA < a.n_gen ? a.out + (size_t)sA * a.out_stride : nullptr;
     unsigned char *oB = 2 * sB < a.n_gen ? a.out + (size_t)sB * a.out_stride : nullptr;
     double *qst = &qs[r][0][lr];
-    double *vst = &vs[r][0][lr];
     unsigned clips = 0;
     double pk = 0.0;
     const int T = a.T;
-    int t = 0;
+    /* block j's inputs in LDS buffer j & 1: loaded at the end of block j - 3, stored at the end of
+     * block j - 2, read (a block ahead) during block j - 1 */
+    __shared__ double xsl[2][4][U], dsl[2][4][U];
+    IcwRowStage stg;
+    icw_rrow_stage_load(a, 0, lane, stg);
+    icw_rrow_stage_store(xsl[0], dsl[0], lane, stg);
+    icw_rrow_stage_load(a, U, lane, stg);
+    icw_rrow_stage_store(xsl[1], dsl[1], lane, stg);
+    icw_rrow_stage_load(a, 2 * U, lane, stg);
+    __builtin_amdgcn_wave_barrier();
     double xin[U], dv[U];
-    if (T >= U) {
 #pragma unroll
-        for (int j = 0; j < U; ++j) {
-            xin[j] = pp[(size_t)j * 2];
-            dv[j] = dp[(size_t)j * dpitch + dl];
-        }
-        for (; t + U <= T; t += U) {
-            /* look-ahead loads of the next block; the last full block re-reads a valid window */
-            const int tn = t + 2 * U <= T ? t + U : T - U;
-            icw_rrow_block<KIND, NN, R, 0, MR>(xin, dv, prev_err, E, O, P, P2, c, k, qst, vst, pp + (size_t)tn * 2,
-                                           dp + (size_t)tn * dpitch, dpitch, dl);
-            icw_rrow_flush(qs, vs, r, lr, lane, U, k, clips, pk, oA ? oA + (size_t)t * 2 * osz : nullptr,
+    for (int j = 0; j < U; ++j) {
+        xin[j] = xsl[0][r][j];
+        dv[j] = dsl[0][r][j];
+    }
+    int t = 0, kb = 0;
+    for (; t + U <= T; t += U, ++kb) {
+        const int nb = (kb + 1) & 1;
+        icw_rrow_block<KIND, NN, R, 0, MR>(xin, dv, prev_err, E, O, P, P2, c, k, qst, &xsl[nb][r][0], &dsl[nb][r][0]);
+        icw_rrow_flush<MR>(qs, r, lr, lane, U, k, clips, pk, oA ? oA + (size_t)t * 2 * osz : nullptr,
                            oB ? oB + (size_t)t * 2 * osz : nullptr, osz);
-        }
+        /* block kb + 2 into the buffer block kb has left, block kb + 3 on its way */
+        icw_rrow_stage_store(xsl[kb & 1], dsl[kb & 1], lane, stg);
+        icw_rrow_stage_load(a, t + 3 * U, lane, stg);
+        __builtin_amdgcn_wave_barrier();
     }
     const int rem = T - t;
     if (rem > 0) {
-#pragma unroll
-        for (int j = 0; j < U; ++j) {
-            xin[j] = j < rem ? pp[(size_t)(t + j) * 2] : 0.0;
-            dv[j] = j < rem ? dp[(size_t)(t + j) * dpitch + dl] : 0.0;
-        }
-        icw_rrow_block_lim<KIND, NN, R, 0, MR>(xin, dv, prev_err, E, O, P, P2, c, k, qst, vst, rem);
-        icw_rrow_flush(qs, vs, r, lr, lane, rem, k, clips, pk, oA ? oA + (size_t)t * 2 * osz : nullptr,
-                       oB ? oB + (size_t)t * 2 * osz : nullptr, osz);
+        icw_rrow_block_lim<KIND, NN, R, 0, MR>(xin, dv, prev_err, E, O, P, P2, c, k, qst, rem);
+        icw_rrow_flush<MR>(qs, r, lr, lane, rem, k, clips, pk, oA ? oA + (size_t)t * 2 * osz : nullptr,
+                           oB ? oB + (size_t)t * 2 * osz : nullptr, osz);
         /* back to the block-start mapping: rotate left by rem mod R */
 #pragma unroll
         for (int q = 1; q < U; ++q)
