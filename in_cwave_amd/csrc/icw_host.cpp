@@ -82,7 +82,7 @@ struct DevState {
 /* streams confined to disjoint CU sets: K1 on k1_cus CUs spread over the device, the rest on
  * the other CUs (hipExtStreamCreateWithCUMask) */
 struct CuSplit {
-    int k1_cus = 0;
+    int k1_cus = 0, rest_cus = 0;
     hipStream_t k1 = nullptr, rest = nullptr, dith = nullptr, render = nullptr;
 };
 
@@ -117,6 +117,11 @@ struct icw_ctx {
      * SIMD) made K1 +21 % slower even alone (C3, 4-wave workgroups), 3 per CU +27 % beside K2, and 1
      * per CU leaves the frame-parallel kernels too few CUs (C4 K2 2.57 -> 3.70 ms) */
     int k1_wpc = 2;
+    /* ICW_REST_CUS: at most this many CUs for the frame-parallel kernels beside K1 (0: all the rest).
+     * Default (-1): all but 32 (4 per XCD) -- idle CUs leave K1 power headroom: C3 41.6-42.2k ->
+     * 42.6-42.9k, C4 20.9k -> 21.1-21.3k Msamples/s at 160 and 176 (profiles/r04_rest_cus.txt);
+     * below 160 K2 falls behind (C3 38.0k at 144 and 128) */
+    int rest_cus = -1;
     /* ICW_K1_WG: K1 waves per workgroup.  Default 1 for the lane kernel, 2 for the row kernel: its I and
      * Q filter waves of the same streams then share a CU, so the second one reads the channel rows
      * (one per channel since round 3) from the L2 / L1 the first one filled (C2 +0.7 %, C5 +0.4 %; the
@@ -686,15 +691,21 @@ void split_ref(int device, int delta)
 const CuSplit *cu_split(icw_ctx *c, int k1_cus)
 {
     std::lock_guard<std::mutex> lk(g_split_mu);
+    const int rest_cus = c->rest_cus >= 0 ? c->rest_cus : std::max(c->n_cu - k1_cus - 32, c->n_cu / 2);
     for (auto &x : g_splits)
-        if (x.first == c->device && x.second.k1_cus == k1_cus) return &x.second;
+        if (x.first == c->device && x.second.k1_cus == k1_cus && x.second.rest_cus == rest_cus) return &x.second;
     const int n = c->n_cu, words = (n + 31) / 32;
     std::vector<uint32_t> mk(words, 0u), mr(words, 0u);
     std::vector<char> used(n, 0);
     for (int i = 0; i < k1_cus && i < n; ++i) used[i] = 1;
-    for (int cu = 0; cu < n; ++cu) (used[cu] ? mk : mr)[cu / 32] |= 1u << (cu % 32);
+    int n_rest = 0;
+    for (int cu = 0; cu < n; ++cu) {
+        if (used[cu]) mk[cu / 32] |= 1u << (cu % 32);
+        else if (rest_cus == 0 || n_rest++ < rest_cus) mr[cu / 32] |= 1u << (cu % 32);
+    }
     CuSplit x;
     x.k1_cus = k1_cus;
+    x.rest_cus = rest_cus;
     if (hipExtStreamCreateWithCUMask(&x.k1, (uint32_t)words, mk.data()) != hipSuccess ||
         hipExtStreamCreateWithCUMask(&x.rest, (uint32_t)words, mr.data()) != hipSuccess ||
         hipExtStreamCreateWithCUMask(&x.dith, (uint32_t)words, mr.data()) != hipSuccess ||
@@ -992,6 +1003,8 @@ int icw_create(const icw_config *cfg, const icw_node *nodes, int n_nodes, int n_
         if (cs && !strcmp(cs, "0")) c->cu_split = false;
         const char *wpc = getenv("ICW_K1_WPC");
         if (wpc && atoi(wpc) >= 1 && atoi(wpc) <= 8) c->k1_wpc = atoi(wpc);
+        const char *rc = getenv("ICW_REST_CUS");
+        if (rc && (atoi(rc) == 0 || atoi(rc) >= 8)) c->rest_cus = atoi(rc);
         const char *bl = getenv("ICW_BLOCK");
         if (bl && atoi(bl) >= 256 && atoi(bl) <= kMaxBlockFrames) { c->max_block = atoi(bl); c->block_env = true; }
         const char *ns = getenv("ICW_SETS");
