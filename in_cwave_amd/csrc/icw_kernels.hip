@@ -1163,10 +1163,11 @@ __device__ __forceinline__ void icw_chain_sig(const IcwK2Args &a, icw_cprog *P, 
  *  - The render (sound_render_value, ROUND + flat shaper, sound_render.c:747-797): q = x * norm_mul +
  *    copysign(round_offset, x) -- for the mid-riser (offset 0) x + +-0 with x's own sign is x exactly,
  *    for the mid-tread it is the reference's x +- 0.5 except at x = -0.0, where -0.5 and +0.5 both
- *    truncate to 0 and have the same magnitude for the peak and the clip tests; the clip stage and the
- *    truncation as v_cvt_i32_f64 (it saturates out-of-range values) + v_med3_i32 into [lo + 1, hi - 1]
- *    (the same integer as min(q, hi - 1), max(., lo + 1), then (int), for every q that is not a NaN);
- *    a NaN q -- INT_MIN, as x86's cvttsd2si gives -- takes a divergent branch of its own. */
+ *    truncate to 0 and have the same magnitude for the peak and the clip tests; the truncation as
+ *    v_cvt_i32_f64, and the clip stage (v_med3_i32 into [lo + 1, hi - 1]: the same integer as
+ *    min(q, hi - 1), max(., lo + 1), then (int), for every q that is not a NaN) only in a pass whose
+ *    largest |q| reaches min(hi, -lo) -- below it the clamp changes nothing; a NaN q -- INT_MIN, as
+ *    x86's cvttsd2si gives -- takes a divergent branch of its own (icw_fast_render). */
 __device__ __forceinline__ int icw_cvt_sat_i32(double q)
 {
     int v;
@@ -1181,6 +1182,73 @@ __device__ __forceinline__ int icw_med3_i32(int x, int lo, int hi)
     return v;
 }
 
+/* max(m, |q|) and max(a, b) as one v_max_f64 each: IEEE maxNum returns the number for a quiet NaN
+ * operand, as fmax; written out because the compiler canonicalised both operands of every fmax here
+ * (two more v_max_f64 per sample).  The operands are sums and products, never signalling NaNs. */
+__device__ __forceinline__ double icw_vmax_abs(double m, double q)
+{
+    double r;
+    asm("v_max_f64 %0, %1, |%2|" : "=v"(r) : "v"(m), "v"(q));
+    return r;
+}
+
+__device__ __forceinline__ double icw_vmax(double a, double b)
+{
+    double r;
+    asm("v_max_f64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+
+/* The render of the R frames (see above).  MR: mid-riser, q = x (x + +-0.0 with x's sign is x) and
+ * delta = -1 below zero; mid-tread: q = copysign(|x| + 0.5, x), the reference's x +- 0.5 (-0.0 gives
+ * -0.5, harmless as above), delta 0.  The integer is the saturating conversion; the clamp to
+ * [lo + 1, hi - 1] is needed only where |q| reaches clip_abs = min(hi, -lo) -- the pass's meter test
+ * -- so it is applied there with the clip counts.  Then the NaN samples: INT_MIN (delta 0). */
+template <bool MR, int R>
+__device__ __forceinline__ void icw_fast_render(const IcwRenderK &rk, const double (&x)[R][2], int (&dv)[R][2],
+                                                double &lm_l, double &lm_r, unsigned &clip_l, unsigned &clip_r)
+{
+    double q[R][2];
+    int del[R][2];
+    bool nan = false;
+    lm_l = lm_r = 0.0;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+            if constexpr (MR) {
+                q[r][c] = x[r][c];
+                del[r][c] = x[r][c] < 0.0 ? -1 : 0;
+            } else {
+                q[r][c] = __builtin_copysign(fabs(x[r][c]) + rk.round_offset, x[r][c]);
+                del[r][c] = 0;
+            }
+            dv[r][c] = (int)((unsigned)(icw_cvt_sat_i32(q[r][c]) + del[r][c]) << rk.norm_shift);
+            nan |= q[r][c] != q[r][c];
+        }
+        lm_l = icw_vmax_abs(lm_l, q[r][0]);
+        lm_r = icw_vmax_abs(lm_r, q[r][1]);
+    }
+    if (icw_vmax(lm_l, lm_r) >= rk.clip_abs) {
+        const int lo1 = (int)rk.lo + 1, hi1 = (int)rk.hi - 1;
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            clip_l += (q[r][0] >= rk.hi ? 1u : 0u) + (q[r][0] <= rk.lo ? 1u : 0u);
+            clip_r += (q[r][1] >= rk.hi ? 1u : 0u) + (q[r][1] <= rk.lo ? 1u : 0u);
+#pragma unroll
+            for (int c = 0; c < 2; ++c)
+                dv[r][c] = (int)((unsigned)(icw_med3_i32(icw_cvt_sat_i32(q[r][c]), lo1, hi1) + del[r][c]) << rk.norm_shift);
+        }
+    }
+    if (nan) {
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+#pragma unroll
+            for (int c = 0; c < 2; ++c)
+                if (q[r][c] != q[r][c]) dv[r][c] = (int)(0x80000000u << rk.norm_shift);
+    }
+}
+
 template <bool TRIG, int R, int SIG, int I>
 __device__ __forceinline__ void icw_sig_fast_ops(const IcwK2Args &a, icw_cprog *P, const IcwLR (&in)[R],
                                                  IcwLR (&prev)[R], double (&lOut)[R], double (&rOut)[R],
@@ -1193,11 +1261,15 @@ __device__ __forceinline__ void icw_sig_fast_ops(const IcwK2Args &a, icw_cprog *
         double cs[R][2], sn[R][2];
         if constexpr (rot) {
             const int ts0 = op.tslot[0], ts1 = op.tslot[1];
+            /* a wave-uniform row base (SGPRs) + the lane's 32-bit byte offset: the loads' saddr form,
+             * no 64-bit address arithmetic per load */
+            const size_t lane_b = (size_t)(tro_lane * 8u);
 #pragma unroll
             for (int r = 0; r < R; ++r) {
-                const double *trow = a.trig_tab + tro_u + (size_t)r * tro_step + tro_lane;
-                const double2 f0 = *(const double2 *)(trow + ts0 * 2);
-                const double2 f1 = *(const double2 *)(trow + ts1 * 2);
+                const char *b0 = (const char *)(a.trig_tab + tro_u + (size_t)r * tro_step + ts0 * 2);
+                const char *b1 = (const char *)(a.trig_tab + tro_u + (size_t)r * tro_step + ts1 * 2);
+                const double2 f0 = *(const double2 *)(b0 + lane_b);
+                const double2 f1 = *(const double2 *)(b1 + lane_b);
                 cs[r][0] = f0.x; sn[r][0] = f0.y;
                 cs[r][1] = f1.x; sn[r][1] = f1.y;
             }
@@ -1272,7 +1344,7 @@ __device__ __forceinline__ void icw_sig_fast(const IcwK2Args &a, icw_cprog *P, c
     }
     icw_sig_fast_ops<TRIG, R, SIG, 0>(a, P, in, prev, lOut, rOut, tro_lane, tro_u, tro_step);
     const IcwRenderK &rk = a.rk;
-    double x[R][2], q[R][2];
+    double x[R][2];
 #pragma unroll
     for (int r = 0; r < R; ++r) { x[r][0] = lOut[r]; x[r][1] = rOut[r]; }
     if (rk.norm_mul != 1.0) {
@@ -1280,39 +1352,13 @@ __device__ __forceinline__ void icw_sig_fast(const IcwK2Args &a, icw_cprog *P, c
 #pragma unroll
         for (int r = 0; r < R; ++r) { x[r][0] *= rk.norm_mul; x[r][1] *= rk.norm_mul; }
     }
-    const int lo1 = (int)rk.lo + 1, hi1 = (int)rk.hi - 1;
-    int del[R][2];
-    bool nan = false;
-    double lm_l = 0.0, lm_r = 0.0;
-#pragma unroll
-    for (int r = 0; r < R; ++r) {
-#pragma unroll
-        for (int c = 0; c < 2; ++c) {
-            q[r][c] = x[r][c] + __builtin_copysign(rk.round_offset, x[r][c]);
-            del[r][c] = x[r][c] < 0.0 ? rk.sign_delta : 0;
-            const int v = icw_med3_i32(icw_cvt_sat_i32(q[r][c]), lo1, hi1);
-            dv[r][c] = (v + del[r][c]) << rk.norm_shift;
-            nan |= q[r][c] != q[r][c];
-        }
-        lm_l = fmax(lm_l, fabs(q[r][0]));
-        lm_r = fmax(lm_r, fabs(q[r][1]));
-    }
-    if (nan) {
-#pragma unroll
-        for (int r = 0; r < R; ++r)
-#pragma unroll
-            for (int c = 0; c < 2; ++c)
-                if (q[r][c] != q[r][c]) dv[r][c] = ((int)0x80000000 + del[r][c]) << rk.norm_shift;
-    }
-    pk_l = fmax(pk_l, lm_l);
-    pk_r = fmax(pk_r, lm_r);
-    if (fmax(lm_l, lm_r) >= rk.clip_abs) {
-#pragma unroll
-        for (int r = 0; r < R; ++r) {
-            clip_l += (q[r][0] >= rk.hi ? 1u : 0u) + (q[r][0] <= rk.lo ? 1u : 0u);
-            clip_r += (q[r][1] >= rk.hi ? 1u : 0u) + (q[r][1] <= rk.lo ? 1u : 0u);
-        }
-    }
+    double lm_l, lm_r;
+    if (rk.sign_delta != 0)
+        icw_fast_render<true, R>(rk, x, dv, lm_l, lm_r, clip_l, clip_r);
+    else
+        icw_fast_render<false, R>(rk, x, dv, lm_l, lm_r, clip_l, clip_r);
+    pk_l = icw_vmax(pk_l, lm_l);
+    pk_r = icw_vmax(pk_r, lm_r);
 }
 
 template <bool TRIG, int R, bool ROWP = false, int SIG = 0>
