@@ -169,6 +169,7 @@ struct IcwRenderK {
     double clip_abs;               /* min(hi, -lo): a q with |q| below it clips at neither bound */
     int32_t sign_delta, norm_shift, is24;
     int32_t render_type, ns_kind, ns_n;
+    int32_t lo1, hi1;              /* (int)lo + 1, (int)hi - 1: the clamp's integer bounds (scalar) */
     double ns_c[40];
 };
 

@@ -533,6 +533,8 @@ void render_consts(const icw_render_cfg &cfg, int is24, IcwRenderK &k)
     }
     k.lo -= (double)k.sign_delta;
     k.clip_abs = std::min(k.hi, -k.lo);
+    k.lo1 = (int32_t)k.lo + 1;
+    k.hi1 = (int32_t)k.hi - 1;
     k.is24 = is24;
     k.render_type = (int)cfg.render_type;
     unsigned t = cfg.nshape_type > ICW_NSHAPE_MAX ? ICW_NSHAPE_FLAT : cfg.nshape_type;

@@ -1230,14 +1230,17 @@ __device__ __forceinline__ void icw_fast_render(const IcwRenderK &rk, const doub
         lm_r = icw_vmax_abs(lm_r, q[r][1]);
     }
     if (icw_vmax(lm_l, lm_r) >= rk.clip_abs) {
-        const int lo1 = (int)rk.lo + 1, hi1 = (int)rk.hi - 1;
+        /* the host's integer bounds (SGPRs), integer min / max: (int)rk.lo is a VALU conversion, whose
+         * result the compiler hoisted to the kernel entry and spilled (+1.6 B of scratch writes per
+         * c2fir frame), and a v_med3_i32 wants VGPR operands */
+        const int lo1 = rk.lo1, hi1 = rk.hi1;
 #pragma unroll
         for (int r = 0; r < R; ++r) {
             clip_l += (q[r][0] >= rk.hi ? 1u : 0u) + (q[r][0] <= rk.lo ? 1u : 0u);
             clip_r += (q[r][1] >= rk.hi ? 1u : 0u) + (q[r][1] <= rk.lo ? 1u : 0u);
 #pragma unroll
             for (int c = 0; c < 2; ++c)
-                dv[r][c] = (int)((unsigned)(icw_med3_i32(icw_cvt_sat_i32(q[r][c]), lo1, hi1) + del[r][c]) << rk.norm_shift);
+                dv[r][c] = (int)((unsigned)(min(max(icw_cvt_sat_i32(q[r][c]), lo1), hi1) + del[r][c]) << rk.norm_shift);
         }
     }
     if (nan) {
@@ -2943,7 +2946,7 @@ __device__ __forceinline__ void icw_rrow_flush(const double (*qs)[ICW_MAX_NS_TAP
     const int sb = lane >> 5, f = lane & 31;
     unsigned char *o = sb ? o1 : o0;
     if (o && f < nf) {
-        const int lo1 = (int)k.lo + 1, hi1 = (int)k.hi - 1;
+        const int lo1 = k.lo1, hi1 = k.hi1;
         const int vl = icw_rrow_val<MR>(qs[2 * sb][f][0], lo1, hi1);
         const int vr = icw_rrow_val<MR>(qs[2 * sb + 1][f][0], lo1, hi1);
         const uint32_t l = (uint32_t)(vl << k.norm_shift);
