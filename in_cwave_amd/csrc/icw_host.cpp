@@ -503,6 +503,11 @@ int compile_graph(const std::vector<icw_node> &nodes, int bypass, IcwProg &P)
     if (plain) {
         P.sig = n_ops;
         for (int oi = 0; oi < n_ops; ++oi) P.sig |= ((P.ops[oi].mode & 3) | (P.ops[oi].chain_in << 2)) << (4 + 4 * oi);
+        /* bit 30: every op but the Master has gain 1.0 on both channels (ICW_SIG_UNIT) */
+        bool unit = true;
+        for (int oi = 0; oi < n_ops; ++oi)
+            if (P.ops[oi].mode != ICW_MODE_MASTER) unit &= P.ops[oi].gain[0] == 1.0 && P.ops[oi].gain[1] == 1.0;
+        if (unit) P.sig |= 1 << 30;
     }
     set_needs_omega(P);
     return ICW_OK;

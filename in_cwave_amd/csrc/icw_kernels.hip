@@ -901,6 +901,9 @@ __device__ __forceinline__ bool icw_exec_op(icw_cop &op, IcwLR d, double omega, 
 #define ICW_SIG_M    0x41
 #define ICW_SIG_SM   0x852
 #define ICW_SIG_PSXM 0x8F964
+/* flag: every op but the Master has gain 1.0 on both channels (the BASELINE lists' Shift / PM / Mix,
+ * DEF_GAIN_MOD in_cwave.h:166), so the render-only form skips those multiplies at compile time */
+#define ICW_SIG_UNIT (1 << 30)
 template <bool TRIG, int R, bool ROWP, int SIG, int I>
 __device__ __forceinline__ void icw_chain_sig(const IcwK2Args &a, icw_cprog *P, int t0, int T, const IcwLR (&in)[R],
                                               IcwLR (&prev)[R], double (&lOut)[R], double (&rOut)[R], double *bus_s,
@@ -927,7 +930,7 @@ __device__ __forceinline__ void icw_frame_graph(const IcwK2Args &a, icw_cprog *P
         double *bus_s = a.bus + (size_t)s * ICW_N_INPUTS * 4;
         if (last) { bus_s[0] = in.lre; bus_s[1] = in.lim; bus_s[2] = in.rre; bus_s[3] = in.rim; }
         double lOut = 0.0, rOut = 0.0;
-        const int sig = P->sig;
+        const int sig = P->sig & ~ICW_SIG_UNIT;
         if (P->chain && (sig == ICW_SIG_M || sig == ICW_SIG_SM || sig == ICW_SIG_PSXM) && (!TRIG || use_tab)) {
             /* a specialised chain signature, factors from the table (or none): the ops straight */
             IcwLR inr[1] = {in}, pv[1] = {in};
@@ -1289,13 +1292,14 @@ __device__ __forceinline__ void icw_sig_fast_ops(const IcwK2Args &a, icw_cprog *
                 d[r].lre = d[r].lim = d[r].rre = d[r].rim = 0.0;
             }
         }
+        constexpr bool unit = (SIG & ICW_SIG_UNIT) && mode != ICW_MODE_MASTER;
         const double g0 = op.gain[0], g1 = op.gain[1];
-        if (g0 != 1.0) {
+        if (!unit && g0 != 1.0) {
             asm volatile("");
 #pragma unroll
             for (int r = 0; r < R; ++r) { d[r].lre *= g0; d[r].lim *= g0; }
         }
-        if (g1 != 1.0) {
+        if (!unit && g1 != 1.0) {
             asm volatile("");
 #pragma unroll
             for (int r = 0; r < R; ++r) { d[r].rre *= g1; d[r].rim *= g1; }
@@ -1395,8 +1399,8 @@ __device__ __forceinline__ void icw_chain_frames(const IcwK2Args &a, icw_cprog *
     }
     if constexpr (SIG != 0) {
         /* a signature has no bypass: a bypassed list is the Master alone reading nothing (chain_in 0) */
-        icw_chain_sig<TRIG, R, ROWP, SIG, 0>(a, P, t0, T, in, prev, lOut, rOut, bus_s, has_last, lastr, tro_lane, tro_u,
-                                             tro_step);
+        icw_chain_sig<TRIG, R, ROWP, SIG & ~ICW_SIG_UNIT, 0>(a, P, t0, T, in, prev, lOut, rOut, bus_s, has_last, lastr,
+                                                             tro_lane, tro_u, tro_step);
     } else {
         const bool bypass = P->bypass != 0;
         for (int oi = 0; oi < P->n_ops; ++oi)
@@ -1445,16 +1449,25 @@ __device__ __forceinline__ void icw_chain_frames_rowp(const IcwK2Args &a, icw_cp
 {
     switch (sig) {
     case ICW_SIG_M:
-        icw_chain_frames<TRIG, R, true, ICW_SIG_M>(a, P, s, t0, nv, in, clip_l, clip_r, pk_l, pk_r, dv, tro_lane, tro_u,
-                                                   tro_step);
+    case ICW_SIG_M | ICW_SIG_UNIT:
+        icw_chain_frames<TRIG, R, true, ICW_SIG_M | ICW_SIG_UNIT>(a, P, s, t0, nv, in, clip_l, clip_r, pk_l, pk_r, dv,
+                                                                tro_lane, tro_u, tro_step);
         break;
     case ICW_SIG_SM:
         icw_chain_frames<TRIG, R, true, ICW_SIG_SM>(a, P, s, t0, nv, in, clip_l, clip_r, pk_l, pk_r, dv, tro_lane, tro_u,
                                                     tro_step);
         break;
+    case ICW_SIG_SM | ICW_SIG_UNIT:
+        icw_chain_frames<TRIG, R, true, ICW_SIG_SM | ICW_SIG_UNIT>(a, P, s, t0, nv, in, clip_l, clip_r, pk_l, pk_r, dv,
+                                                                 tro_lane, tro_u, tro_step);
+        break;
     case ICW_SIG_PSXM:
         icw_chain_frames<TRIG, R, true, ICW_SIG_PSXM>(a, P, s, t0, nv, in, clip_l, clip_r, pk_l, pk_r, dv, tro_lane, tro_u,
                                                       tro_step);
+        break;
+    case ICW_SIG_PSXM | ICW_SIG_UNIT:
+        icw_chain_frames<TRIG, R, true, ICW_SIG_PSXM | ICW_SIG_UNIT>(a, P, s, t0, nv, in, clip_l, clip_r, pk_l, pk_r, dv,
+                                                                   tro_lane, tro_u, tro_step);
         break;
     default:
         icw_chain_frames<TRIG, R, true>(a, P, s, t0, nv, in, clip_l, clip_r, pk_l, pk_r, dv, tro_lane, tro_u, tro_step);

@@ -20,8 +20,11 @@ def graphs():
     sm_gains = graph.graph_shift_master()
     sm_gains[0].gain[0] = sm_gains[0].gain[1] = 1.0      # Master gain 1.0
     sm_gains[1].gain[0] = 0.5                            # Shift L gain 0.5, R 1.0
+    psxm_gains = graph.graph_pm_shift_mix()
+    psxm_gains[1].gain[0] = 0.75                         # Mix gain 0.75 (locked: both channels)
     return {"master": graph.graph_master_only(), "shift_master": graph.graph_shift_master(),
-            "pm_shift_mix": graph.graph_pm_shift_mix(), "shift_master_gains": sm_gains}
+            "pm_shift_mix": graph.graph_pm_shift_mix(), "shift_master_gains": sm_gains,
+            "pm_shift_mix_gains": psxm_gains}
 
 
 def special_f32(n_streams, n, ch, seed):
@@ -47,7 +50,7 @@ def run(oracle, icw, cfg, nodes, raw, n, want_pre):
     return out, meters
 
 
-@pytest.mark.parametrize("gname", ["master", "shift_master", "pm_shift_mix", "shift_master_gains"])
+@pytest.mark.parametrize("gname", ["master", "shift_master", "pm_shift_mix", "shift_master_gains", "pm_shift_mix_gains"])
 @pytest.mark.parametrize("quantz", [abi.QUANTZ_MID_RISER, abi.QUANTZ_MID_TREAD])
 @pytest.mark.parametrize("b24,sign16", [(False, 16), (False, 11), (True, 16)])
 @pytest.mark.parametrize("fmt,ch", [(abi.FMT_I16, 2), (abi.FMT_F32, 2), (abi.FMT_F32, 1)])
@@ -77,3 +80,44 @@ def test_sig_fast_render(oracle, icw, gname, quantz, b24, sign16, fmt, ch, monke
         bad = np.flatnonzero(out[s] != ro)
         assert bad.size == 0, (s, bad[:8])
         assert meters[s] == st.meters(), (s, meters[s], st.meters())
+
+
+@pytest.mark.parametrize("gname,fb", [("shift_master", ("A",)), ("pm_shift_mix", ("C",))])
+@pytest.mark.parametrize("ch", [2, 1])
+def test_sig_fast_last_frame_and_bus(oracle, icw, gname, fb, ch, monkeypatch):
+    """Calls of whole tiles (4096 frames): the block's last frame sits in a tile the render-only
+    form takes, so its wave votes for the exact form -- the bus that frame leaves must be the
+    reference's.  The state blobs of a render-only context and an exact one are identical, and a
+    feedback list set afterwards reads the bus slots the first list wrote (adv_modulator.c:637-665)."""
+    monkeypatch.setenv("ICW_FIR_FUSED", "1")
+    cfg = graph.default_config(48000, channels=ch)
+    nodes = graphs()[gname]
+    slot = fb[0]
+    feedback = [graph.master(inputs=(slot,)), graph.mix(inputs=("in", slot), out=slot, gain=0.5)]
+    n, S = 4096, 2
+    raw = synth.batch_pcm(S, 2 * n, 48000, channels=ch, first=9)
+    fsz = 2 * ch
+    ctxs = []
+    for want_pre in (False, True):
+        ctx = icw.Context(cfg, nodes, S)
+        ctx.set_fir_hilbert(ORDER, BETA)
+        ctx.process(np.ascontiguousarray(raw[:, :n * fsz]), n, want_pre=want_pre)
+        ctxs.append(ctx)
+    for s in range(S):
+        assert bytes(ctxs[0].get_state(s)) == bytes(ctxs[1].get_state(s)), s
+    refs = []
+    for s in range(S):
+        st = oracle.Stream(cfg, nodes)
+        st.set_fir(ORDER, BETA)
+        st.process(raw[s, :n * fsz], n)
+        assert st.set_graph(feedback)
+        refs.append(st)
+    ctx = ctxs[0]
+    assert ctx.set_graph(feedback)
+    out, pre = ctx.process(np.ascontiguousarray(raw[:, n * fsz:]), n, want_pre=True)
+    for s, st in enumerate(refs):
+        ro, rp = st.process(raw[s, n * fsz:], n, want_pre=True)
+        assert np.array_equal(pre[s].view(np.uint64), rp.view(np.uint64)), s
+        assert np.array_equal(out[s], ro), s
+    for c in ctxs:
+        c.close()
