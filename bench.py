@@ -656,13 +656,13 @@ def main():
             except (SystemExit, Exception) as e:      # reported, never silently replaced
                 others["c1"] = {"error": repr(e)}
 
-    # ---- the CPU baseline: rank 0, after the last GPU barrier (never beside GPU timing); the other
-    # ranks wait for it at a final barrier
+    # ---- the CPU baseline: at N = 1 only (the task's contract), after the GPU legs (never beside GPU
+    # timing); a multi-GPU line carries null
     if dist:
         torch.cuda.synchronize()
         dist.barrier()
     cpu = None
-    if rank == 0 and not a.no_cpu_baseline:
+    if rank == 0 and world == 1 and not a.no_cpu_baseline:
         try:
             cpu = cpu_baseline(a.cpu_workers, a.cpu_frames, a.workload)
         except Exception as e:  # reported, never silently replaced

@@ -54,12 +54,10 @@ def test_bench_gpus_flag_self_launches():
     """python bench.py --gpus 2 with no launcher: two rank processes sharing the box's GPU (gloo),
     n_gpus 2 in the one line rank 0 prints, whole-job value; the multi-GPU line carries the C4 / C5
     legs BASELINE.json quotes at 8 GPUs (per-GPU shard sizes, whole-job values over the max-over-ranks
-    time), the roofline from rank 0's K1 events and the CPU baseline rank 0 runs after the last GPU
-    barrier"""
+    time) and the roofline from rank 0's K1 events; the CPU baseline is an N = 1 field (null here)"""
     env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK")}
     r = subprocess.run([sys.executable, "bench.py", "--gpus", "2", "--steps", "1", "--warmup", "1",
-                        "--frames", "32768", "--streams", "64", "--e2e-steps", "0", "--other-frames", "16384",
-                        "--cpu-frames", "65536", "--cpu-workers", "2"],
+                        "--frames", "32768", "--streams", "64", "--e2e-steps", "0", "--other-frames", "16384"],
                        cwd=ROOT, capture_output=True, text=True, timeout=600, env=env)
     assert r.returncode == 0, r.stderr[-3000:]
     d = _line(r.stdout)
@@ -68,8 +66,7 @@ def test_bench_gpus_flag_self_launches():
     assert d["config"]["control_backend"] == "gloo"
     assert abs(d["value"] - 2.0 * 2 * 64 * 32768 / (d["ms_per_step"] / 1e3) / 1e6) < 1e-6 * d["value"]
     assert d["roofline"]["avg_launch_ms"] > 0 and 0 < d["roofline"]["frac"] < 1
-    cpu = d["cpu_baseline"]
-    assert cpu and cpu["cores"] == 2 and cpu["value"] > 0, cpu
+    assert d["cpu_baseline"] is None
     ow = d["other_workloads"]
     for w, streams in (("c4", 2048), ("c5", 256), ("c4fir", 2048), ("c5fir", 256)):
         o = ow[w]
