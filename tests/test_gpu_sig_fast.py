@@ -1,5 +1,5 @@
 """GPU parity of the render-only form of the specialised chain programs (icw_sig_fast in
-icw_kernels.hip): calls that ask for no pre-render doubles run the BASELINE graphs' signatures
+icw_kernels.hip, KF2): calls that ask for no pre-render doubles run the BASELINE graphs' signatures
 without the reference's leading `0.0 +` per op input, with the division by SQRT2 tested once per op
 and the render's clip stage as a saturating conversion + integer clamp.  Its rendered bytes and
 meters must be the oracle's, and the exact form's (the same call asking for the doubles), for both
@@ -40,22 +40,27 @@ def special_f32(n_streams, n, ch, seed):
     return x.reshape(n_streams, -1).view(np.uint8)
 
 
-def run(oracle, icw, cfg, nodes, raw, n, want_pre):
+def run(oracle, icw, cfg, nodes, raw, n, want_pre, fir=True):
     S = raw.shape[0]
     ctx = icw.Context(cfg, nodes, S)
-    ctx.set_fir_hilbert(ORDER, BETA)
+    if fir:
+        ctx.set_fir_hilbert(ORDER, BETA)
     out, _ = ctx.process(raw, n, want_pre=want_pre)
     meters = [ctx.meters(s) for s in range(S)]
     ctx.close()
     return out, meters
 
 
+@pytest.mark.parametrize("path", ["fir", "iir"])
 @pytest.mark.parametrize("gname", ["master", "shift_master", "pm_shift_mix", "shift_master_gains", "pm_shift_mix_gains"])
 @pytest.mark.parametrize("quantz", [abi.QUANTZ_MID_RISER, abi.QUANTZ_MID_TREAD])
 @pytest.mark.parametrize("b24,sign16", [(False, 16), (False, 11), (True, 16)])
 @pytest.mark.parametrize("fmt,ch", [(abi.FMT_I16, 2), (abi.FMT_F32, 2), (abi.FMT_F32, 1)])
-def test_sig_fast_render(oracle, icw, gname, quantz, b24, sign16, fmt, ch, monkeypatch):
+def test_sig_fast_render(oracle, icw, path, gname, quantz, b24, sign16, fmt, ch, monkeypatch):
+    """fir: KF2's render-only passes of two frames per lane; iir: the same calls through K2's exact
+    frame graph (the quadrature IIR, K1 / K1r), against the same oracle"""
     monkeypatch.setenv("ICW_FIR_FUSED", "1")
+    fir = path == "fir"
     cfg = graph.default_config(48000, fmt=fmt, channels=ch, need24bits=b24)
     cfg.render.quantz_type = quantz
     cfg.render.sign_bits16 = sign16
@@ -69,22 +74,24 @@ def test_sig_fast_render(oracle, icw, gname, quantz, b24, sign16, fmt, ch, monke
         v = raw.view(np.int16).copy()
         v[:, 4000:4400] = np.where(v[:, 4000:4400] >= 0, 32767, -32768)
         raw = v.view(np.uint8)
-    out, meters = run(oracle, icw, cfg, nodes, raw, N, want_pre=False)
-    out_x, meters_x = run(oracle, icw, cfg, nodes, raw, N, want_pre=True)
+    out, meters = run(oracle, icw, cfg, nodes, raw, N, want_pre=False, fir=fir)
+    out_x, meters_x = run(oracle, icw, cfg, nodes, raw, N, want_pre=True, fir=fir)
     assert np.array_equal(out, out_x)
     assert meters == meters_x
     for s in range(S):
         st = oracle.Stream(cfg, nodes)
-        st.set_fir(ORDER, BETA)
+        if fir:
+            st.set_fir(ORDER, BETA)
         ro, _ = st.process(raw[s], N)
         bad = np.flatnonzero(out[s] != ro)
         assert bad.size == 0, (s, bad[:8])
         assert meters[s] == st.meters(), (s, meters[s], st.meters())
 
 
+@pytest.mark.parametrize("path", ["fir", "iir"])
 @pytest.mark.parametrize("gname,fb", [("shift_master", ("A",)), ("pm_shift_mix", ("C",))])
 @pytest.mark.parametrize("ch", [2, 1])
-def test_sig_fast_last_frame_and_bus(oracle, icw, gname, fb, ch, monkeypatch):
+def test_sig_fast_last_frame_and_bus(oracle, icw, path, gname, fb, ch, monkeypatch):
     """Calls of whole tiles (4096 frames): the block's last frame sits in a tile the render-only
     form takes, so its wave votes for the exact form -- the bus that frame leaves must be the
     reference's.  The state blobs of a render-only context and an exact one are identical, and a
@@ -100,7 +107,8 @@ def test_sig_fast_last_frame_and_bus(oracle, icw, gname, fb, ch, monkeypatch):
     ctxs = []
     for want_pre in (False, True):
         ctx = icw.Context(cfg, nodes, S)
-        ctx.set_fir_hilbert(ORDER, BETA)
+        if path == "fir":
+            ctx.set_fir_hilbert(ORDER, BETA)
         ctx.process(np.ascontiguousarray(raw[:, :n * fsz]), n, want_pre=want_pre)
         ctxs.append(ctx)
     for s in range(S):
@@ -108,7 +116,8 @@ def test_sig_fast_last_frame_and_bus(oracle, icw, gname, fb, ch, monkeypatch):
     refs = []
     for s in range(S):
         st = oracle.Stream(cfg, nodes)
-        st.set_fir(ORDER, BETA)
+        if path == "fir":
+            st.set_fir(ORDER, BETA)
         st.process(raw[s, :n * fsz], n)
         assert st.set_graph(feedback)
         refs.append(st)
