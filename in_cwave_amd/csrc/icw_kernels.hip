@@ -1161,22 +1161,24 @@ __device__ __forceinline__ void icw_chain_sig(const IcwK2Args &a, icw_cprog *P, 
 }
 
 /* The render-only form of a signature pass (no pre-render doubles requested, no lane holding the
- * block's last frame): the same rendered integers and meters in about a third of the instructions.
+ * block's last frame): the same rendered integers and meters in about half the instructions (KF2's
+ * graph phase, c2fir: ~800 -> ~410 VALU per wave, profiles/r04_c2fir_sq.json).
  *  - An op's input is the sum in + prev without the reference's leading 0.0 + (adv_modulator.c:655-665).
  *    0.0 + x differs from x only for x = -0.0, and in this arithmetic (products, sums, the division by
  *    SQRT2 -- no reciprocal, no sign test) a zero's sign changes nothing but zero signs downstream.
  *    The render cannot see one (below), so the integers and meters are the exact pass's; the pre-render
  *    doubles and the bus state can, which is why those calls and frames take icw_chain_frames' path.
- *  - A gain of 1.0 is branched over (the compiler had turned the uniform test into a multiply and
- *    two selects per double).
+ *  - Gains of 1.0 on every op but the Master (ICW_SIG_UNIT, the BASELINE lists) are left out at
+ *    compile time; any other gain of 1.0 is branched over (the compiler had turned the uniform test
+ *    into a multiply and two selects per double).
  *  - The division by SQRT2: icw_div_sqrt2's three operations for every value, then one test per value
  *    and one divergent branch per op for those outside its range.
  *  - The render (sound_render_value, ROUND + flat shaper, sound_render.c:747-797): q = x * norm_mul +
  *    copysign(round_offset, x) -- for the mid-riser (offset 0) x + +-0 with x's own sign is x exactly,
  *    for the mid-tread it is the reference's x +- 0.5 except at x = -0.0, where -0.5 and +0.5 both
  *    truncate to 0 and have the same magnitude for the peak and the clip tests; the truncation as
- *    v_cvt_i32_f64, and the clip stage (v_med3_i32 into [lo + 1, hi - 1]: the same integer as
- *    min(q, hi - 1), max(., lo + 1), then (int), for every q that is not a NaN) only in a pass whose
+ *    v_cvt_i32_f64 (saturating), and the clip stage (an integer clamp into [lo + 1, hi - 1]: the same
+ *    integer as min(q, hi - 1), max(., lo + 1), then (int), for every q that is not a NaN) only in a pass whose
  *    largest |q| reaches min(hi, -lo) -- below it the clamp changes nothing; a NaN q -- INT_MIN, as
  *    x86's cvttsd2si gives -- takes a divergent branch of its own (icw_fast_render). */
 __device__ __forceinline__ int icw_cvt_sat_i32(double q)
