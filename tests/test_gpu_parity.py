@@ -379,3 +379,32 @@ def test_meters_and_output_after_device_call_without_sync(oracle, icw):
         r = st.meters()
         assert meters[s]["clips"] == r["clips"] and meters[s]["peak_db"] == r["peak_db"], s
         assert meters[s]["desubnorm"] == r["desubnorm"], s
+
+
+@pytest.mark.parametrize("ns", [abi.NSHAPE_FLAT, abi.NSHAPE_FW44, abi.NSHAPE_MEW44, 9, abi.NSHAPE_MAX])
+def test_serial_render_short_and_ragged_calls(oracle, icw, ns):
+    """the serial renders over calls shorter than one, two and three 20-sample blocks and around
+    their multiples -- K3r stages a block's inputs in LDS two blocks ahead (its prologue reads past a
+    short call's end, its last block is partial) and rotates the shaper ring by the remainder; three
+    streams leave two spare rows in the second K3r wave; the state carries across the calls"""
+    cfg = graph.default_config(48000, need24bits=(ns % 2 == 1))
+    cfg.render.render_type = abi.RENDER_TPDF
+    cfg.render.nshape_type = ns
+    nodes = graph.graph_master_only()
+    lens = [1, 7, 19, 20, 21, 39, 40, 41, 59, 61, 100]
+    S = 3
+    raw = synth.batch_pcm(S, sum(lens), 48000, first=31)
+    ctx = icw.Context(cfg, nodes, S)
+    refs = [oracle.Stream(cfg, nodes) for _ in range(S)]
+    t = 0
+    for n in lens:
+        seg = np.ascontiguousarray(raw[:, t * 4:(t + n) * 4])
+        out, pre = ctx.process(seg, n, want_pre=True)
+        for s, st in enumerate(refs):
+            ro, rp = st.process(seg[s], n, want_pre=True)
+            assert np.array_equal(pre[s].view(np.uint64), rp.view(np.uint64)), (n, s)
+            assert np.array_equal(out[s], ro), (n, s)
+        t += n
+    for s, st in enumerate(refs):
+        assert ctx.meters(s) == st.meters(), s
+    ctx.close()
