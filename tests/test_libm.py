@@ -47,7 +47,7 @@ def test_div_sqrt2_hard_cases():
     so it can miss RN(x/c) only where x/c is that close to a rounding midpoint: for c = C 2^-52
     (C odd) those significands X solve (2M + 1) C - 2^s X = k, s = 53 (X >= C) or 54 (X < C), odd
     |k| < 8 -- one residue class mod C each.  Every such X (|k| <= 63, several binades) must give
-    RN(x/c), computed here in exact rationals; plus random values."""
+    RN(x/c), computed here in exact rationals; plus random values, and the range test on the result."""
     import math
     import random
     from fractions import Fraction as Fr
@@ -82,3 +82,15 @@ def test_div_sqrt2_hard_cases():
     for _ in range(20000):
         x = rng.uniform(-1e5, 1e5) * 2.0 ** rng.randint(-800, 900)
         assert fast(x) == float(Fr(x) / Fr(c)), x
+    # the device keeps the fast value only where |q| >= 2^-900 (icw_div_sqrt2_ok): around that bound
+    # and far below it, every kept value is RN(x / c), and from 2^-899.5 up every value is kept
+    kept = 0
+    for _ in range(4000):
+        x = rng.choice((-1.0, 1.0)) * rng.uniform(1.0, 2.0) * 2.0 ** rng.randint(-1074, -896)
+        q = fast(x)
+        if abs(q) >= 2.0 ** -900:
+            assert q == float(Fr(x) / Fr(c)), x
+            kept += 1
+        if abs(x) >= 2.0 ** -899.5:
+            assert abs(q) >= 2.0 ** -900, x
+    assert kept > 50
