@@ -1457,32 +1457,43 @@ __device__ __forceinline__ void icw_chain_frames_rowp(const IcwK2Args &a, icw_cp
                                                       double &pk_l, double &pk_r, int (&dv)[R][2], uint32_t tro_lane,
                                                       size_t tro_u, size_t tro_step)
 {
-    switch (sig) {
-    case ICW_SIG_M:
-    case ICW_SIG_M | ICW_SIG_UNIT:
-        icw_chain_frames<TRIG, R, true, ICW_SIG_M | ICW_SIG_UNIT>(a, P, s, t0, nv, in, clip_l, clip_r, pk_l, pk_r, dv,
-                                                                tro_lane, tro_u, tro_step);
-        break;
-    case ICW_SIG_SM:
-        icw_chain_frames<TRIG, R, true, ICW_SIG_SM>(a, P, s, t0, nv, in, clip_l, clip_r, pk_l, pk_r, dv, tro_lane, tro_u,
-                                                    tro_step);
-        break;
-    case ICW_SIG_SM | ICW_SIG_UNIT:
-        icw_chain_frames<TRIG, R, true, ICW_SIG_SM | ICW_SIG_UNIT>(a, P, s, t0, nv, in, clip_l, clip_r, pk_l, pk_r, dv,
-                                                                 tro_lane, tro_u, tro_step);
-        break;
-    case ICW_SIG_PSXM:
-        icw_chain_frames<TRIG, R, true, ICW_SIG_PSXM>(a, P, s, t0, nv, in, clip_l, clip_r, pk_l, pk_r, dv, tro_lane, tro_u,
-                                                      tro_step);
-        break;
-    case ICW_SIG_PSXM | ICW_SIG_UNIT:
-        icw_chain_frames<TRIG, R, true, ICW_SIG_PSXM | ICW_SIG_UNIT>(a, P, s, t0, nv, in, clip_l, clip_r, pk_l, pk_r, dv,
-                                                                   tro_lane, tro_u, tro_step);
-        break;
-    default:
-        icw_chain_frames<TRIG, R, true>(a, P, s, t0, nv, in, clip_l, clip_r, pk_l, pk_r, dv, tro_lane, tro_u, tro_step);
-        break;
+    /* a plain Shift / PM always rotates, so a kernel without TRIG sees only the Master signature and
+     * carries only that one: with all of them the mono kernel spilled in its loop (c3fir WRITE_SIZE
+     * 1.98 against 1.09 GB per launch).  The TRIG kernels keep the Master case they never take: without
+     * it the stereo kernel's allocation spilled instead (c2fir 96 against 67 MB). */
+    if constexpr (TRIG) {
+        switch (sig) {
+        case ICW_SIG_M:
+        case ICW_SIG_M | ICW_SIG_UNIT:
+            icw_chain_frames<TRIG, R, true, ICW_SIG_M | ICW_SIG_UNIT>(a, P, s, t0, nv, in, clip_l, clip_r, pk_l, pk_r,
+                                                                    dv, tro_lane, tro_u, tro_step);
+            return;
+        case ICW_SIG_SM:
+            icw_chain_frames<TRIG, R, true, ICW_SIG_SM>(a, P, s, t0, nv, in, clip_l, clip_r, pk_l, pk_r, dv, tro_lane,
+                                                        tro_u, tro_step);
+            return;
+        case ICW_SIG_SM | ICW_SIG_UNIT:
+            icw_chain_frames<TRIG, R, true, ICW_SIG_SM | ICW_SIG_UNIT>(a, P, s, t0, nv, in, clip_l, clip_r, pk_l, pk_r,
+                                                                     dv, tro_lane, tro_u, tro_step);
+            return;
+        case ICW_SIG_PSXM:
+            icw_chain_frames<TRIG, R, true, ICW_SIG_PSXM>(a, P, s, t0, nv, in, clip_l, clip_r, pk_l, pk_r, dv, tro_lane,
+                                                          tro_u, tro_step);
+            return;
+        case ICW_SIG_PSXM | ICW_SIG_UNIT:
+            icw_chain_frames<TRIG, R, true, ICW_SIG_PSXM | ICW_SIG_UNIT>(a, P, s, t0, nv, in, clip_l, clip_r, pk_l,
+                                                                       pk_r, dv, tro_lane, tro_u, tro_step);
+            return;
+        default: break;
+        }
+    } else {
+        if (sig == ICW_SIG_M || sig == (ICW_SIG_M | ICW_SIG_UNIT)) {
+            icw_chain_frames<TRIG, R, true, ICW_SIG_M | ICW_SIG_UNIT>(a, P, s, t0, nv, in, clip_l, clip_r, pk_l, pk_r, dv,
+                                                                    tro_lane, tro_u, tro_step);
+            return;
+        }
     }
+    icw_chain_frames<TRIG, R, true>(a, P, s, t0, nv, in, clip_l, clip_r, pk_l, pk_r, dv, tro_lane, tro_u, tro_step);
 }
 
 /* per-workgroup meters (ICW_K2_TILE threads): wave reduce, LDS, one atomic per stream/channel */
