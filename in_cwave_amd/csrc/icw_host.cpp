@@ -57,6 +57,11 @@ constexpr int kDefBlockFrames = 1 << 14;   /* launch block: shorter pipeline fil
 constexpr int kSets = 3;                    /* most block scratch sets (ICW_SETS); default 2 */
 constexpr double kAutoTaper = 0.85;          /* tail block ratio where the taper is on by default */
 constexpr double kRowTaper = 0.25;           /* tail ratio of the row kernel's long blocks (no serial render) */
+/* FIR converter + serial render: the first blocks grow by this ratio from kFirRenderFirst frames (the
+ * render K3r takes ~2.6x the converter + dither generator's time per frame, so each block's
+ * converter and dither are done before the render of the block before it ends) */
+constexpr double kFirRenderRamp = 2.5;
+constexpr int kFirRenderFirst = 4096;
 constexpr int kRowRenderMax = 2048;          /* channels up to which the render runs a row per channel */
 constexpr size_t kPinnedStage = 1u << 20;   /* host-pointer calls up to this size stage through pinned memory */
 
@@ -610,8 +615,9 @@ int grow(void **p, size_t *cur, size_t need)
  *   - the first block is `first` frames, long enough that K1 of it covers K0 of the next full one;
  *   - the tail shrinks geometrically (ratio r) down to `tmin`, so that K2 of every tail block, which
  *     runs beside K1 of the next one, stays no longer than that K1 (C4: K2 ~0.8 K1 per frame).
- * Block sizes stay multiples of 64 frames; short calls keep uniform blocks. */
-std::vector<std::pair<int, int>> plan_blocks(int n_frames, int Tb, int first, double r, int tmin)
+ * With `ramp` > 1 the blocks after the first grow by that ratio up to Tb (the FIR converter's fill,
+ * below).  Block sizes stay multiples of 64 frames; short calls keep uniform blocks. */
+std::vector<std::pair<int, int>> plan_blocks(int n_frames, int Tb, int first, double r, int tmin, double ramp = 0.0)
 {
     std::vector<std::pair<int, int>> bl;
     std::vector<int> tail;
@@ -623,15 +629,21 @@ std::vector<std::pair<int, int>> plan_blocks(int n_frames, int Tb, int first, do
         if (sum > n_frames / 2) tail.clear();
     }
     int t = 0;
+    double grow = 0.0;
     if (shape && first >= 64 && first < Tb) {
         bl.emplace_back(0, first);
         t = first;
+        if (ramp > 1.0) grow = first * ramp;
     }
     long tail_sum = 0;
     for (int v : tail) tail_sum += v;
     const int body_end = n_frames - (int)tail_sum;
     while (t < body_end) {
-        const int T = std::min(Tb, body_end - t);
+        int T = std::min(Tb, body_end - t);
+        if (grow > 0.0 && grow < Tb) {
+            T = std::min(T, std::max(64, ((int)grow) & ~63));
+            grow *= ramp;
+        }
         bl.emplace_back(t, T);
         t += T;
     }
@@ -1469,8 +1481,13 @@ int icw_process_streams(icw_ctx *c, int first, int count, const void *in, size_t
     const int Tb = std::min(n_frames, ((fir_fused || row_long) && !c->block_env) ? kMaxBlockFrames : c->max_block);
     const double taper = c->taper >= 0.0 ? c->taper
                        : (!cw && k1_mode == 3) ? (c->serial_render ? kAutoTaper : (row_long ? kRowTaper : 0.0)) : 0.0;
+    /* the fused FIR converter with a serial render (c5fir): the render of block 0 waits for its
+     * converter and dither alone, so block 0 is short and the next ones ramp up (kFirRenderRamp:
+     * profiles/r04_c5fir_timeline_after.txt had 2.2 ms of fill in a 24.3 ms step) */
+    const bool fir_ramp = fir_fused && c->serial_render && !c->block_env && c->first_block > 0;
     const std::vector<std::pair<int, int>> blocks =
-        plan_blocks(n_frames, Tb, fir_fused ? 0 : c->first_block, taper, c->taper_min);
+        fir_ramp ? plan_blocks(n_frames, Tb, std::min(kFirRenderFirst, c->first_block), 0.0, c->taper_min, kFirRenderRamp)
+                 : plan_blocks(n_frames, Tb, fir_fused ? 0 : c->first_block, taper, c->taper_min);
     const int n_blocks = (int)blocks.size();
     /* K5 (icw_stream1): one stream, one block, the row recurrence, register-form graph, ROUND / flat */
     const bool s1 = c->stream1 && count == 1 && n_blocks == 1 && !cw && !fcm && k1_mode == 3 && !c->serial_render &&
