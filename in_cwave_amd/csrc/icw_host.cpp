@@ -62,6 +62,10 @@ constexpr double kRowTaper = 0.25;           /* tail ratio of the row kernel's l
  * converter and dither are done before the render of the block before it ends) */
 constexpr double kFirRenderRamp = 2.5;
 constexpr int kFirRenderFirst = 4096;
+/* the fused FIR converter on device buffers with nothing after it (no serial render, no host copies
+ * to overlap): one launch block per 2^20 frames.  At 65 536 each block paid a rotation-table launch
+ * and two ~12 us gaps beside its 0.26 ms kernel, 13 % of a c2fir step */
+constexpr int kMaxFirBlockFrames = 1 << 20;
 constexpr int kRowRenderMax = 2048;          /* channels up to which the render runs a row per channel */
 constexpr size_t kPinnedStage = 1u << 20;   /* host-pointer calls up to this size stage through pinned memory */
 
@@ -1478,7 +1482,9 @@ int icw_process_streams(icw_ctx *c, int first, int count, const void *in, size_t
      * (65 536 -> 16 384 -> 4 096 -> 1 024: the drain stays one short K2) measured +0.8 % on C2
      * (3 170 -> 3 196 Msamples/s; 32 768 with r = 0.5 +0.5 %, 65 536 with no tail +0.5 %). */
     const bool row_long = !cw && k1_mode == 3 && !c->serial_render && !c->block_env && n_frames >= 4 * kMaxBlockFrames;
-    const int Tb = std::min(n_frames, ((fir_fused || row_long) && !c->block_env) ? kMaxBlockFrames : c->max_block);
+    const bool fir_long = fir_fused && dev && !c->serial_render && !bus;
+    const int Tb = std::min(n_frames, ((fir_fused || row_long) && !c->block_env)
+                                          ? (fir_long ? kMaxFirBlockFrames : kMaxBlockFrames) : c->max_block);
     const double taper = c->taper >= 0.0 ? c->taper
                        : (!cw && k1_mode == 3) ? (c->serial_render ? kAutoTaper : (row_long ? kRowTaper : 0.0)) : 0.0;
     /* the fused FIR converter with a serial render (c5fir): the render of block 0 waits for its
