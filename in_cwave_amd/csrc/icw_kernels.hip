@@ -1770,10 +1770,14 @@ __global__ __launch_bounds__(256, ICW_FIR_OCC) void icw_fir_graph(IcwFirArgs f, 
     extern __shared__ double lds[];
     __shared__ unsigned red_clip[2][ICW_K2_TILE / 64];
     __shared__ double red_pk[2][ICW_K2_TILE / 64];
-    const int s = blockIdx.y;
+    /* workgroups in stream-fastest order (the grid is tiles x streams): the workgroups of one tile run
+     * together, so its rotation-table rows come from the L2 for every stream, where tile-fastest order
+     * swept the whole block's table once per stream (a 2^20-frame block's table is 32 MB) */
+    const int wgid = blockIdx.y * gridDim.x + blockIdx.x;
+    const int s = wgid % gridDim.y;
     constexpr int nchc = NC;
     const int TF = 256 * ICW_FIR_R / nchc;
-    const int tt = blockIdx.x * TF;
+    const int tt = (wgid / (int)gridDim.y) * TF;
     const int M = f.M, c = M >> 1;
     const int sh = (8 - ((c - 1) & 7)) & 7;
     const int av = (c - 1 + sh) >> 3;
