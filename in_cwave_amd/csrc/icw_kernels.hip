@@ -1770,14 +1770,14 @@ __global__ __launch_bounds__(256, ICW_FIR_OCC) void icw_fir_graph(IcwFirArgs f, 
     extern __shared__ double lds[];
     __shared__ unsigned red_clip[2][ICW_K2_TILE / 64];
     __shared__ double red_pk[2][ICW_K2_TILE / 64];
-    /* workgroups in stream-fastest order (the grid is tiles x streams): the workgroups of one tile run
+    /* workgroups in stream-fastest order (the grid is streams x tiles): the workgroups of one tile run
      * together, so its rotation-table rows come from the L2 for every stream, where tile-fastest order
-     * swept the whole block's table once per stream (a 2^20-frame block's table is 32 MB) */
-    const int wgid = blockIdx.y * gridDim.x + blockIdx.x;
-    const int s = wgid % gridDim.y;
+     * swept the whole block's table once per stream (a 2^20-frame block's table is 32 MB: c2fir 37 HBM
+     * bytes per frame against 9.4) */
+    const int s = blockIdx.x;
     constexpr int nchc = NC;
     const int TF = 256 * ICW_FIR_R / nchc;
-    const int tt = (wgid / (int)gridDim.y) * TF;
+    const int tt = blockIdx.y * TF;
     const int M = f.M, c = M >> 1;
     const int sh = (8 - ((c - 1) & 7)) & 7;
     const int av = (c - 1 + sh) >> 3;
@@ -3234,7 +3234,7 @@ template <int NC>
 static hipError_t launch_fir_graph_nc(const IcwFirArgs *f, const IcwK2Args *a, int in_step, size_t lds, hipStream_t st)
 {
     const int TF = 256 * ICW_FIR_R / NC;
-    dim3 grid((f->T + TF - 1) / TF, f->n_streams);
+    dim3 grid(f->n_streams, (f->T + TF - 1) / TF);        /* stream-fastest (icw_fir_graph); <= 1 024 tiles */
     const void *fn = !a->trig ? (const void *)icw_fir_graph<false, false, NC>
                    : in_step ? (const void *)icw_fir_graph<true, true, NC> : (const void *)icw_fir_graph<true, false, NC>;
     if (fir_lds_attr(fn, lds) != hipSuccess) return hipErrorInvalidValue;
