@@ -131,6 +131,7 @@ struct icw_ctx {
      * 42.6-42.9k, C4 20.9k -> 21.1-21.3k Msamples/s at 160 and 176 (profiles/r04_rest_cus.txt);
      * below 160 K2 falls behind (C3 38.0k at 144 and 128) */
     int rest_cus = -1;
+    double fir_ramp = 0.0;                /* ICW_FIR_RAMP: the ramp of a FIR + serial-render call (0: kFirRenderRamp) */
     /* ICW_K1_WG: K1 waves per workgroup.  Default 1 for the lane kernel, 2 for the row kernel: its I and
      * Q filter waves of the same streams then share a CU, so the second one reads the channel rows
      * (one per channel since round 3) from the L2 / L1 the first one filled (C2 +0.7 %, C5 +0.4 %; the
@@ -152,6 +153,7 @@ struct icw_ctx {
      * streams) r = 0.85 measured +2 %.  So it is on by default for the row kernel with a serial
      * render only (icw_process_streams). */
     int first_block = 4096;               /* ICW_FIRST_BLOCK (0: uniform blocks) */
+    bool first_block_env = false;
     double taper = -1.0;                  /* ICW_TAPER: tail block ratio (0: no tail; -1: auto) */
     int taper_min = 1024;                 /* ICW_TAPER_MIN: smallest tail block */
     /* dither generation (K3a) runs on its own stream, double-buffered like the block scratch */
@@ -1026,6 +1028,8 @@ int icw_create(const icw_config *cfg, const icw_node *nodes, int n_nodes, int n_
         if (cs && !strcmp(cs, "0")) c->cu_split = false;
         const char *wpc = getenv("ICW_K1_WPC");
         if (wpc && atoi(wpc) >= 1 && atoi(wpc) <= 8) c->k1_wpc = atoi(wpc);
+        const char *fr = getenv("ICW_FIR_RAMP");
+        if (fr && atof(fr) > 1.0 && atof(fr) <= 16.0) c->fir_ramp = atof(fr);
         const char *rc = getenv("ICW_REST_CUS");
         if (rc && (atoi(rc) == 0 || atoi(rc) >= 8)) c->rest_cus = atoi(rc);
         const char *bl = getenv("ICW_BLOCK");
@@ -1037,7 +1041,7 @@ int icw_create(const icw_config *cfg, const icw_node *nodes, int n_nodes, int n_
         const char *sw = getenv("ICW_SPIN");
         if (sw && !strcmp(sw, "0")) c->spin_wait = false;
         const char *fb = getenv("ICW_FIRST_BLOCK");
-        if (fb && atoi(fb) >= 0) c->first_block = atoi(fb);
+        if (fb && atoi(fb) >= 0) { c->first_block = atoi(fb); c->first_block_env = true; }
         const char *tp = getenv("ICW_TAPER");
         if (tp && atof(tp) >= 0.0 && atof(tp) < 1.0) c->taper = atof(tp);
         const char *tm = getenv("ICW_TAPER_MIN");
@@ -1492,7 +1496,8 @@ int icw_process_streams(icw_ctx *c, int first, int count, const void *in, size_t
      * profiles/r04_c5fir_timeline_after.txt had 2.2 ms of fill in a 24.3 ms step) */
     const bool fir_ramp = fir_fused && c->serial_render && !c->block_env && c->first_block > 0;
     const std::vector<std::pair<int, int>> blocks =
-        fir_ramp ? plan_blocks(n_frames, Tb, std::min(kFirRenderFirst, c->first_block), 0.0, c->taper_min, kFirRenderRamp)
+        fir_ramp ? plan_blocks(n_frames, Tb, c->first_block_env ? c->first_block : kFirRenderFirst, 0.0, c->taper_min,
+                               c->fir_ramp > 0.0 ? c->fir_ramp : kFirRenderRamp)
                  : plan_blocks(n_frames, Tb, fir_fused ? 0 : c->first_block, taper, c->taper_min);
     const int n_blocks = (int)blocks.size();
     /* K5 (icw_stream1): one stream, one block, the row recurrence, register-form graph, ROUND / flat */
