@@ -284,3 +284,40 @@ def test_fir_chain_frames_round_renders(oracle, icw, ch, b24, nodes):
     ctx, out, pre, ro, rp = run_fir(oracle, icw, cfg, nodes, raw, 5003, 254, blocks=[2049, 7, 2947])
     assert_parity(out, pre, ro, rp)
     ctx.close()
+
+
+def test_fir_long_blocks_device_buffers(oracle, icw):
+    """device buffers, nothing after the converter: launch blocks of 2^20 frames (icw_host.cpp
+    kMaxFirBlockFrames) -- a call of two blocks (the history hand-off between them in the device's
+    double buffer, no copy-back) and then a call of one (odd: copy-back), against the oracle with the
+    stream-fastest grid of three streams"""
+    import torch
+    cfg = graph.default_config(48000)
+    nodes = graph.graph_shift_master()
+    S, n1, n2 = 3, (1 << 20) + 3000, 70000
+    raw = synth.batch_pcm(S, n1 + n2, 48000, first=41)
+    dev = torch.device("cuda", 0)
+    ctx = icw.Context(cfg, nodes, S, device=0)
+    ctx.set_fir_hilbert(254, BETA)
+    osz = 2 * ctx.render_size
+    outs = []
+    t = 0
+    for n in (n1, n2):
+        d_in = torch.from_numpy(np.ascontiguousarray(raw[:, t * 4:(t + n) * 4])).to(dev)
+        d_out = torch.empty((S, n * osz), dtype=torch.uint8, device=dev)
+        ctx.process_device(d_in, d_in.stride(0), d_out, d_out.stride(0), n)
+        torch.cuda.synchronize()
+        outs.append(d_out.cpu().numpy())
+        t += n
+    meters = [ctx.meters(s) for s in range(S)]
+    ctx.close()
+    for s in range(S):
+        st = oracle.Stream(cfg, nodes)
+        st.set_fir(254, BETA)
+        t = 0
+        for k, n in enumerate((n1, n2)):
+            ro, _ = st.process(raw[s, t * 4:(t + n) * 4], n)
+            assert np.array_equal(outs[k][s], ro), (s, k)
+            t += n
+        m, r = meters[s], st.meters()
+        assert tuple(m["clips"]) == tuple(r["clips"]) and tuple(m["peak_db"]) == tuple(r["peak_db"]), s
