@@ -126,8 +126,10 @@ def workload_config(w):
     if w["render"] == "tpdf24_mew44":
         cfg.render.render_type = abi.RENDER_TPDF
         cfg.render.nshape_type = abi.NSHAPE_MEW44
+    # ICW_BENCH_GRAPH (diagnostics only, never the headline): another of the three lists on the same shape
+    g = os.environ.get("ICW_BENCH_GRAPH") or w["graph"]
     nodes = {"shift_master": graph.graph_shift_master, "master_only": graph.graph_master_only,
-             "pm_shift_mix": graph.graph_pm_shift_mix}[w["graph"]]()
+             "pm_shift_mix": graph.graph_pm_shift_mix}[g]()
     return cfg, nodes, fmt
 
 
