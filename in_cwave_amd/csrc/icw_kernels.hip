@@ -1761,6 +1761,47 @@ extern "C" int icw_fir_stamps_read(unsigned long long *dst, size_t n)
 #define ICW_FIR_STAMP(k) do { } while (0)
 #endif
 
+/* KF2's mono chain form: the lane's ICW_FIR_R frames (from t0, nv of them in the block) two at a time
+ * through one signature (SIG; 0: the generic op loop, ROWP: rows at known offsets), the rendered
+ * frames packed into w (16-bit: w[0..8), 24-bit: 12 words) */
+template <bool TRIG, int SIG, bool ROWP>
+__device__ __forceinline__ void icw_mono_passes(const IcwK2Args &a, icw_cprog *P, int s, int t0, int nv,
+                                                const double (&vi)[ICW_FIR_R], const double (&q)[ICW_FIR_R],
+                                                unsigned &clip_l, unsigned &clip_r, double &pk_l, double &pk_r,
+                                                unsigned (&w)[ICW_FIR_R / 2 * 3], bool b24, uint32_t tro_lane,
+                                                size_t pq)
+{
+#pragma unroll
+    for (int hh = 0; hh < ICW_FIR_R; hh += 2) {
+        IcwLR in2[2];
+#pragma unroll
+        for (int r = 0; r < 2; ++r) {
+            in2[r].lre = in2[r].rre = vi[hh + r];
+            in2[r].lim = in2[r].rim = q[hh + r];
+        }
+        int dv[2][2];
+        const int n2 = min(2, max(nv - hh, 0));
+        if constexpr (!ROWP)
+            icw_chain_frames<TRIG, 2>(a, P, s, t0 + hh, n2, in2, clip_l, clip_r, pk_l, pk_r, dv);
+        else if constexpr (SIG != 0)
+            icw_chain_frames<TRIG, 2, true, SIG>(a, P, s, t0 + hh, n2, in2, clip_l, clip_r, pk_l, pk_r, dv, tro_lane,
+                                                 (size_t)hh * pq, pq);
+        else
+            icw_chain_frames<TRIG, 2, true>(a, P, s, t0 + hh, n2, in2, clip_l, clip_r, pk_l, pk_r, dv, tro_lane,
+                                            (size_t)hh * pq, pq);
+        if (b24) {
+            const unsigned l0 = (unsigned)dv[0][0] & 0xffffffu, r0 = (unsigned)dv[0][1] & 0xffffffu;
+            const unsigned l1 = (unsigned)dv[1][0] & 0xffffffu, r1 = (unsigned)dv[1][1] & 0xffffffu;
+            w[hh / 2 * 3 + 0] = l0 | (r0 << 24);
+            w[hh / 2 * 3 + 1] = (r0 >> 8) | (l1 << 16);
+            w[hh / 2 * 3 + 2] = (l1 >> 16) | (r1 << 8);
+        } else {
+            w[hh] = ((unsigned)dv[0][0] & 0xffffu) | ((unsigned)dv[0][1] << 16);
+            w[hh + 1] = ((unsigned)dv[1][0] & 0xffffu) | ((unsigned)dv[1][1] << 16);
+        }
+    }
+}
+
 /* ICW_FIR_OCC 5 (96 VGPRs) spills and ran 2.4x slower (profiles/r03_fir_swap_ab.jsonl) */
 template <bool TRIG, bool TAB, int NC>
 __global__ __launch_bounds__(256, ICW_FIR_OCC) void icw_fir_graph(IcwFirArgs f, IcwK2Args a)
@@ -1941,32 +1982,27 @@ __global__ __launch_bounds__(256, ICW_FIR_OCC) void icw_fir_graph(IcwFirArgs f, 
         const int sig = P->sig;
         const size_t pq = (size_t)a.trig_perm_q * a.trig_pitch;
         const uint32_t tro_lane = (uint32_t)(((size_t)(tt >> 3) + ll) * a.trig_pitch);
-#pragma unroll
-        for (int hh = 0; hh < ICW_FIR_R; hh += 2) {
-            IcwLR in2[2];
-#pragma unroll
-            for (int r = 0; r < 2; ++r) {
-                in2[r].lre = in2[r].rre = vi[hh + r];
-                in2[r].lim = in2[r].rim = q[hh + r];
+        /* the signature is chosen once for the lane's four passes (inside the pass loop every pass
+         * carried all variants while the eight inputs stayed live, and the rotating kernel spilled) */
+#define ICW_MONO(SIGV, RP) icw_mono_passes<TRIG, SIGV, RP>(a, P, s, tt + fr0, nf - fr0, vi, q, clip_l, clip_r, pk_l, pk_r, \
+                                                         w, b24, tro_lane, pq)
+        if (!rowp) {
+            ICW_MONO(0, false);
+        } else if constexpr (TRIG) {
+            switch (sig) {
+            case ICW_SIG_M:
+            case ICW_SIG_M | ICW_SIG_UNIT: ICW_MONO(ICW_SIG_M | ICW_SIG_UNIT, true); break;
+            case ICW_SIG_SM: ICW_MONO(ICW_SIG_SM, true); break;
+            case ICW_SIG_SM | ICW_SIG_UNIT: ICW_MONO(ICW_SIG_SM | ICW_SIG_UNIT, true); break;
+            case ICW_SIG_PSXM: ICW_MONO(ICW_SIG_PSXM, true); break;
+            case ICW_SIG_PSXM | ICW_SIG_UNIT: ICW_MONO(ICW_SIG_PSXM | ICW_SIG_UNIT, true); break;
+            default: ICW_MONO(0, true); break;
             }
-            int dv[2][2];
-            if (rowp)
-                icw_chain_frames_rowp<TRIG, 2>(a, P, sig, s, tt + fr0 + hh, min(2, max(nf - fr0 - hh, 0)), in2, clip_l,
-                                               clip_r, pk_l, pk_r, dv, tro_lane, (size_t)hh * pq, pq);
-            else
-                icw_chain_frames<TRIG, 2>(a, P, s, tt + fr0 + hh, min(2, max(nf - fr0 - hh, 0)), in2, clip_l, clip_r, pk_l,
-                                          pk_r, dv);
-            if (b24) {
-                const unsigned l0 = (unsigned)dv[0][0] & 0xffffffu, r0 = (unsigned)dv[0][1] & 0xffffffu;
-                const unsigned l1 = (unsigned)dv[1][0] & 0xffffffu, r1 = (unsigned)dv[1][1] & 0xffffffu;
-                w[hh / 2 * 3 + 0] = l0 | (r0 << 24);
-                w[hh / 2 * 3 + 1] = (r0 >> 8) | (l1 << 16);
-                w[hh / 2 * 3 + 2] = (l1 >> 16) | (r1 << 8);
-            } else {
-                w[hh] = ((unsigned)dv[0][0] & 0xffffu) | ((unsigned)dv[0][1] << 16);
-                w[hh + 1] = ((unsigned)dv[1][0] & 0xffffu) | ((unsigned)dv[1][1] << 16);
-            }
+        } else {
+            if (sig == ICW_SIG_M || sig == (ICW_SIG_M | ICW_SIG_UNIT)) ICW_MONO(ICW_SIG_M | ICW_SIG_UNIT, true);
+            else ICW_MONO(0, true);
         }
+#undef ICW_MONO
         unsigned char *o = a.out + (size_t)s * a.out_stride;
         const int nv = min(ICW_FIR_R, max(nf - fr0, 0));
         if (b24) {
