@@ -143,7 +143,7 @@ int main(int argc, char **argv)
     int status = 0;
     icw_mod_context *mc = icw_mod_context_create(&cfg, nodes, nn, -1, &status);
     if (!mc) { fprintf(stderr, "icw_mod_context_create: %s\n", icw_strerror(status)); return 1; }
-    status = icw_mod_context_fopen(mc, rate, fmt, channels, n_frames, 0, 0, 0, 0, 0);
+    status = icw_mod_context_fopen(mc, rate, fmt, channels, n_frames, 0, 0, 0, 0, 0, cfg.need24bits);
     if (status) { fprintf(stderr, "fopen: %s\n", icw_strerror(status)); return 1; }
     const int osz = icw_mod_context_out_size(mc);
 

@@ -135,6 +135,7 @@ SIGNATURES = {
     "icw_set_fir_hilbert": (_i, [_vp, C.c_int32, C.c_double]),
     "icw_set_graph": (_i, [_vp, C.POINTER(Node), _i, _i, C.POINTER(_i)]),
     "icw_set_render": (_i, [_vp, C.POINTER(RenderCfg)]),
+    "icw_set_outbits": (_i, [_vp, _i]),
     "icw_clear_bus_slot": (_i, [_vp, _i]),
     "icw_graph_del_last": (_i, [_vp]),
     "icw_graph_del_all": (_i, [_vp]),
@@ -148,7 +149,7 @@ SIGNATURES = {
     "icw_mod_context_destroy": (None, [_vp]),
     "icw_mod_context_ctx": (_vp, [_vp]),
     "icw_mod_context_fopen": (_i, [_vp, C.c_uint32, C.c_uint32, C.c_uint32, C.c_int64, C.c_uint32, C.c_uint32,
-                                   C.c_uint32, _i, _i]),
+                                   C.c_uint32, _i, _i, _i]),
     "icw_amod_process_samples": (_i, [_vp, _vp, _vp, _u]),
     "icw_mod_context_seek": (_i, [_vp, C.c_int64, _i]),
     "icw_mod_context_out_size": (_i, [_vp]),

@@ -61,9 +61,12 @@ void icw_mod_context_destroy(icw_mod_context *mc)
     free(mc);
 }
 
+/* mod_context_fopen (in_cwave.c:207-236): need24bits is read first (the.cfg.need24bits, :212), the
+ * reader and the clears follow, and the renders get the depth last (sound_render_set_outbits on both,
+ * :233-234); the caller's next buffers are sized from the new out_size (playback.c:215, transcode.c:55) */
 int icw_mod_context_fopen(icw_mod_context *mc, uint32_t sample_rate, uint32_t fmt, uint32_t channels,
                           int64_t n_samples, uint32_t fade_in_ms, uint32_t fade_out_ms, uint32_t sec_align,
-                          int clr_nframe, int clr_hilb)
+                          int clr_nframe, int clr_hilb, int need24bits)
 {
     int rc;
     if (!mc) return ICW_EINVAL;
@@ -72,7 +75,13 @@ int icw_mod_context_fopen(icw_mod_context *mc, uint32_t sample_rate, uint32_t fm
     mc->cfg.sample_rate = sample_rate;
     mc->cfg.in_format = fmt;
     mc->cfg.in_channels = channels;
-    return icw_stream_open(mc->ctx, 0, n_samples, fade_in_ms, fade_out_ms, sec_align, clr_nframe, clr_hilb);
+    rc = icw_stream_open(mc->ctx, 0, n_samples, fade_in_ms, fade_out_ms, sec_align, clr_nframe, clr_hilb);
+    if (rc != ICW_OK) return rc;
+    rc = icw_set_outbits(mc->ctx, need24bits);
+    if (rc != ICW_OK) return rc;
+    mc->cfg.need24bits = need24bits ? 1 : 0;
+    mc->out_size = 2 * icw_render_size(mc->ctx);
+    return ICW_OK;
 }
 
 int icw_amod_process_samples(char *buf, icw_mod_context *mc, const void *tbuff, unsigned n_frames)

@@ -226,6 +226,9 @@ struct icw_ctx {
     bool chain_ok = true;                 /* ICW_CHAIN=0: chain programs keep the LDS register file (A/B) */
     unsigned long long *s1_stamps = nullptr;   /* ICW_S1_STAMPS=1: K5 phase stamps, printed per call */
     unsigned long long calls = 0;         /* icw_process_* calls so far (icw_prepare needs a fresh context) */
+    /* per-stream state set by an entry point other than a call (stream_open, seek, set_state, the
+     * resets, set_outbits): icw_prepare's closing icw_stream_init would wipe it, so it refuses */
+    bool touched = false;
     std::mutex mu;
 };
 
@@ -1152,6 +1155,7 @@ int icw_stream_open(icw_ctx *c, int s, int64_t n_samples, uint32_t fade_in, uint
     std::lock_guard<std::mutex> lk(c->mu);
     if (set_dev(c)) return ICW_EDEVICE;
     long long fd[3] = {(long long)n_samples, nfi, nfo};
+    c->touched = true;
     bool ok = quiesce(c) == hipSuccess;
     ok &= hipMemcpy(c->st.fade + (size_t)s * 3, fd, sizeof(fd), hipMemcpyHostToDevice) == hipSuccess;
     ok &= hipMemset(c->st.pos + s, 0, sizeof(long long)) == hipSuccess;
@@ -1179,6 +1183,7 @@ int icw_stream_reset_hilbert(icw_ctx *c, int s)
     if (!c || s < 0 || s >= c->n_streams) return ICW_EINVAL;
     std::lock_guard<std::mutex> lk(c->mu);
     if (set_dev(c)) return ICW_EDEVICE;
+    c->touched = true;
     bool ok = quiesce(c) == hipSuccess;
     ok &= hipMemset(c->st.hist + (size_t)s * 4 * ICW_HIST_PITCH, 0, 4 * ICW_HIST_PITCH * sizeof(double)) == hipSuccess;
     ok &= hipMemset(c->st.sncnt + (size_t)s * 4, 0, 4 * sizeof(unsigned long long)) == hipSuccess;
@@ -1245,6 +1250,7 @@ int icw_stream_reset_framecnt(icw_ctx *c, int s)
     std::lock_guard<std::mutex> lk(c->mu);
     if (set_dev(c)) return ICW_EDEVICE;
     if (quiesce(c) != hipSuccess) return ICW_EDEVICE;
+    c->touched = true;
     c->nf_host[s] = 0;
     return hipMemset(c->st.n_frame + s, 0, sizeof(unsigned long long)) == hipSuccess ? ICW_OK : ICW_EDEVICE;
 }
@@ -1255,6 +1261,7 @@ int icw_stream_seek(icw_ctx *c, int s, int64_t frame_pos)
     std::lock_guard<std::mutex> lk(c->mu);
     if (set_dev(c)) return ICW_EDEVICE;
     long long v = (long long)frame_pos;
+    c->touched = true;
     bool ok = quiesce(c) == hipSuccess;
     ok &= hipMemcpy(c->st.pos + s, &v, sizeof(v), hipMemcpyHostToDevice) == hipSuccess;
     return ok ? ICW_OK : ICW_EDEVICE;
@@ -1377,6 +1384,35 @@ int icw_set_render(icw_ctx *c, const icw_render_cfg *r)
     if (c->st.rs && hipMemset(c->st.rs, 0, (size_t)c->n_streams * 2 * ICW_RSTATE * sizeof(double)) != hipSuccess)
         return ICW_EDEVICE;
     c->cfg.render = *r;
+    c->rk = k;
+    c->serial_render = serial;
+    return ICW_OK;
+}
+
+/* sound_render_set_outbits (sound_render.c:617-621) on both renders of every stream, as
+ * mod_context_fopen applies the.cfg.need24bits at every track open (in_cwave.c:212, 233-234): the
+ * new bounds, norm_mul and norm_shift, then sound_render_recalc (prev_rnd, the shaper rings and
+ * prev_ns_err restart; the MT19937 generators go on).  Applied even when the depth is unchanged,
+ * since recalc runs either way. */
+int icw_set_outbits(icw_ctx *c, int need24bits)
+{
+    if (!c) return ICW_EINVAL;
+    const int is24 = need24bits ? 1 : 0;
+    std::lock_guard<std::mutex> lk(c->mu);
+    if (set_dev(c) || quiesce(c) != hipSuccess) return ICW_EDEVICE;
+    IcwRenderK k;
+    render_consts(c->cfg.render, is24, k);
+    icw_config cfg = c->cfg;
+    cfg.need24bits = is24;
+    const bool serial = needs_serial(cfg, k, c->prog);
+    int rc;
+    if (serial && (rc = ensure_render_state(c))) return rc;
+    /* peaks so far in dB against the old bound (sound_render.c:769-780 converts each sample with the
+     * bound of its time) */
+    if (k.hi != c->rk.hi && !fold_peaks(c)) return ICW_EDEVICE;
+    if (c->st.rs && hipMemset(c->st.rs, 0, (size_t)c->n_streams * 2 * ICW_RSTATE * sizeof(double)) != hipSuccess)
+        return ICW_EDEVICE;
+    c->cfg.need24bits = is24;
     c->rk = k;
     c->serial_render = serial;
     return ICW_OK;
@@ -2143,7 +2179,7 @@ int icw_prepare(icw_ctx *c, int n_frames)
     const size_t S = (size_t)c->n_streams;
     {
         std::lock_guard<std::mutex> lk(c->mu);
-        if (c->calls) return ICW_EINVAL;          /* would have to restore state it cannot know */
+        if (c->calls || c->touched) return ICW_EINVAL;   /* would have to restore state it cannot know */
         if (set_dev(c)) return ICW_EDEVICE;
         const size_t widest = 2 * fmt_size(ICW_FMT_CW_F64), osz = 2 * 3;
         if (grow((void **)&c->d_in, &c->d_in_bytes, (size_t)n_frames * widest * S) ||
@@ -2318,6 +2354,7 @@ int icw_set_state(icw_ctx *c, int s, const void *blob, size_t size)
     std::lock_guard<std::mutex> lk(c->mu);
     if (set_dev(c)) return ICW_EDEVICE;
     long long fd[3] = {b.n_samples, b.n_fade_in, b.n_fade_out};
+    c->touched = true;
     bool ok = quiesce(c) == hipSuccess;
     ok &= hipMemcpy(c->st.n_frame + s, &b.n_frame, 8, hipMemcpyHostToDevice) == hipSuccess;
     c->nf_host[s] = b.n_frame;

@@ -190,6 +190,13 @@ class Context:
         self._own_cfg()
         self.cfg.render = render
 
+    def set_outbits(self, need24bits):
+        """sound_render_set_outbits for every stream (icw_set_outbits): 16 or 24 output bits"""
+        _check(self._lib.icw_set_outbits(self.h, int(bool(need24bits))), "icw_set_outbits")
+        self._own_cfg()
+        self.cfg.need24bits = int(bool(need24bits))
+        self.render_size = self._lib.icw_render_size(self.h)
+
     def set_hilbert_filter(self, type_):
         """mod_context_change_all_hilberts_filter (icw_set_hilbert_filter)"""
         _check(self._lib.icw_set_hilbert_filter(self.h, type_), "icw_set_hilbert_filter")

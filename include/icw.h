@@ -211,7 +211,8 @@ int icw_set_input(icw_ctx *ctx, uint32_t sample_rate, uint32_t fmt, uint32_t cha
  * icw_set_render  <- srenders_set_vcfg (in_cwave.c:457-469) -> sound_render_setup
  *                    (sound_render.c:625-629): the new SR_VCONFIG for both renders of every
  *                    stream; sound_render_recalc restarts prev_rnd, the shaper rings and
- *                    prev_ns_err, the MT19937 generators go on.  16/24 bits stay (need24bits).
+ *                    prev_ns_err, the MT19937 generators go on.  16/24 bits stay (need24bits;
+ *                    a new track's depth is icw_set_outbits below).
  * icw_set_hilbert_filter <- mod_context_change_all_hilberts_filter (in_cwave.c:186-199): a
  *                    different type re-creates every converter (hq_rp_create: zero rings, phase 0,
  *                    de-subnorm counters 0); the same type changes nothing.  type 0..5.
@@ -244,6 +245,15 @@ int icw_graph_del_all(icw_ctx *ctx);
 int icw_graph_add_last(icw_ctx *ctx, const icw_node *node);
 int icw_graph_set_output_plug(icw_ctx *ctx, int index, int n);
 int icw_set_render(icw_ctx *ctx, const icw_render_cfg *render);
+/* icw_set_outbits <- sound_render_set_outbits (sound_render.c:617-621), which mod_context_fopen
+ *                    applies to both renders with the.cfg.need24bits at every track open
+ *                    (in_cwave.c:212, 233-234; the GUI flips the flag between tracks,
+ *                    amod_gui_control.c:1641): 16 (0) or 24 (!= 0) output bits for every stream of
+ *                    the context.  New bounds, norm_mul and norm_shift, then sound_render_recalc:
+ *                    prev_rnd, the shaper rings and prev_ns_err restart (also at an unchanged
+ *                    depth), the MT19937 generators go on.  The peaks so far are kept in dB against
+ *                    the old bound; icw_render_size follows the new depth. */
+int icw_set_outbits(icw_ctx *ctx, int need24bits);
 int icw_set_hilbert_filter(icw_ctx *ctx, uint32_t type);
 int icw_set_hilbert_config(icw_ctx *ctx, int kahan, int subnorm_reject);
 
@@ -290,7 +300,10 @@ int icw_process_streams(icw_ctx *ctx, int first, int count, const void *in,
  * configuration takes, then the fresh state back (icw_stream_init).  The pinned staging, the device
  * buffers and the lazily loaded kernel code objects are then in place, so the first real call costs
  * what the later ones do -- the DecodeThread's first block (playback.c:619) included.
- * icw_mod_context_create calls it.  ICW_EINVAL once a call has been made. */
+ * icw_mod_context_create calls it.  ICW_EINVAL once a call has been made, or once per-stream state
+ * was set another way (icw_stream_open, _seek, _reset_hilbert, _reset_framecnt, icw_set_state), since
+ * the closing icw_stream_init would wipe it.  Context-wide settings (icw_set_input, _set_graph,
+ * _set_render, _set_outbits, the Hilbert setters) may come first: the warm-up runs with them. */
 int icw_prepare(icw_ctx *ctx, int n_frames);
 
 int icw_synchronize(icw_ctx *ctx);

@@ -36,10 +36,13 @@ void icw_mod_context_destroy(icw_mod_context *mc);
 
 /* mod_context_fopen (in_cwave.c:207-236): a new track with its own sample format.  The Hilbert
  * state and frame counter carry over unless clr_hilb / clr_nframe (is_clr_hilb_trk /
- * is_clr_nframe_trk, default FALSE); the renders' shaping state is reset, the RNG is not. */
+ * is_clr_nframe_trk, default FALSE).  need24bits is the.cfg.need24bits as the track opens
+ * (in_cwave.c:212): both renders take that depth (sound_render_set_outbits, :233-234, icw_set_outbits),
+ * their shaping state is reset, the RNG is not, and icw_mod_context_out_size follows (4 or 6 bytes
+ * per frame, the out_size playback.c:215 / transcode.c:55 size their buffers with). */
 int icw_mod_context_fopen(icw_mod_context *mc, uint32_t sample_rate, uint32_t fmt, uint32_t channels,
                           int64_t n_samples, uint32_t fade_in_ms, uint32_t fade_out_ms,
-                          uint32_t sec_align, int clr_nframe, int clr_hilb);
+                          uint32_t sec_align, int clr_nframe, int clr_hilb, int need24bits);
 
 /* The DSP half of amod_process_samples: render `n_frames` frames of raw interleaved input
  * (what xwave_read_samples left in xr->tbuff) into `buf` (interleaved L,R, 2 or 3 bytes LE
@@ -51,7 +54,8 @@ int icw_amod_process_samples(char *buf, icw_mod_context *mc, const void *tbuff, 
  * Playback also resets the Hilbert converters on seek (playback.c:594): reset_hilb = 1. */
 int icw_mod_context_seek(icw_mod_context *mc, int64_t frame_pos, int reset_hilb);
 
-/* sound_render_size(L) + sound_render_size(R): output bytes per frame (4 or 6) */
+/* sound_render_size(L) + sound_render_size(R): output bytes per frame (4 or 6) at the depth the
+ * last icw_mod_context_fopen set (icw_mod_context_create: cfg->need24bits) */
 int icw_mod_context_out_size(const icw_mod_context *mc);
 
 /* amod_get_clips_peaks (adv_modulator.c:445-465): reset clears the clips / peaks first and returns

@@ -825,6 +825,18 @@ void orc_set_hilbert_config(orc_stream *s, int kahan, int subn)
     }
 }
 
+/* sound_render_set_outbits (sound_render.c:617-621) on both renders: is24bits, then
+ * sound_render_recalc (new bounds; prev_rnd, shaper rings, prev_ns_err restart; the MT goes on).
+ * mod_context_fopen applies it with the.cfg.need24bits at every track open (in_cwave.c:212, 233-234). */
+void orc_set_outbits(orc_stream *s, int need24bits)
+{
+    for (int c = 0; c < 2; ++c) {
+        s->rd[c].is24 = need24bits ? 1 : 0;
+        render_recalc(&s->rd[c]);
+    }
+    s->cfg.need24bits = need24bits ? 1 : 0;
+}
+
 /* mod_context_fopen + xwave_reader_create fade/tail arithmetic; returns n_tail */
 int64_t orc_stream_open(orc_stream *s, int64_t n_samples, uint32_t fade_in, uint32_t fade_out,
                         uint32_t sec_align, int clr_nframe, int clr_hilb)

@@ -55,6 +55,7 @@ def load():
         lib.orc_set_graph.restype = C.c_int
         lib.orc_set_graph.argtypes = [vp, C.POINTER(abi.Node), C.c_int, C.c_int]
         lib.orc_set_render.argtypes = [vp, C.POINTER(abi.RenderCfg)]
+        lib.orc_set_outbits.argtypes = [vp, C.c_int]
         lib.orc_clear_inout.argtypes = [vp, C.c_int]
         lib.orc_share_meters.argtypes = [vp, vp]
         lib.orc_get_clips_peaks.argtypes = [vp, C.c_int, C.POINTER(abi.Meters)]
@@ -168,8 +169,20 @@ class Stream:
         load().orc_set_input(self.h, sample_rate, fmt, channels)
         self.fsz = abi.FMT_BYTES[fmt] * channels
 
-    def open(self, n_samples, fade_in_ms=0, fade_out_ms=0, sec_align=0, clr_nframe=0, clr_hilb=0):
-        return load().orc_stream_open(self.h, n_samples, fade_in_ms, fade_out_ms, sec_align, clr_nframe, clr_hilb)
+    def set_outbits(self, need24bits):
+        """sound_render_set_outbits on both renders (sound_render.c:617-621)"""
+        load().orc_set_outbits(self.h, int(bool(need24bits)))
+        self.osz = 2 * (3 if need24bits else 2)
+
+    def open(self, n_samples, fade_in_ms=0, fade_out_ms=0, sec_align=0, clr_nframe=0, clr_hilb=0,
+             need24bits=None):
+        """mod_context_fopen (in_cwave.c:207-236).  need24bits: the.cfg.need24bits as the track opens,
+        applied to both renders last (:233-234); None keeps the depth the stream has"""
+        n_tail = load().orc_stream_open(self.h, n_samples, fade_in_ms, fade_out_ms, sec_align, clr_nframe,
+                                        clr_hilb)
+        if need24bits is not None:
+            self.set_outbits(need24bits)
+        return n_tail
 
     def process(self, raw, n_frames, want_pre=False):
         raw = np.ascontiguousarray(raw, dtype=np.uint8)

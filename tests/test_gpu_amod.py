@@ -35,7 +35,7 @@ class _Mod:
         st = C.c_int()
         self.mc = self.lib.icw_mod_context_create(C.byref(cfg), arr, len(nodes), 0, C.byref(st))
         assert self.mc and st.value == abi.OK
-        assert self.lib.icw_mod_context_fopen(self.mc, fs, fmt, ch, n_samples, 0, 0, 0, 0, 0) == abi.OK
+        assert self.lib.icw_mod_context_fopen(self.mc, fs, fmt, ch, n_samples, 0, 0, 0, 0, 0, cfg.need24bits) == abi.OK
         self.ref = oracle.Stream(cfg, nodes)
         self.ref.set_input(fs, fmt, ch)
         self.ref.open(n_samples)
@@ -163,4 +163,89 @@ def test_graph_primitives_batched_context(oracle, icw):
             ro, rp = refs[s].process(seg[s], 1000, want_pre=True)
             assert np.array_equal(pre[s].view(np.uint64), rp.view(np.uint64)), (k, s)
             assert np.array_equal(out[s], ro), (k, s)
+    ctx.close()
+
+
+def _meters_equal(lib, m):
+    got = abi.Meters()
+    assert lib.icw_mod_context_meters(m.mc, 0, C.byref(got)) == abi.OK
+    want = m.ref.meters()
+    assert (got.clips[0], got.clips[1]) == want["clips"]
+    assert (got.peak_db[0], got.peak_db[1]) == want["peak_db"]
+    assert got.desubnorm == want["desubnorm"]
+
+
+def test_track_bit_depth_follows_fopen(oracle, icw):
+    """mod_context_fopen applies the.cfg.need24bits to both renders at every track open
+    (in_cwave.c:212, 233-234 -> sound_render_set_outbits, sound_render.c:617-621), and the GUI flips the
+    flag between tracks (amod_gui_control.c:1641).  One drop-in context, three tracks: 16-bit, then
+    24-bit, then 16-bit, 576-frame blocks (playback.c:619) with a short last block, a TPDF + MEW44
+    render (the generators go on across the tracks, the shaper state restarts at each open), no
+    is_clr_*: the Hilbert rings and the frame counter carry over.  Bytes and meters equal the oracle's
+    after every block, and out_size follows each track (playback.c:215 sizes the buffer from it)."""
+    cfg = graph.default_config(44100)
+    cfg.render.render_type = abi.RENDER_TPDF
+    cfg.render.nshape_type = abi.NSHAPE_MEW44
+    nodes = [graph.master(inputs=("A",), gain=1.6), graph.shift(inputs=("in",), out="A")]
+    lib = icw.load()
+    st = C.c_int()
+    mc = lib.icw_mod_context_create(C.byref(cfg), graph.node_array(nodes), len(nodes), 0, C.byref(st))
+    assert mc and st.value == abi.OK
+    ref = oracle.Stream(cfg, nodes)
+    m = type("M", (), {})()
+    m.mc, m.ref = mc, ref
+    tracks = [(44100, abi.FMT_I16, 2, False), (48000, abi.FMT_F32, 1, True), (44100, abi.FMT_I16, 2, False),
+              (96000, abi.FMT_I24, 2, True)]
+    for t, (fs, fmt, ch, b24) in enumerate(tracks):
+        n = 576 * 5 + 100
+        assert lib.icw_mod_context_fopen(mc, fs, fmt, ch, n, 0, 0, 0, 0, 0, int(b24)) == abi.OK
+        ref.set_input(fs, fmt, ch)
+        ref.open(n, need24bits=b24)
+        osz = lib.icw_mod_context_out_size(mc)
+        assert osz == (6 if b24 else 4)
+        if fmt == abi.FMT_I16:
+            raw = _loud_i16(n, fs, 20 + t, 0.95)
+        else:
+            raw = synth.stream_pcm(20 + t, n, fs, channels=ch, fmt=fmt)
+        fsz = abi.FMT_BYTES[fmt] * ch
+        for k in range(0, n, 576):
+            nb = min(576, n - k)
+            blk = np.ascontiguousarray(raw[k * fsz:(k + nb) * fsz])
+            buf = np.zeros(nb * osz, np.uint8)
+            assert lib.icw_amod_process_samples(buf.ctypes.data, mc, blk.ctypes.data, nb) == nb
+            ro, _ = ref.process(blk, nb)
+            assert np.array_equal(buf, ro), (t, k)
+            _meters_equal(lib, m)
+    lib.icw_mod_context_destroy(mc)
+
+
+@pytest.mark.parametrize("rtype,ns", [(abi.RENDER_ROUND, abi.NSHAPE_FLAT), (abi.RENDER_GAUSS, abi.NSHAPE_FLAT),
+                                      (abi.RENDER_RPDF, abi.NSHAPE_FW44)])
+def test_set_outbits_batched(oracle, icw, rtype, ns):
+    """icw_set_outbits on a many-stream context between calls (a new track on every stream): the
+    render-in-K2 ROUND path and the serial render, 24 -> 16 -> 24 bit, against per-stream oracles
+    given sound_render_set_outbits at the same points; pre-render doubles, bytes and meters"""
+    cfg = graph.default_config(48000, need24bits=True)
+    cfg.render.render_type = rtype
+    cfg.render.nshape_type = ns
+    nodes = graph.graph_pm_shift_mix()
+    S = 3
+    raw = synth.batch_pcm(S, 9000, 48000, first=60)
+    ctx = icw.Context(cfg, nodes, S)
+    refs = [oracle.Stream(cfg, nodes) for _ in range(S)]
+    for k, b24 in enumerate([True, False, True]):
+        if k:
+            ctx.set_outbits(b24)
+            for r in refs:
+                r.set_outbits(b24)
+        assert ctx.render_size == (3 if b24 else 2)
+        seg = np.ascontiguousarray(raw[:, k * 3000 * 4:(k + 1) * 3000 * 4])
+        out, pre = ctx.process(seg, 3000, want_pre=k == 1)
+        for s in range(S):
+            ro, rp = refs[s].process(seg[s], 3000, want_pre=k == 1)
+            assert np.array_equal(out[s], ro), (k, s)
+            if k == 1:
+                assert np.array_equal(pre[s].view(np.uint64), rp.view(np.uint64)), (k, s)
+            got, want = ctx.meters(s), refs[s].meters()
+            assert got["clips"] == want["clips"] and got["peak_db"] == want["peak_db"], (k, s)
     ctx.close()

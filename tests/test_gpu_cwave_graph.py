@@ -192,7 +192,7 @@ def test_dropin_boundary_takes_cwave(oracle, icw, fmt):
     osz = lib.icw_mod_context_out_size(mc)
     for track, (f, n) in enumerate([(abi.FMT_I16, 1700), (fmt, 2300)]):
         raw = synth.batch_pcm(1, n, fs, channels=2, fmt=f, first=11 + track)[0]
-        assert lib.icw_mod_context_fopen(mc, fs, f, 2, n, 0, 0, 0, 0, 0) == abi.OK
+        assert lib.icw_mod_context_fopen(mc, fs, f, 2, n, 0, 0, 0, 0, 0, cfg.need24bits) == abi.OK
         ref.set_input(fs, f, 2)
         ref.open(n)
         fsz = abi.FMT_BYTES[f] * 2

@@ -76,7 +76,7 @@ def test_stream1_drop_in_boundary(oracle, icw):
     mc = lib.icw_mod_context_create(C.byref(cfg), arr, len(nodes), 0, C.byref(st))
     assert mc and st.value == abi.OK
     n = 576 * 20
-    assert lib.icw_mod_context_fopen(mc, fs, abi.FMT_I16, 2, n, 20, 30, 0, 0, 0) == abi.OK
+    assert lib.icw_mod_context_fopen(mc, fs, abi.FMT_I16, 2, n, 20, 30, 0, 0, 0, cfg.need24bits) == abi.OK
     ref = oracle.Stream(cfg, nodes)
     ref.open(n, 20, 30)
     raw = synth.batch_pcm(1, n, fs, first=77)[0]
