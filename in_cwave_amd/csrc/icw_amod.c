@@ -146,38 +146,42 @@ int icw_amod_get_clips_peaks(icw_mod_context *const *mcs, int n, unsigned *lc, u
     return ICW_OK;
 }
 
+/* The list primitives over the contexts, in order, stopping at the first error (include/icw_amod.h).
+ * The contexts hold the same list, so a list refused by graph_accept (ICW_EGRAPH) is refused by the
+ * first context, before anything changed; only a device error after an earlier context took the edit
+ * leaves them apart, and the host then re-sends the whole list (icw_set_graph) to each. */
 int icw_amod_del_lastdsp(icw_mod_context *const *mcs, int n)
 {
-    int i, st, rc = ICW_OK;
+    int i, st;
     if (!mcs || n < 0) return ICW_EINVAL;
     for (i = 0; i < n; ++i)
-        if (mcs[i] && (st = icw_graph_del_last(mcs[i]->ctx)) != ICW_OK && rc == ICW_OK) rc = st;
-    return rc;
+        if (mcs[i] && (st = icw_graph_del_last(mcs[i]->ctx)) != ICW_OK) return st;
+    return ICW_OK;
 }
 
 int icw_amod_del_dsplist(icw_mod_context *const *mcs, int n)
 {
-    int i, st, rc = ICW_OK;
+    int i, st;
     if (!mcs || n < 0) return ICW_EINVAL;
     for (i = 0; i < n; ++i)
-        if (mcs[i] && (st = icw_graph_del_all(mcs[i]->ctx)) != ICW_OK && rc == ICW_OK) rc = st;
-    return rc;
+        if (mcs[i] && (st = icw_graph_del_all(mcs[i]->ctx)) != ICW_OK) return st;
+    return ICW_OK;
 }
 
 int icw_amod_add_lastdsp(icw_mod_context *const *mcs, int n, const icw_node *node)
 {
-    int i, st, rc = ICW_OK;
+    int i, st;
     if (!mcs || n < 0 || !node) return ICW_EINVAL;
     for (i = 0; i < n; ++i)
-        if (mcs[i] && (st = icw_graph_add_last(mcs[i]->ctx, node)) != ICW_OK && rc == ICW_OK) rc = st;
-    return rc;
+        if (mcs[i] && (st = icw_graph_add_last(mcs[i]->ctx, node)) != ICW_OK) return st;
+    return ICW_OK;
 }
 
 int icw_amod_set_output_plug(icw_mod_context *const *mcs, int n, int index, int plug)
 {
-    int i, st, rc = ICW_OK;
+    int i, st;
     if (!mcs || n < 0) return ICW_EINVAL;
     for (i = 0; i < n; ++i)
-        if (mcs[i] && (st = icw_graph_set_output_plug(mcs[i]->ctx, index, plug)) != ICW_OK && rc == ICW_OK) rc = st;
-    return rc;
+        if (mcs[i] && (st = icw_graph_set_output_plug(mcs[i]->ctx, index, plug)) != ICW_OK) return st;
+    return ICW_OK;
 }

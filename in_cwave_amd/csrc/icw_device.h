@@ -167,6 +167,9 @@ struct IcwProg {
 struct IcwRenderK {
     double norm_mul, dth_mul, hi, lo, round_offset;
     double clip_abs;               /* min(hi, -lo): a q with |q| below it clips at neither bound */
+    double spec_thr;               /* K3r: a 20-sample block whose every x * norm_mul is <= this in magnitude,
+                                      after a block whose every |q| < clip_abs, clips nowhere (render_consts);
+                                      -1: no clamp-free blocks */
     int32_t sign_delta, norm_shift, is24;
     int32_t render_type, ns_kind, ns_n;
     int32_t lo1, hi1;              /* (int)lo + 1, (int)hi - 1: the clamp's integer bounds (scalar) */

@@ -561,6 +561,26 @@ void render_consts(const icw_render_cfg &cfg, int is24, IcwRenderK &k)
     k.ns_n = icw_ns_n[t];
     const int nc = k.ns_kind == 2 ? 2 * k.ns_n : k.ns_n;
     for (int i = 0; i < nc; ++i) k.ns_c[i] = u2d(icw_ns_c[t][i]);
+    /* K3r's clamp-free blocks (icw_render_row).  Without a clip the error fed back is small: with
+     * q = input + d and the integer trunc(q) + delta (mid-riser) or trunc(q +- 0.5) (mid-tread),
+     * |ev| = |(double)val - input| <= 1.5 + Dm, Dm the largest |rnd * dth_mul| of the render type
+     * (sound_render.c:711-751: RPDF |dsopen| / SQRT2 < 0.708, TPDF and STPDF < 1, GAUSS 12 / (2 SQRT6)
+     * < 2.45), so a FIR shaper's output |prev_ns_err| <= B (1.5 + Dm), B = sum |c_i|.  A block whose
+     * inputs all have |x * norm_mul| <= spec_thr, after a block without a clip (so the shaper history
+     * holds only such errors), then has |q| <= spec_thr + B (1.5 + Dm) + Dm + 0.5 < clip_abs for every
+     * sample: nothing clips and the clamp is the identity, so the block runs without it.  The IIR
+     * shaper feeds back its own output: never. */
+    k.spec_thr = -1.0;
+    static const bool spec = !getenv("ICW_K3R_SPEC") || atoi(getenv("ICW_K3R_SPEC")) != 0;
+    if (spec && k.ns_kind != 2 && cfg.render_type <= ICW_RENDER_GAUSS) {
+        static const double cdm[5] = {0.0, 0.708, 1.0, 1.0, 2.45};
+        double B = 0.0;
+        if (k.ns_kind == 1)
+            for (int i = 0; i < k.ns_n; ++i) B += fabs(k.ns_c[i]);
+        const double Dm = cfg.render_type == ICW_RENDER_ROUND ? 0.0 : fabs(k.dth_mul) * cdm[cfg.render_type];
+        const double thr = k.clip_abs - B * (1.5 + Dm) * 1.001 - Dm - 0.5 - 1.0;
+        if (thr > 0.0) k.spec_thr = thr;             /* NaN / inf dth_mul: never */
+    }
 }
 
 /* The normalised list (graph_accept) as the device program: register form, or the bus form when a
@@ -663,17 +683,21 @@ std::vector<std::pair<int, int>> plan_blocks(int n_frames, int Tb, int first, do
     return bl;
 }
 
-/* page-locked host memory (hipHostMalloc / hipHostRegister): the DMA engines read it directly, so
- * an asynchronous copy does not block the host thread.  A pageable pointer makes the query fail;
- * the error is cleared so that it does not surface as the call's own. */
-bool host_pinned(const void *p)
+/* page-locked host memory (hipHostMalloc / hipHostRegister) that device `dev` may copy from: the DMA
+ * engines read it directly, so an asynchronous copy does not block the host thread.  Memory pinned
+ * while another device was current counts only if it was pinned portable (hipHostMallocPortable /
+ * hipHostRegisterPortable, as icw_host_alloc does): the shards of icw_group_process hand slices of one
+ * caller buffer to contexts on different devices.  Anything else takes the whole-call staging copies.
+ * A pageable pointer makes the query fail; the error is cleared so that it does not surface as the
+ * call's own. */
+bool host_pinned(const void *p, int dev)
 {
     hipPointerAttribute_t a;
     if (hipPointerGetAttributes(&a, p) != hipSuccess) {
         (void)hipGetLastError();
         return false;
     }
-    return a.type == hipMemoryTypeHost;
+    return a.type == hipMemoryTypeHost && (a.device == dev || (a.allocationFlags & hipHostMallocPortable));
 }
 
 /* wait for a K5 call's sequence number in host memory; the stream is queried now and then, so a
@@ -892,9 +916,10 @@ int plug_slot(const icw_node &n)
 }
 
 /* A live list edit (the caller holds c->mu and has waited for the context's work): compile the
- * normalised list nv, zero the bus slots the reference's edit clears, then install the program.
- * The slots are cleared before the program goes to the device, so an error leaves the old program
- * on both sides. */
+ * normalised list nv, install the program, then zero the bus slots the reference's edit clears.  The
+ * program goes to the device first, so a failed copy leaves the old program and the old bus on both
+ * sides; a failed clear after it returns ICW_EDEVICE with the new program in place (the context is
+ * quiesced, so the order of the two steps changes no output). */
 int apply_graph(icw_ctx *c, std::vector<icw_node> &nv, int bypass, const std::vector<int> &clears)
 {
     icw_config cfg = c->cfg;
@@ -905,13 +930,13 @@ int apply_graph(icw_ctx *c, std::vector<icw_node> &nv, int bypass, const std::ve
     if (!c->chain_ok) P.chain = P.sig = 0;
     const bool serial = needs_serial(cfg, c->rk, P);
     if (serial && (rc = ensure_render_state(c))) return rc;
-    for (int slot : clears)
-        if (clear_slot(c, slot) != ICW_OK) return ICW_EDEVICE;
     if (hipMemcpy(c->d_prog, &P, sizeof(IcwProg), hipMemcpyHostToDevice) != hipSuccess) return ICW_EDEVICE;
     c->cfg.bypass_list = cfg.bypass_list;
     c->nodes = nv;
     c->prog = P;
     c->serial_render = serial;
+    for (int slot : clears)
+        if (clear_slot(c, slot) != ICW_OK) return ICW_EDEVICE;
     return ICW_OK;
 }
 
@@ -1548,7 +1573,7 @@ int icw_process_streams(icw_ctx *c, int first, int count, const void *in, size_t
     const bool pinned = !dev && stage_in + stage_out + 16 <= kPinnedStage;
     /* pinned host buffers on a call of several launch blocks: each block's input slice goes in and
      * its output slice comes out on the copy stream, beside the other blocks' kernels */
-    const bool pipe_io = !dev && !pinned && n_blocks > 1 && !c->serialize && host_pinned(in) && host_pinned(out);
+    const bool pipe_io = !dev && !pinned && n_blocks > 1 && !c->serialize && host_pinned(in, c->device) && host_pinned(out, c->device);
     bool zcopy = false;
     if (pinned) {
         if (c->h_stage_bytes < stage_in + stage_out + 16) {
@@ -2209,7 +2234,9 @@ int icw_host_alloc(size_t bytes, void **p)
 {
     if (!p || !bytes) return ICW_EINVAL;
     *p = nullptr;
-    return hipHostMalloc(p, bytes, hipHostMallocDefault) == hipSuccess ? ICW_OK : ICW_ENOMEM;
+    /* portable: pinned for every device, so an icw_group's shards on other devices pipeline their
+     * slices of the same buffer too (host_pinned) */
+    return hipHostMalloc(p, bytes, hipHostMallocPortable) == hipSuccess ? ICW_OK : ICW_ENOMEM;
 }
 
 int icw_host_free(void *p)

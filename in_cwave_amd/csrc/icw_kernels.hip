@@ -1231,7 +1231,7 @@ __device__ __forceinline__ void icw_fast_render(const IcwRenderK &rk, const doub
         for (int c = 0; c < 2; ++c) {
             if constexpr (MR) {
                 q[r][c] = x[r][c];
-                del[r][c] = x[r][c] < 0.0 ? -1 : 0;
+                del[r][c] = x[r][c] < 0.0 ? rk.sign_delta : 0;   /* -1 (icw_launch_fir_graph checks) */
             } else {
                 q[r][c] = __builtin_copysign(fabs(x[r][c]) + rk.round_offset, x[r][c]);
                 del[r][c] = 0;
@@ -2880,17 +2880,23 @@ struct IcwRowNs {
  * beside the clamp.  Mid-tread (round_offset 0.5, sign_delta 0): q +- 0.5 by the sign of q, both
  * sums formed beside the compare, delta 0.
  * The FIR shaper's first term 0.0 + c0 * ev (ns_fir, sound_render.c:420-427: the sum starts at 0.0)
- * is one fma(c0, ev, +0.0): the exact product plus +0.0, rounded once, is round(c0 * ev) with a
- * zero's sign made +, exactly what 0.0 + round(c0 * ev) gives.  On the chain per sample: the input
- * and q, clamp (2), trunc, + delta, ev, the fma and the shaper's DPP sum -- 16 ops for MEW44 where
- * the integer round trip and the rounding's compare / select / add made it 23. */
-template <int KIND, int NN, int R, int J, bool MR>
-__device__ __forceinline__ void icw_rrow_step(double x, double d, double &prev_err, double (&E)[R], double (&O)[R],
+ * is one fma(c0, ev, +0.0): the exact product plus +0.0, rounded once, is round(c0 * ev) with an
+ * exact zero's sign made +, what 0.0 + round(c0 * ev) gives -- except where c0 * ev is nonzero but
+ * rounds to zero (|ev| below ~2^-1022 / |c0|: a subnormal input with vd = 0): the fma then gives the
+ * product's sign, -0.0 for a negative one, where the reference's 0.0 + (-0.0) is +0.0.  Only the sign
+ * of a zero differs, in res (prev_ns_err), and nothing downstream can see it: input = xs - res, then
+ * q = input + d, differ at most in a zero's sign, which trunc + delta, the clip stage and the peak
+ * (fabs) all map alike, so ev, the integer and the meters are the reference's (the saved prev_ns_err
+ * of the state blob may hold -0.0 for its +0.0).  On the chain per sample: the input and q, clamp
+ * (2), trunc, + delta, ev, the fma and the shaper's DPP sum -- 16 ops for MEW44 where the integer
+ * round trip and the rounding's compare / select / add made it 23 (14 in a clamp-free block). */
+template <int KIND, int NN, int R, int J, bool MR, bool FAST>
+__device__ __forceinline__ void icw_rrow_step(double xs, double d, double &prev_err, double (&E)[R], double (&O)[R],
                                               double (&P)[R], double (&P2)[R], const IcwRowNs &c,
                                               const IcwRenderK &k, double *qst)
 {
     constexpr int S = J % R;
-    const double input = (x * k.norm_mul) - prev_err;
+    const double input = xs - prev_err;                /* xs = x * norm_mul, formed in the staging */
     double q = input + d;
     double dd;                                         /* (double)delta */
     if constexpr (MR) {
@@ -2900,8 +2906,12 @@ __device__ __forceinline__ void icw_rrow_step(double x, double d, double &prev_e
         q = q < 0.0 ? qb : qa;
         dd = 0.0;
     }
-    /* the clip stage as it reaches the integer (icw_clamp_int); clips and peak from the staged q */
-    const double vd = __builtin_trunc(fmax(fmin(q, k.hi - 1.0), k.lo + 1.0)) + dd;
+    /* the clip stage as it reaches the integer (icw_clamp_int); clips and peak from the staged q.  A
+     * clamp-free block (FAST, icw_render_row) has lo < q < hi for every sample, where the reference's
+     * clip stage changes nothing and trunc(q) is already in [lo + 1, hi - 1] */
+    double vd;
+    if constexpr (FAST) vd = __builtin_trunc(q) + dd;
+    else vd = __builtin_trunc(fmax(fmin(q, k.hi - 1.0), k.lo + 1.0)) + dd;
     qst[J * 16] = q;                                   /* the integer is the flush's, from q */
     const double ev = vd - input;
     double res = 0.0;
@@ -2928,17 +2938,17 @@ __device__ __forceinline__ void icw_rrow_step(double x, double d, double &prev_e
 /* look-ahead reads: the next block's inputs and dither values of the row's channel, staged in LDS
  * (icw_rrow_stage_*): sample J of this block reads sample J of the next -- a whole block ahead of
  * its use, at an immediate offset (no address arithmetic per sample, no wait on global memory) */
-template <int KIND, int NN, int R, int J, bool MR>
+template <int KIND, int NN, int R, int J, bool MR, bool FAST>
 __device__ __forceinline__ void icw_rrow_block(double (&xin)[ICW_MAX_NS_TAPS], double (&dv)[ICW_MAX_NS_TAPS],
                                                double &prev_err, double (&E)[R], double (&O)[R], double (&P)[R],
                                                double (&P2)[R], const IcwRowNs &c, const IcwRenderK &k, double *qst,
                                                const double *xn, const double *dn)
 {
     if constexpr (J < ICW_MAX_NS_TAPS) {
-        icw_rrow_step<KIND, NN, R, J, MR>(xin[J], dv[J], prev_err, E, O, P, P2, c, k, qst);
+        icw_rrow_step<KIND, NN, R, J, MR, FAST>(xin[J], dv[J], prev_err, E, O, P, P2, c, k, qst);
         xin[J] = xn[J];
         dv[J] = dn[J];
-        icw_rrow_block<KIND, NN, R, J + 1, MR>(xin, dv, prev_err, E, O, P, P2, c, k, qst, xn, dn);
+        icw_rrow_block<KIND, NN, R, J + 1, MR, FAST>(xin, dv, prev_err, E, O, P, P2, c, k, qst, xn, dn);
     }
 }
 
@@ -2950,7 +2960,7 @@ __device__ __forceinline__ void icw_rrow_block_lim(const double (&xin)[ICW_MAX_N
 {
     if constexpr (J < ICW_MAX_NS_TAPS) {
         if (J < lim) {
-            icw_rrow_step<KIND, NN, R, J, MR>(xin[J], dv[J], prev_err, E, O, P, P2, c, k, qst);
+            icw_rrow_step<KIND, NN, R, J, MR, false>(xin[J], dv[J], prev_err, E, O, P, P2, c, k, qst);
             icw_rrow_block_lim<KIND, NN, R, J + 1, MR>(xin, dv, prev_err, E, O, P, P2, c, k, qst, lim);
         }
     }
@@ -2968,6 +2978,9 @@ struct IcwRowStage {
 
 __device__ __forceinline__ void icw_rrow_stage_load(const IcwK3Args &a, int t0, int lane, IcwRowStage &st)
 {
+#ifdef ICW_K3R_NOLOAD
+    if (t0 >= 3 * ICW_MAX_NS_TAPS) return;          /* diagnostic build (timing only): no staging loads */
+#endif
     constexpr int U = ICW_MAX_NS_TAPS;
     const int sb = lane >> 5, i = lane & 31;
     const int s = blockIdx.x * 2 + sb;
@@ -2980,14 +2993,24 @@ __device__ __forceinline__ void icw_rrow_stage_load(const IcwK3Args &a, int t0, 
         st.d = *(const double2 *)(a.dith + (size_t)(t0 + tt) * a.dith_pitch + blockIdx.x * 4 + 2 * h);
 }
 
-__device__ __forceinline__ void icw_rrow_stage_store(double (*xs)[ICW_MAX_NS_TAPS], double (*ds)[ICW_MAX_NS_TAPS],
-                                                     int lane, const IcwRowStage &st)
+/* The inputs go to LDS as x * norm_mul (sound_render.c:754's product, formed here lane-parallel: two
+ * multiplies per block instead of one per sample on the chain).  Returns, wave-uniform, whether every
+ * staged |x * norm_mul| <= thr (render_consts' spec_thr; NaN fails): the block may run clamp-free. */
+__device__ __forceinline__ bool icw_rrow_stage_store(double (*xs)[ICW_MAX_NS_TAPS], double (*ds)[ICW_MAX_NS_TAPS],
+                                                     int lane, const IcwRowStage &st, double nm, double thr)
 {
     constexpr int U = ICW_MAX_NS_TAPS;
     const int sb = lane >> 5, i = lane & 31;
-    if (i < U) { xs[2 * sb][i] = st.x.x; xs[2 * sb + 1][i] = st.x.y; }
+    bool ok = true;
+    if (i < U) {
+        const double a = st.x.x * nm, b = st.x.y * nm;
+        xs[2 * sb][i] = a;
+        xs[2 * sb + 1][i] = b;
+        ok = fabs(a) <= thr && fabs(b) <= thr;
+    }
     const int tt = lane >> 1, h = lane & 1;
     if (lane < 2 * U) { ds[2 * h][tt] = st.d.x; ds[2 * h + 1][tt] = st.d.y; }
+    return __all(ok);
 }
 
 /* End of a block of nf samples: clips and peak of the staged q (lane l: samples l, l + 16 of its
@@ -3002,12 +3025,15 @@ __device__ __forceinline__ int icw_rrow_val(double q, int lo1, int hi1)
     return q != q ? (int)0x80000000 : v;
 }
 
+/* (the exact form; returns, wave-uniform, whether every q of the block had |q| < clip_abs -- no clip,
+ * so the next block may run clamp-free) */
 template <bool MR>
-__device__ __forceinline__ void icw_rrow_flush(const double (*qs)[ICW_MAX_NS_TAPS][16], int r, int lr, int lane,
+__device__ __forceinline__ bool icw_rrow_flush(const double (*qs)[ICW_MAX_NS_TAPS][16], int r, int lr, int lane,
                                                int nf, const IcwRenderK &k, unsigned &clips, double &pk,
                                                unsigned char *o0, unsigned char *o1, int osz)
 {
     __builtin_amdgcn_wave_barrier();
+    bool calm = true;
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
         const int j = lr + 16 * h;
@@ -3015,8 +3041,10 @@ __device__ __forceinline__ void icw_rrow_flush(const double (*qs)[ICW_MAX_NS_TAP
             const double q = qs[r][j][lr];
             clips += (q >= k.hi ? 1u : 0u) + (q <= k.lo ? 1u : 0u);
             pk = fmax(pk, fabs(q));
+            calm &= fabs(q) < k.clip_abs;
         }
     }
+    calm = __all(calm);
     const int sb = lane >> 5, f = lane & 31;
     unsigned char *o = sb ? o1 : o0;
     if (o && f < nf) {
@@ -3025,6 +3053,41 @@ __device__ __forceinline__ void icw_rrow_flush(const double (*qs)[ICW_MAX_NS_TAP
         const int vr = icw_rrow_val<MR>(qs[2 * sb + 1][f][0], lo1, hi1);
         const uint32_t l = (uint32_t)(vl << k.norm_shift);
         const uint32_t rr = (uint32_t)(vr << k.norm_shift);
+        if (osz == 2) {
+            *(uint32_t *)(o + (size_t)f * 4) = (l & 0xffffu) | (rr << 16);
+        } else {
+            uint16_t *p = (uint16_t *)(o + (size_t)f * 6);
+            p[0] = (uint16_t)(l & 0xffffu);
+            p[1] = (uint16_t)(((l >> 16) & 0xffu) | ((rr & 0xffu) << 8));
+            p[2] = (uint16_t)((rr >> 8) & 0xffffu);
+        }
+    }
+    __builtin_amdgcn_wave_barrier();
+    return calm;
+}
+
+/* the flush of a clamp-free block: every |q| < clip_abs, finite -- no clip to count, the integer is the
+ * plain conversion (exact below 2^31) + the mid-riser's delta, no clamp, no NaN */
+template <bool MR>
+__device__ __forceinline__ void icw_rrow_flush_fast(const double (*qs)[ICW_MAX_NS_TAPS][16], int r, int lr, int lane,
+                                                    const IcwRenderK &k, double &pk, unsigned char *o0,
+                                                    unsigned char *o1, int osz)
+{
+    constexpr int U = ICW_MAX_NS_TAPS;
+    __builtin_amdgcn_wave_barrier();
+    /* the four reads first, unconditionally (clamped indices; a lane's second peak sample repeats its
+     * first where lr + 16 >= U, which changes no maximum), so they share one wait */
+    const int f = lane & 31, sb = lane >> 5, fc = f < U ? f : U - 1;
+    const double q0 = qs[r][lr][lr];
+    const double q1 = qs[r][lr + 16 < U ? lr + 16 : lr][lr];
+    const double ql = qs[2 * sb][fc][0], qr = qs[2 * sb + 1][fc][0];
+    pk = icw_vmax_abs(icw_vmax_abs(pk, q0), q1);
+    const int vl = icw_cvt_sat_i32(ql) + (MR && ql < 0.0 ? -1 : 0);
+    const int vr = icw_cvt_sat_i32(qr) + (MR && qr < 0.0 ? -1 : 0);
+    const uint32_t l = (uint32_t)(vl << k.norm_shift);
+    const uint32_t rr = (uint32_t)(vr << k.norm_shift);
+    unsigned char *o = sb ? o1 : o0;
+    if (o && f < U) {
         if (osz == 2) {
             *(uint32_t *)(o + (size_t)f * 4) = (l & 0xffffu) | (rr << 16);
         } else {
@@ -3092,11 +3155,12 @@ __global__ __launch_bounds__(64) void icw_render_row(IcwK3Args a)
     /* block j's inputs in LDS buffer j & 1: loaded at the end of block j - 3, stored at the end of
      * block j - 2, read (a block ahead) during block j - 1 */
     __shared__ double xsl[2][4][U], dsl[2][4][U];
+    const double nm = k.norm_mul, thr = k.spec_thr;
     IcwRowStage stg;
     icw_rrow_stage_load(a, 0, lane, stg);
-    icw_rrow_stage_store(xsl[0], dsl[0], lane, stg);
+    bool x_ok0 = icw_rrow_stage_store(xsl[0], dsl[0], lane, stg, nm, thr);
     icw_rrow_stage_load(a, U, lane, stg);
-    icw_rrow_stage_store(xsl[1], dsl[1], lane, stg);
+    bool x_ok1 = icw_rrow_stage_store(xsl[1], dsl[1], lane, stg, nm, thr);
     icw_rrow_stage_load(a, 2 * U, lane, stg);
     __builtin_amdgcn_wave_barrier();
     double xin[U], dv[U];
@@ -3105,16 +3169,46 @@ __global__ __launch_bounds__(64) void icw_render_row(IcwK3Args a)
         xin[j] = xsl[0][r][j];
         dv[j] = dsl[0][r][j];
     }
+    /* Clamp-free blocks (render_consts: spec_thr).  A block runs without the clip stage when the block
+     * before it clipped nowhere (every |q| < clip_abs: `calm`) and its own inputs are all within
+     * spec_thr; it then clips nowhere itself, so the next block's history is calm too.  The first block
+     * of a launch starts from a saved history and takes the exact form.  Wave-uniform (__all).
+     * The two forms run in loops of their own, each with its own back edge: with one loop and the form
+     * chosen per block, the register allocation of the two unrolled bodies met at the loop's end, and
+     * every block paid ~80 AGPR / VGPR moves for it (more than the clamp it saved). */
+    bool calm = false;
     int t = 0, kb = 0;
-    for (; t + U <= T; t += U, ++kb) {
+    /* one block of either form, the staging of block kb + 2 (into the buffer block kb has left), the
+     * block's flush, and block kb + 3 on its way.  The staging comes before the flush: its stores to
+     * LDS wait for the registers loaded one block ago, and on gfx950 that wait (vmcnt) also counts
+     * the global stores issued before it -- after the flush it waited for the block's own output
+     * stores to complete. */
+    auto step = [&](auto fast) {
+        constexpr bool FAST = decltype(fast)::value;
         const int nb = (kb + 1) & 1;
-        icw_rrow_block<KIND, NN, R, 0, MR>(xin, dv, prev_err, E, O, P, P2, c, k, qst, &xsl[nb][r][0], &dsl[nb][r][0]);
-        icw_rrow_flush<MR>(qs, r, lr, lane, U, k, clips, pk, oA ? oA + (size_t)t * 2 * osz : nullptr,
-                           oB ? oB + (size_t)t * 2 * osz : nullptr, osz);
-        /* block kb + 2 into the buffer block kb has left, block kb + 3 on its way */
-        icw_rrow_stage_store(xsl[kb & 1], dsl[kb & 1], lane, stg);
+        unsigned char *ot0 = oA ? oA + (size_t)t * 2 * osz : nullptr, *ot1 = oB ? oB + (size_t)t * 2 * osz : nullptr;
+        icw_rrow_block<KIND, NN, R, 0, MR, FAST>(xin, dv, prev_err, E, O, P, P2, c, k, qst, &xsl[nb][r][0],
+                                                 &dsl[nb][r][0]);
+        x_ok0 = x_ok1;
+        x_ok1 = icw_rrow_stage_store(xsl[kb & 1], dsl[kb & 1], lane, stg, nm, thr);
+        if constexpr (FAST) {
+            icw_rrow_flush_fast<MR>(qs, r, lr, lane, k, pk, ot0, ot1, osz);
+#ifdef ICW_K3R_COUNT
+            if (lr == 0 && valid) atomicAdd(&a.clips[g], 1u);   /* diagnostic build: clamp-free blocks */
+#endif
+        } else {
+            calm = icw_rrow_flush<MR>(qs, r, lr, lane, U, k, clips, pk, ot0, ot1, osz);
+        }
         icw_rrow_stage_load(a, t + 3 * U, lane, stg);
         __builtin_amdgcn_wave_barrier();
+        t += U;
+        ++kb;
+    };
+    while (t + U <= T) {
+        while (t + U <= T && !(KIND != 2 && calm && x_ok0)) step(icw_ic<0>());
+        if constexpr (KIND != 2) {
+            while (t + U <= T && x_ok0) step(icw_ic<1>());
+        }
     }
     const int rem = T - t;
     if (rem > 0) {
@@ -3283,6 +3377,10 @@ static hipError_t launch_fir_graph_nc(const IcwFirArgs *f, const IcwK2Args *a, i
 extern "C" hipError_t icw_launch_fir_graph(const IcwFirArgs *f, const IcwK2Args *a, int in_step, hipStream_t st)
 {
     if (!fir_ok(f->M, f->nt)) return hipErrorInvalidValue;
+    /* the render-only form (icw_fast_render) takes the quantiser from sign_delta alone: mid-riser
+     * (sign_delta -1, round_offset 0) or mid-tread (0, 0.5), the only pairs render_consts gives */
+    if (a->rk.sign_delta != 0 ? (a->rk.sign_delta != -1 || a->rk.round_offset != 0.0) : a->rk.round_offset != 0.5)
+        return hipErrorInvalidValue;
     const size_t lds = icw_fir_graph_lds(f->M, f->nt, f->nch, a->n_regs);
     if (!lds) return hipErrorInvalidValue;
     if (in_step && !(a->trig && a->trig_tab)) return hipErrorInvalidValue;

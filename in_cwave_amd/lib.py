@@ -452,10 +452,14 @@ class Group:
                "icw_group_shard")
         return f.value, c.value, dev.value
 
-    def process(self, inp, n_frames, want_pre=False):
+    def process(self, inp, n_frames, want_pre=False, out=None):
+        """out: an optional [n_streams, >= n_frames * osz] uint8 array (e.g. host_array: pinned, so every
+        shard copies its slices block by block on its own device)"""
         inp = np.ascontiguousarray(inp)
         assert inp.dtype == np.uint8 and inp.shape[0] == self.n_streams and inp.shape[1] >= n_frames * self.fsz
-        out = np.zeros((self.n_streams, n_frames * self.osz), dtype=np.uint8)
+        if out is None:
+            out = np.zeros((self.n_streams, n_frames * self.osz), dtype=np.uint8)
+        assert out.dtype == np.uint8 and out.shape[0] == self.n_streams and out.shape[1] >= n_frames * self.osz
         pre = np.zeros((self.n_streams, n_frames, 2), dtype=np.float64) if want_pre else None
         _check(self._lib.icw_group_process(self.h, _ptr(inp), inp.strides[0], _ptr(out), out.strides[0], n_frames,
                                            abi.F_DEBUG_PRE if want_pre else 0, _ptr(pre)), "icw_group_process")

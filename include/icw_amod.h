@@ -81,7 +81,12 @@ int icw_amod_get_clips_peaks(icw_mod_context *const *mcs, int n, unsigned *lc, u
 /* The DSP-list primitives over the decoding contexts: the reference's list is one (am.head, shared
  * by both contexts, adv_modulator.c:51-52), and replace_output_plug clears the removed / re-plugged
  * node's old slot in every context (mod_context_clear_all_inouts, in_cwave.c:255-261).  Each applies
- * the icw.h primitive of the same name to every non-NULL context; the first error is returned.
+ * the icw.h primitive of the same name to the non-NULL contexts in order and stops at the first error,
+ * which it returns.  The contexts hold the same list, so a refused edit (ICW_EGRAPH: amod_init's rules,
+ * a Master added) is refused by the first context before any changed.  A device error (ICW_EDEVICE /
+ * ICW_ENOMEM) after an earlier context took the edit leaves the contexts with different lists: the
+ * host re-sends the whole list to each with icw_set_graph (which matches it by position) before the
+ * next block.
  *   icw_amod_del_lastdsp      <- amod_del_lastdsp       (adv_modulator.c:378-390)
  *   icw_amod_del_dsplist      <- amod_del_dsplist       (adv_modulator.c:360-374)
  *   icw_amod_add_lastdsp      <- amod_add_lastdsp + the GUI's field writes (adv_modulator.c:394-411)

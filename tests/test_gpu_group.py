@@ -45,6 +45,32 @@ def test_group_equals_one_context_and_oracle(oracle, icw, shape):
     ctx.close()
 
 
+def test_group_pinned_host_buffers(oracle, icw):
+    """one caller buffer pair in pinned memory (icw_host_alloc: portable, so pinned for every device),
+    sliced over the shards: each shard takes the per-block copy pipeline (several launch blocks per
+    call) on its own device, and the bytes equal one context over all streams and the oracle.  On this
+    box every shard is device 0; on an 8-GPU node the same slices go to devices 0..7 (host_pinned
+    accepts them there because the block is portable)."""
+    fs = 48000
+    cfg = graph.default_config(fs)
+    nodes = graph.graph_shift_master()
+    S, n = 5, 40000                                   # 40 000 frames: three launch blocks per call
+    raw = synth.batch_pcm(S, n, fs, first=31)
+    inp = L.host_array(raw.shape)
+    inp[:] = raw
+    out = L.host_array((S, n * 4))
+    grp = L.Group(cfg, nodes, S, [0, 0])
+    grp.process(inp, n, out=out)
+    ctx = icw.Context(cfg, nodes, S)
+    out1, _ = ctx.process(raw, n)
+    assert np.array_equal(np.asarray(out), out1)
+    for s in range(S):
+        ro, _ = oracle.Stream(cfg, nodes).process(raw[s], n)
+        assert np.array_equal(np.asarray(out)[s], ro), s
+    grp.close()
+    ctx.close()
+
+
 def test_transcode_files_devices_byte_identical(tmp_path):
     """the many-file transcoder split over two 'devices' (both device 0) writes the same files as
     one device"""

@@ -1,0 +1,14 @@
+#!/bin/bash
+mkdir -p gpurun_out; export TMPDIR=/tmp; R=$(pwd)
+timeout -k 10 600 python -u -m pytest tests/test_gpu_render_spec.py tests/test_gpu_parity.py -x -q --timeout 200 --timeout-method thread > gpurun_out/r5k3rd_tests.txt 2>&1
+rc=$?; echo "[tests] rc=$rc"; tail -2 gpurun_out/r5k3rd_tests.txt; [ $rc -eq 0 ] || exit 2
+for L in libicw.so libicw_noload.so libicw_prev.so; do
+  ( cd /tmp && ICW_LIB=$L timeout -s KILL 150 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/gpurun_out/r5k3rd_trace_${L%.so}" -o run \
+      -- python3 "$R/bench.py" --workload c5fir --steps 2 --warmup 1 --no-cpu-baseline --e2e-steps 0 ) > gpurun_out/r5k3rd_trace_${L%.so}.txt 2>&1 || { echo "trace $L failed"; exit 4; }
+  python3 -c "
+import csv,sys
+for r in csv.DictReader(open('gpurun_out/r5k3rd_trace_${L%.so}/run_kernel_stats.csv')):
+    if 'render_row' in r['Name']: print('$L', r['Name'][:40], r['AverageNs'])"
+done
+TAG=r5k3rd LIBS="libicw.so libicw_noload.so" bash tools/r5_k3r_wait.sh || exit 5
+echo all-ok
