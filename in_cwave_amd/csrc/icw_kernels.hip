@@ -1496,18 +1496,25 @@ __device__ __forceinline__ void icw_chain_frames_rowp(const IcwK2Args &a, icw_cp
     icw_chain_frames<TRIG, R, true>(a, P, s, t0, nv, in, clip_l, clip_r, pk_l, pk_r, dv, tro_lane, tro_u, tro_step);
 }
 
+/* the device library's wave reduction of doubles (declared by HIP only with its extra warp-sync types) */
+extern "C" __device__ __attribute__((const)) double __ockl_wfred_max_f64(double);
+
 /* per-workgroup meters (ICW_K2_TILE threads): wave reduce, LDS, one atomic per stream/channel */
 __device__ __forceinline__ void icw_meters_wg(const IcwK2Args &a, int s, unsigned clip_l, unsigned clip_r, double pk_l,
                                               double pk_r, unsigned (*red_clip)[ICW_K2_TILE / 64],
                                               double (*red_pk)[ICW_K2_TILE / 64])
 {
     const int tl = threadIdx.x;
-    for (int off = 32; off > 0; off >>= 1) {
-        clip_l += __shfl_xor(clip_l, off);
-        clip_r += __shfl_xor(clip_r, off);
-        pk_l = fmax(pk_l, __shfl_xor(pk_l, off));
-        pk_r = fmax(pk_r, __shfl_xor(pk_r, off));
+    /* wave reductions by DPP (the device library's wfred): six dependent __shfl_xor rounds each were
+     * an LDS permute and its wait -- 36 LDS instructions per wave in the fused converter's graph phase.
+     * Sums of the clip counts and maxima of the peaks are exact in any order; the counts are reduced
+     * only when a lane of the wave clipped (a ballot), the usual case being none. */
+    if (__any((clip_l | clip_r) != 0u)) {
+        clip_l = __ockl_wfred_add_u32(clip_l);
+        clip_r = __ockl_wfred_add_u32(clip_r);
     }
+    pk_l = __ockl_wfred_max_f64(pk_l);
+    pk_r = __ockl_wfred_max_f64(pk_r);
     const int wv = tl >> 6;
     if ((tl & 63) == 0) {
         red_clip[0][wv] = clip_l; red_clip[1][wv] = clip_r;
@@ -2890,10 +2897,12 @@ struct IcwRowNs {
  * of the state blob may hold -0.0 for its +0.0).  On the chain per sample: the input and q, clamp
  * (2), trunc, + delta, ev, the fma and the shaper's DPP sum -- 16 ops for MEW44 where the integer
  * round trip and the rounding's compare / select / add made it 23 (14 in a clamp-free block). */
+/* qst: the lane's slot for sample 0 in the q stage qs[row][U / 2][16][2] -- samples 2i and 2i + 1 of a
+ * lane side by side, written together by one ds_write_b128 at the odd sample (qh holds the even one) */
 template <int KIND, int NN, int R, int J, bool MR, bool FAST>
 __device__ __forceinline__ void icw_rrow_step(double xs, double d, double &prev_err, double (&E)[R], double (&O)[R],
                                               double (&P)[R], double (&P2)[R], const IcwRowNs &c,
-                                              const IcwRenderK &k, double *qst)
+                                              const IcwRenderK &k, double *qst, double &qh)
 {
     constexpr int S = J % R;
     const double input = xs - prev_err;                /* xs = x * norm_mul, formed in the staging */
@@ -2912,7 +2921,8 @@ __device__ __forceinline__ void icw_rrow_step(double xs, double d, double &prev_
     double vd;
     if constexpr (FAST) vd = __builtin_trunc(q) + dd;
     else vd = __builtin_trunc(fmax(fmin(q, k.hi - 1.0), k.lo + 1.0)) + dd;
-    qst[J * 16] = q;                                   /* the integer is the flush's, from q */
+    if constexpr (J & 1) *(double2 *)(qst + (J >> 1) * 32) = make_double2(qh, q);   /* the integer is the flush's */
+    else qh = q;
     const double ev = vd - input;
     double res = 0.0;
     /* the new products go out before this sample's sum, whose volatile fmac block then separates
@@ -2945,10 +2955,17 @@ __device__ __forceinline__ void icw_rrow_block(double (&xin)[ICW_MAX_NS_TAPS], d
                                                const double *xn, const double *dn)
 {
     if constexpr (J < ICW_MAX_NS_TAPS) {
-        icw_rrow_step<KIND, NN, R, J, MR, FAST>(xin[J], dv[J], prev_err, E, O, P, P2, c, k, qst);
-        xin[J] = xn[J];
-        dv[J] = dn[J];
-        icw_rrow_block<KIND, NN, R, J + 1, MR, FAST>(xin, dv, prev_err, E, O, P, P2, c, k, qst, xn, dn);
+        /* the next block's samples J, J + 1 by one ds_read_b128 each for x and d (16-byte aligned rows) */
+        double qh;
+        icw_rrow_step<KIND, NN, R, J, MR, FAST>(xin[J], dv[J], prev_err, E, O, P, P2, c, k, qst, qh);
+        icw_rrow_step<KIND, NN, R, J + 1, MR, FAST>(xin[J + 1], dv[J + 1], prev_err, E, O, P, P2, c, k, qst, qh);
+        /* after both steps, so the 16 bytes land in the pair's own registers (no moves) */
+        const double2 x2 = *(const double2 *)(xn + J), d2 = *(const double2 *)(dn + J);
+        xin[J] = x2.x;
+        xin[J + 1] = x2.y;
+        dv[J] = d2.x;
+        dv[J + 1] = d2.y;
+        icw_rrow_block<KIND, NN, R, J + 2, MR, FAST>(xin, dv, prev_err, E, O, P, P2, c, k, qst, xn, dn);
     }
 }
 
@@ -2960,8 +2977,14 @@ __device__ __forceinline__ void icw_rrow_block_lim(const double (&xin)[ICW_MAX_N
 {
     if constexpr (J < ICW_MAX_NS_TAPS) {
         if (J < lim) {
-            icw_rrow_step<KIND, NN, R, J, MR, false>(xin[J], dv[J], prev_err, E, O, P, P2, c, k, qst);
-            icw_rrow_block_lim<KIND, NN, R, J + 1, MR>(xin, dv, prev_err, E, O, P, P2, c, k, qst, lim);
+            double qh;
+            icw_rrow_step<KIND, NN, R, J, MR, false>(xin[J], dv[J], prev_err, E, O, P, P2, c, k, qst, qh);
+            if (J + 1 < lim) {
+                icw_rrow_step<KIND, NN, R, J + 1, MR, false>(xin[J + 1], dv[J + 1], prev_err, E, O, P, P2, c, k, qst, qh);
+                icw_rrow_block_lim<KIND, NN, R, J + 2, MR>(xin, dv, prev_err, E, O, P, P2, c, k, qst, lim);
+            } else {
+                qst[(J >> 1) * 32] = qh;                 /* the last sample, an even one, alone */
+            }
         }
     }
 }
@@ -3028,7 +3051,7 @@ __device__ __forceinline__ int icw_rrow_val(double q, int lo1, int hi1)
 /* (the exact form; returns, wave-uniform, whether every q of the block had |q| < clip_abs -- no clip,
  * so the next block may run clamp-free) */
 template <bool MR>
-__device__ __forceinline__ bool icw_rrow_flush(const double (*qs)[ICW_MAX_NS_TAPS][16], int r, int lr, int lane,
+__device__ __forceinline__ bool icw_rrow_flush(const double (*qs)[ICW_MAX_NS_TAPS / 2][16][2], int r, int lr, int lane,
                                                int nf, const IcwRenderK &k, unsigned &clips, double &pk,
                                                unsigned char *o0, unsigned char *o1, int osz)
 {
@@ -3038,7 +3061,7 @@ __device__ __forceinline__ bool icw_rrow_flush(const double (*qs)[ICW_MAX_NS_TAP
     for (int h = 0; h < 2; ++h) {
         const int j = lr + 16 * h;
         if (j < nf) {
-            const double q = qs[r][j][lr];
+            const double q = qs[r][j >> 1][lr][j & 1];
             clips += (q >= k.hi ? 1u : 0u) + (q <= k.lo ? 1u : 0u);
             pk = fmax(pk, fabs(q));
             calm &= fabs(q) < k.clip_abs;
@@ -3049,8 +3072,8 @@ __device__ __forceinline__ bool icw_rrow_flush(const double (*qs)[ICW_MAX_NS_TAP
     unsigned char *o = sb ? o1 : o0;
     if (o && f < nf) {
         const int lo1 = k.lo1, hi1 = k.hi1;
-        const int vl = icw_rrow_val<MR>(qs[2 * sb][f][0], lo1, hi1);
-        const int vr = icw_rrow_val<MR>(qs[2 * sb + 1][f][0], lo1, hi1);
+        const int vl = icw_rrow_val<MR>(qs[2 * sb][f >> 1][0][f & 1], lo1, hi1);
+        const int vr = icw_rrow_val<MR>(qs[2 * sb + 1][f >> 1][0][f & 1], lo1, hi1);
         const uint32_t l = (uint32_t)(vl << k.norm_shift);
         const uint32_t rr = (uint32_t)(vr << k.norm_shift);
         if (osz == 2) {
@@ -3069,7 +3092,7 @@ __device__ __forceinline__ bool icw_rrow_flush(const double (*qs)[ICW_MAX_NS_TAP
 /* the flush of a clamp-free block: every |q| < clip_abs, finite -- no clip to count, the integer is the
  * plain conversion (exact below 2^31) + the mid-riser's delta, no clamp, no NaN */
 template <bool MR>
-__device__ __forceinline__ void icw_rrow_flush_fast(const double (*qs)[ICW_MAX_NS_TAPS][16], int r, int lr, int lane,
+__device__ __forceinline__ void icw_rrow_flush_fast(const double (*qs)[ICW_MAX_NS_TAPS / 2][16][2], int r, int lr, int lane,
                                                     const IcwRenderK &k, double &pk, unsigned char *o0,
                                                     unsigned char *o1, int osz)
 {
@@ -3078,9 +3101,10 @@ __device__ __forceinline__ void icw_rrow_flush_fast(const double (*qs)[ICW_MAX_N
     /* the four reads first, unconditionally (clamped indices; a lane's second peak sample repeats its
      * first where lr + 16 >= U, which changes no maximum), so they share one wait */
     const int f = lane & 31, sb = lane >> 5, fc = f < U ? f : U - 1;
-    const double q0 = qs[r][lr][lr];
-    const double q1 = qs[r][lr + 16 < U ? lr + 16 : lr][lr];
-    const double ql = qs[2 * sb][fc][0], qr = qs[2 * sb + 1][fc][0];
+    const int j1 = lr + 16 < U ? lr + 16 : lr;
+    const double q0 = qs[r][lr >> 1][lr][lr & 1];
+    const double q1 = qs[r][j1 >> 1][lr][j1 & 1];
+    const double ql = qs[2 * sb][fc >> 1][0][fc & 1], qr = qs[2 * sb + 1][fc >> 1][0][fc & 1];
     pk = icw_vmax_abs(icw_vmax_abs(pk, q0), q1);
     const int vl = icw_cvt_sat_i32(ql) + (MR && ql < 0.0 ? -1 : 0);
     const int vr = icw_cvt_sat_i32(qr) + (MR && qr < 0.0 ? -1 : 0);
@@ -3106,7 +3130,8 @@ __global__ __launch_bounds__(64) void icw_render_row(IcwK3Args a)
     constexpr int U = ICW_MAX_NS_TAPS;                 /* samples per unrolled block */
     constexpr int R = KIND == 1 ? U : (KIND == 2 ? 4 : 1);
     static_assert(U % R == 0, "ring period must divide the unroll");
-    __shared__ double qs[4][U][16];                    /* q of each sample, every lane its own slot */
+    static_assert(U % 2 == 0, "samples go in pairs");
+    __shared__ __attribute__((aligned(16))) double qs[4][U / 2][16][2];   /* q of each sample, every lane its own slots */
     const int lane = threadIdx.x, r = lane >> 4, lr = lane & 15;
     const int g0 = blockIdx.x * 4 + r;
     const bool valid = g0 < a.n_gen;
@@ -3148,13 +3173,14 @@ __global__ __launch_bounds__(64) void icw_render_row(IcwK3Args a)
     const int sA = blockIdx.x * 2, sB = sA + 1;
     unsigned char *oA = 2 * sA < a.n_gen ? a.out + (size_t)sA * a.out_stride : nullptr;
     unsigned char *oB = 2 * sB < a.n_gen ? a.out + (size_t)sB * a.out_stride : nullptr;
-    double *qst = &qs[r][0][lr];
+    double *qst = &qs[r][0][lr][0];
     unsigned clips = 0;
     double pk = 0.0;
     const int T = a.T;
     /* block j's inputs in LDS buffer j & 1: loaded at the end of block j - 3, stored at the end of
      * block j - 2, read (a block ahead) during block j - 1 */
-    __shared__ double xsl[2][4][U], dsl[2][4][U];
+    __shared__ __attribute__((aligned(16))) double xsl[2][4][U];
+    __shared__ __attribute__((aligned(16))) double dsl[2][4][U];
     const double nm = k.norm_mul, thr = k.spec_thr;
     IcwRowStage stg;
     icw_rrow_stage_load(a, 0, lane, stg);

@@ -1,6 +1,6 @@
 #!/bin/bash
 mkdir -p gpurun_out; export TMPDIR=/tmp; R=$(pwd)
-timeout -k 10 600 python -u -m pytest tests/test_gpu_render_spec.py tests/test_gpu_parity.py -x -q --timeout 200 --timeout-method thread > gpurun_out/r5k3rd_tests.txt 2>&1
+timeout -k 10 600 python -u -m pytest tests/test_gpu_render_spec.py tests/test_gpu_parity.py tests/test_gpu_sig_fast.py tests/test_gpu_fir.py -x -q --timeout 200 --timeout-method thread > gpurun_out/r5k3rd_tests.txt 2>&1
 rc=$?; echo "[tests] rc=$rc"; tail -2 gpurun_out/r5k3rd_tests.txt; [ $rc -eq 0 ] || exit 2
 for L in libicw.so libicw_noload.so libicw_prev.so; do
   ( cd /tmp && ICW_LIB=$L timeout -s KILL 150 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/gpurun_out/r5k3rd_trace_${L%.so}" -o run \
@@ -11,4 +11,9 @@ for r in csv.DictReader(open('gpurun_out/r5k3rd_trace_${L%.so}/run_kernel_stats.
     if 'render_row' in r['Name']: print('$L', r['Name'][:40], r['AverageNs'])"
 done
 TAG=r5k3rd LIBS="libicw.so libicw_noload.so" bash tools/r5_k3r_wait.sh || exit 5
+
+for r in 1 2; do for W in c2fir c4fir; do for L in libicw_prev.so libicw.so; do
+  ICW_LIB=$L timeout -k 10 200 python -u bench.py --workload $W --steps 3 --warmup 1 --no-cpu-baseline --e2e-steps 0 > gpurun_out/r5k3rd_${W}_${L%.so}_$r.json 2>>gpurun_out/r5k3rd_err.log || { echo "bench failed"; exit 6; }
+  python3 -c "import json,sys; d=json.load(open(sys.argv[1])); print(sys.argv[2], round(d['value'],1), round(d['roofline'].get('achieved',0),2))" gpurun_out/r5k3rd_${W}_${L%.so}_$r.json "$W $L"
+done; done; done
 echo all-ok
