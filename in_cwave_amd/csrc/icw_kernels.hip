@@ -2999,40 +2999,68 @@ struct IcwRowStage {
     double2 x, d;
 };
 
-__device__ __forceinline__ void icw_rrow_stage_load(const IcwK3Args &a, int t0, int lane, IcwRowStage &st)
+/* What a lane stages, fixed for the launch: its source rows at t0 = 0 (the addresses then advance by
+ * t0, no per-block 64-bit multiplies), its frame within a block for the t0 + i < T test, whether it
+ * loads at all, and its LDS offsets inside one buffer (the buffer's own offset is a scalar) */
+struct IcwRowLane {
+    const double *xp, *dp;
+    int xi, di;
+    bool xv, dvv;
+    uint32_t xo, dof;
+};
+
+__device__ __forceinline__ IcwRowLane icw_rrow_lane(const IcwK3Args &a, int lane)
+{
+    constexpr int U = ICW_MAX_NS_TAPS;
+    IcwRowLane L;
+    const int sb = lane >> 5, i = lane & 31;
+    const int s = blockIdx.x * 2 + sb;
+    L.xi = i;
+    L.xv = i < U && 2 * s < a.n_gen;
+    L.xp = L.xv ? a.pre + (size_t)s * a.pre_stride + (size_t)i * 2 : a.pre;
+    const int tt = lane >> 1, h = lane & 1;
+    L.di = tt;
+    L.dvv = a.dith && lane < 2 * U && (int)blockIdx.x * 4 + 2 * h < a.n_gen;
+    L.dp = L.dvv ? a.dith + (size_t)tt * a.dith_pitch + blockIdx.x * 4 + 2 * h : a.dith;
+    L.xo = (uint32_t)(((2 * sb) * U + (i < U ? i : 0)) * sizeof(double));
+    L.dof = (uint32_t)(((2 * h) * U + (lane < 2 * U ? tt : 0)) * sizeof(double));
+    return L;
+}
+
+__device__ __forceinline__ void icw_rrow_stage_load(const IcwK3Args &a, const IcwRowLane &L, int t0, IcwRowStage &st)
 {
 #ifdef ICW_K3R_NOLOAD
     if (t0 >= 3 * ICW_MAX_NS_TAPS) return;          /* diagnostic build (timing only): no staging loads */
 #endif
-    constexpr int U = ICW_MAX_NS_TAPS;
-    const int sb = lane >> 5, i = lane & 31;
-    const int s = blockIdx.x * 2 + sb;
     st.x = make_double2(0.0, 0.0);
     st.d = make_double2(0.0, 0.0);
-    if (i < U && t0 + i < a.T && 2 * s < a.n_gen)
-        st.x = *(const double2 *)(a.pre + (size_t)s * a.pre_stride + (size_t)(t0 + i) * 2);
-    const int tt = lane >> 1, h = lane & 1;
-    if (a.dith && lane < 2 * U && t0 + tt < a.T && (int)blockIdx.x * 4 + 2 * h < a.n_gen)
-        st.d = *(const double2 *)(a.dith + (size_t)(t0 + tt) * a.dith_pitch + blockIdx.x * 4 + 2 * h);
+    if (L.xv && t0 + L.xi < a.T) st.x = *(const double2 *)(L.xp + (size_t)t0 * 2);
+    if (L.dvv && t0 + L.di < a.T) st.d = *(const double2 *)(L.dp + (size_t)t0 * a.dith_pitch);
 }
 
 /* The inputs go to LDS as x * norm_mul (sound_render.c:754's product, formed here lane-parallel: two
  * multiplies per block instead of one per sample on the chain).  Returns, wave-uniform, whether every
- * staged |x * norm_mul| <= thr (render_consts' spec_thr; NaN fails): the block may run clamp-free. */
+ * staged |x * norm_mul| <= thr (render_consts' spec_thr; NaN fails): the block may run clamp-free.
+ * xs / ds: the buffer's x rows [4][U] and dither rows [4][U]. */
 __device__ __forceinline__ bool icw_rrow_stage_store(double (*xs)[ICW_MAX_NS_TAPS], double (*ds)[ICW_MAX_NS_TAPS],
-                                                     int lane, const IcwRowStage &st, double nm, double thr)
+                                                     int lane, const IcwRowLane &L, const IcwRowStage &st, double nm,
+                                                     double thr)
 {
     constexpr int U = ICW_MAX_NS_TAPS;
-    const int sb = lane >> 5, i = lane & 31;
+    const int i = lane & 31;
     bool ok = true;
     if (i < U) {
         const double a = st.x.x * nm, b = st.x.y * nm;
-        xs[2 * sb][i] = a;
-        xs[2 * sb + 1][i] = b;
+        double *p = (double *)((char *)&xs[0][0] + L.xo);
+        p[0] = a;
+        p[U] = b;
         ok = fabs(a) <= thr && fabs(b) <= thr;
     }
-    const int tt = lane >> 1, h = lane & 1;
-    if (lane < 2 * U) { ds[2 * h][tt] = st.d.x; ds[2 * h + 1][tt] = st.d.y; }
+    if (lane < 2 * U) {
+        double *p = (double *)((char *)&ds[0][0] + L.dof);
+        p[0] = st.d.x;
+        p[U] = st.d.y;
+    }
     return __all(ok);
 }
 
@@ -3093,8 +3121,7 @@ __device__ __forceinline__ bool icw_rrow_flush(const double (*qs)[ICW_MAX_NS_TAP
  * plain conversion (exact below 2^31) + the mid-riser's delta, no clamp, no NaN */
 template <bool MR>
 __device__ __forceinline__ void icw_rrow_flush_fast(const double (*qs)[ICW_MAX_NS_TAPS / 2][16][2], int r, int lr, int lane,
-                                                    const IcwRenderK &k, double &pk, unsigned char *o0,
-                                                    unsigned char *o1, int osz)
+                                                    const IcwRenderK &k, double &pk, unsigned char *o, int osz)
 {
     constexpr int U = ICW_MAX_NS_TAPS;
     __builtin_amdgcn_wave_barrier();
@@ -3110,12 +3137,12 @@ __device__ __forceinline__ void icw_rrow_flush_fast(const double (*qs)[ICW_MAX_N
     const int vr = icw_cvt_sat_i32(qr) + (MR && qr < 0.0 ? -1 : 0);
     const uint32_t l = (uint32_t)(vl << k.norm_shift);
     const uint32_t rr = (uint32_t)(vr << k.norm_shift);
-    unsigned char *o = sb ? o1 : o0;
-    if (o && f < U) {
+    /* o: this lane's frame in the block's output (null: no frame to write) */
+    if (o) {
         if (osz == 2) {
-            *(uint32_t *)(o + (size_t)f * 4) = (l & 0xffffu) | (rr << 16);
+            *(uint32_t *)o = (l & 0xffffu) | (rr << 16);
         } else {
-            uint16_t *p = (uint16_t *)(o + (size_t)f * 6);
+            uint16_t *p = (uint16_t *)o;
             p[0] = (uint16_t)(l & 0xffffu);
             p[1] = (uint16_t)(((l >> 16) & 0xffu) | ((rr & 0xffu) << 8));
             p[2] = (uint16_t)((rr >> 8) & 0xffffu);
@@ -3183,11 +3210,15 @@ __global__ __launch_bounds__(64) void icw_render_row(IcwK3Args a)
     __shared__ __attribute__((aligned(16))) double dsl[2][4][U];
     const double nm = k.norm_mul, thr = k.spec_thr;
     IcwRowStage stg;
-    icw_rrow_stage_load(a, 0, lane, stg);
-    bool x_ok0 = icw_rrow_stage_store(xsl[0], dsl[0], lane, stg, nm, thr);
-    icw_rrow_stage_load(a, U, lane, stg);
-    bool x_ok1 = icw_rrow_stage_store(xsl[1], dsl[1], lane, stg, nm, thr);
-    icw_rrow_stage_load(a, 2 * U, lane, stg);
+    const IcwRowLane sl = icw_rrow_lane(a, lane);
+    /* the frame this lane writes in a clamp-free block's flush: frame lane & 31 of stream A / B */
+    unsigned char *const olane = (lane & 31) < U && ((lane >> 5) ? oB : oA) ? ((lane >> 5) ? oB : oA) + (size_t)(lane & 31) * 2 * osz
+                                                                          : nullptr;
+    icw_rrow_stage_load(a, sl, 0, stg);
+    bool x_ok0 = icw_rrow_stage_store(xsl[0], dsl[0], lane, sl, stg, nm, thr);
+    icw_rrow_stage_load(a, sl, U, stg);
+    bool x_ok1 = icw_rrow_stage_store(xsl[1], dsl[1], lane, sl, stg, nm, thr);
+    icw_rrow_stage_load(a, sl, 2 * U, stg);
     __builtin_amdgcn_wave_barrier();
     double xin[U], dv[U];
 #pragma unroll
@@ -3216,16 +3247,16 @@ __global__ __launch_bounds__(64) void icw_render_row(IcwK3Args a)
         icw_rrow_block<KIND, NN, R, 0, MR, FAST>(xin, dv, prev_err, E, O, P, P2, c, k, qst, &xsl[nb][r][0],
                                                  &dsl[nb][r][0]);
         x_ok0 = x_ok1;
-        x_ok1 = icw_rrow_stage_store(xsl[kb & 1], dsl[kb & 1], lane, stg, nm, thr);
+        x_ok1 = icw_rrow_stage_store(xsl[kb & 1], dsl[kb & 1], lane, sl, stg, nm, thr);
         if constexpr (FAST) {
-            icw_rrow_flush_fast<MR>(qs, r, lr, lane, k, pk, ot0, ot1, osz);
+            icw_rrow_flush_fast<MR>(qs, r, lr, lane, k, pk, olane ? olane + (size_t)t * 2 * osz : nullptr, osz);
 #ifdef ICW_K3R_COUNT
             if (lr == 0 && valid) atomicAdd(&a.clips[g], 1u);   /* diagnostic build: clamp-free blocks */
 #endif
         } else {
             calm = icw_rrow_flush<MR>(qs, r, lr, lane, U, k, clips, pk, ot0, ot1, osz);
         }
-        icw_rrow_stage_load(a, t + 3 * U, lane, stg);
+        icw_rrow_stage_load(a, sl, t + 3 * U, stg);
         __builtin_amdgcn_wave_barrier();
         t += U;
         ++kb;

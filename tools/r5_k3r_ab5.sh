@@ -14,4 +14,5 @@ for r in 1 2; do for W in c5fir; do for L in libicw_prev.so libicw.so; do
   ICW_LIB=$L timeout -k 10 200 python -u bench.py --workload $W --steps 3 --warmup 1 --no-cpu-baseline --e2e-steps 0 > gpurun_out/${TAG}_${W}_${L%.so}_$r.json 2>>gpurun_out/${TAG}_err.log || { echo "bench failed"; exit 6; }
   python3 -c "import json,sys; d=json.load(open(sys.argv[1])); print(sys.argv[2], round(d['value'],1))" gpurun_out/${TAG}_${W}_${L%.so}_$r.json "$W $L"
 done; done; done
+TAG=r5k3rf_sq bash tools/r5_k3r_sq.sh || exit 7
 echo all-ok
