@@ -243,7 +243,14 @@ __global__ __launch_bounds__(256) void icw_unpack_frames(IcwK0Args a)
 #define ICW_CHAIN4 1                                 /* KF2: chain programs op by op over a lane's frames */
 #endif
 
-__device__ __forceinline__ int icw_fir_phys(int i) { return i + (i >> 3); }
+/* The staged inputs carry ICW_FIR_PAD pad doubles after every 8 (physical index i + PAD (i / 8)).  With
+ * 2 a lane's window (8 outputs apart: 10 doubles = 20 dwords) starts 16-byte aligned at every lane, and
+ * the sums read it two doubles at a time (ds_read_b128, conflict-free over each 16-lane group: 20 l
+ * mod 64 covers the 64 banks once), half the LDS instructions of the 1-pad layout's ds_read_b64. */
+#ifndef ICW_FIR_PAD
+#define ICW_FIR_PAD 2
+#endif
+__device__ __forceinline__ int icw_fir_phys(int i) { return i + ICW_FIR_PAD * (i >> 3); }
 
 
 /* inputs of NC channels from ch0 for the outputs [tt, tt + nout) of a launch block, at logical
@@ -438,15 +445,33 @@ __device__ __forceinline__ void icw_fir_block8(const double *xs, icw_ctap *gs, i
 {
     constexpr int W = ICW_FIR_R + 14;
     double L[W], Rt[W], g[8];
+    if constexpr (ICW_FIR_PAD == 2) {
+        /* elements e, e + 1 (e even) never straddle a pad: the window starts at logical phase 2 */
 #pragma unroll
-    for (int e = 0; e < W; ++e) {
-        L[e] = xs[bl + e + ((e + 2) >> 3)];
-        asm volatile("" ::: "memory");               /* no ds_read2 pairing: 2 x 2 cycles, not 8 */
-    }
+        for (int e = 0; e < W; e += 2) {
+            const double2 v = *(const double2 *)(xs + bl + e + 2 * ((e + 2) >> 3));
+            L[e] = v.x;
+            L[e + 1] = v.y;
+            asm volatile("" ::: "memory");
+        }
 #pragma unroll
-    for (int e = 0; e < W; ++e) {
-        Rt[e] = xs[br + e + ((e + 2) >> 3)];
-        asm volatile("" ::: "memory");
+        for (int e = 0; e < W; e += 2) {
+            const double2 v = *(const double2 *)(xs + br + e + 2 * ((e + 2) >> 3));
+            Rt[e] = v.x;
+            Rt[e + 1] = v.y;
+            asm volatile("" ::: "memory");
+        }
+    } else {
+#pragma unroll
+        for (int e = 0; e < W; ++e) {
+            L[e] = xs[bl + e + ((e + 2) >> 3)];
+            asm volatile("" ::: "memory");               /* no ds_read2 pairing: 2 x 2 cycles, not 8 */
+        }
+#pragma unroll
+        for (int e = 0; e < W; ++e) {
+            Rt[e] = xs[br + e + ((e + 2) >> 3)];
+            asm volatile("" ::: "memory");
+        }
     }
 #pragma unroll
     for (int j = 0; j < 8; ++j) g[j] = gs[k0 + j];
@@ -465,12 +490,13 @@ __device__ __forceinline__ void icw_fir_sums(const double *xs, icw_ctap *gs, int
 #pragma unroll
     for (int r = 0; r < ICW_FIR_R; ++r) acc[r] = 0.0;
     const int nb = nt >> 3;
-    int bl = 9 * (ll + a - 2) + 2, br = 9 * (ll + a) + 2;
+    constexpr int G = 8 + ICW_FIR_PAD;                  /* physical doubles per group of 8 */
+    int bl = G * (ll + a - 2) + 2, br = G * (ll + a) + 2;
 #pragma unroll 1
     for (int b = 0; b < nb; ++b) {
         icw_fir_block8(xs, gs, 8 * b, bl, br, acc);
-        bl -= 18;
-        br += 18;
+        bl -= 2 * G;
+        br += 2 * G;
     }
     const int A = 8 * a;
 #pragma unroll 1
@@ -489,7 +515,7 @@ __device__ __forceinline__ void icw_fir_sums(const double *xs, icw_ctap *gs, int
  * go out coalesced through LDS to the CWAVE rows K2 reads */
 __global__ __launch_bounds__(256) void icw_fir_hilbert(IcwFirArgs a)
 {
-    extern __shared__ double xs[];                   /* staged inputs (padded), taps, Q */
+    extern __shared__ __attribute__((aligned(16))) double xs[];   /* staged inputs (padded), taps, Q */
     constexpr int TF = 256 * ICW_FIR_R;
     const int ch = blockIdx.y, s = blockIdx.z;
     const int tt = blockIdx.x * TF;
@@ -498,7 +524,7 @@ __global__ __launch_bounds__(256) void icw_fir_hilbert(IcwFirArgs a)
     const int av = (c - 1 + sh) >> 3;
     const int nf = min(TF, a.T - tt);
     icw_fir_stage<1>(a, s, ch, xs, 0, tt, TF, sh, threadIdx.x, 256);
-    const int px = icw_fir_phys(sh + M + TF + 24) + 1;
+    const int px = (icw_fir_phys(sh + M + TF + 24) + 2) & ~1;   /* even: the next row stays 16-byte aligned */
     double *qs = xs + px + ((a.nt + 1) & ~1);
     icw_ctap *gs = (icw_ctap *)a.g;
     __syncthreads();
@@ -1815,7 +1841,7 @@ __global__ __launch_bounds__(256, ICW_FIR_OCC) void icw_fir_graph(IcwFirArgs f, 
 {
     ICW_FIR_STAMP(0);
     ICW_FIR_STAMP(1);                                /* diagnostic build: 0 / 7 = 100 MHz clock, 1-6 shader clock */
-    extern __shared__ double lds[];
+    extern __shared__ __attribute__((aligned(16))) double lds[];
     __shared__ unsigned red_clip[2][ICW_K2_TILE / 64];
     __shared__ double red_pk[2][ICW_K2_TILE / 64];
     /* workgroups in stream-fastest order (the grid is streams x tiles): the workgroups of one tile run
@@ -1830,7 +1856,7 @@ __global__ __launch_bounds__(256, ICW_FIR_OCC) void icw_fir_graph(IcwFirArgs f, 
     const int sh = (8 - ((c - 1) & 7)) & 7;
     const int av = (c - 1 + sh) >> 3;
     const int nf = min(TF, f.T - tt);
-    const int px = icw_fir_phys(sh + M + TF + 24) + 1;     /* doubles per staged channel */
+    const int px = (icw_fir_phys(sh + M + TF + 24) + 2) & ~1;   /* doubles per staged channel (even) */
     double *lregs = lds + nchc * px + ((f.nt + 1) & ~1);
     icw_ctap *gs = (icw_ctap *)f.g;
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -3380,7 +3406,7 @@ static size_t fir_lds(int M, int nt, int nchc, int tf, int n_regs)
 {
     const int sh = (8 - ((M / 2 - 1) & 7)) & 7;
     const int nl = sh + M + tf + 24;
-    const size_t px = (size_t)(nl + (nl >> 3)) + 1;
+    const size_t px = (size_t)(nl + ICW_FIR_PAD * (nl >> 3) + 2) & ~(size_t)1;
     return ((size_t)nchc * px + (size_t)((nt + 1) & ~1) + (size_t)nchc * tf + (size_t)n_regs * 4 * ICW_K2_TILE) *
            sizeof(double);
 }
