@@ -1238,6 +1238,14 @@ __device__ __forceinline__ double icw_vmax(double a, double b)
     return r;
 }
 
+/* max(|a|, |b|) as one v_max_f64: a NaN operand gives the other magnitude (maxNum), two NaNs a NaN */
+__device__ __forceinline__ double icw_vmax_abs2(double a, double b)
+{
+    double r;
+    asm("v_max_f64 %0, |%1|, |%2|" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+
 /* The render of the R frames (see above).  MR: mid-riser, q = x (x + +-0.0 with x's sign is x) and
  * delta = -1 below zero; mid-tread: q = copysign(|x| + 0.5, x), the reference's x +- 0.5 (-0.0 gives
  * -0.5, harmless as above), delta 0.  The integer is the saturating conversion; the clamp to
@@ -1247,10 +1255,10 @@ template <bool MR, int R>
 __device__ __forceinline__ void icw_fast_render(const IcwRenderK &rk, const double (&x)[R][2], int (&dv)[R][2],
                                                 double &lm_l, double &lm_r, unsigned &clip_l, unsigned &clip_r)
 {
+    static_assert(R >= 2, "the meters start from the first two frames");
     double q[R][2];
     int del[R][2];
     bool nan = false;
-    lm_l = lm_r = 0.0;
 #pragma unroll
     for (int r = 0; r < R; ++r) {
 #pragma unroll
@@ -1265,6 +1273,13 @@ __device__ __forceinline__ void icw_fast_render(const IcwRenderK &rk, const doub
             dv[r][c] = (int)((unsigned)(icw_cvt_sat_i32(q[r][c]) + del[r][c]) << rk.norm_shift);
             nan |= q[r][c] != q[r][c];
         }
+    }
+    /* the largest |q| of the frames (a NaN q counts as nothing, as fmax from 0.0 does; all-NaN
+     * frames give a NaN here, which no comparison passes and the peak's v_max_f64 skips) */
+    lm_l = icw_vmax_abs2(q[0][0], q[1][0]);
+    lm_r = icw_vmax_abs2(q[0][1], q[1][1]);
+#pragma unroll
+    for (int r = 2; r < R; ++r) {
         lm_l = icw_vmax_abs(lm_l, q[r][0]);
         lm_r = icw_vmax_abs(lm_r, q[r][1]);
     }
@@ -1291,6 +1306,19 @@ __device__ __forceinline__ void icw_fast_render(const IcwRenderK &rk, const doub
     }
 }
 
+/* 16 bytes at a wave-uniform base + a lane's 32-bit byte offset, as a raw buffer load: the base goes
+ * into the descriptor (SGPRs), so no address arithmetic runs on the VALU -- a global load took a
+ * v_lshl_add_u64 per load (the lane offset held as 64 bits), 4-8 per pass of the fused converter */
+__device__ __forceinline__ double2 icw_ld_row2(const double *base, uint32_t lane_bytes)
+{
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void *)base, (short)0, 0x7fffffff, 0x00020000);
+    const auto v = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)lane_bytes, 0, 0);
+    double2 d;
+    d.x = __longlong_as_double((long long)(((unsigned long long)v[1] << 32) | v[0]));
+    d.y = __longlong_as_double((long long)(((unsigned long long)v[3] << 32) | v[2]));
+    return d;
+}
+
 template <bool TRIG, int R, int SIG, int I>
 __device__ __forceinline__ void icw_sig_fast_ops(const IcwK2Args &a, icw_cprog *P, const IcwLR (&in)[R],
                                                  IcwLR (&prev)[R], double (&lOut)[R], double (&rOut)[R],
@@ -1303,15 +1331,12 @@ __device__ __forceinline__ void icw_sig_fast_ops(const IcwK2Args &a, icw_cprog *
         double cs[R][2], sn[R][2];
         if constexpr (rot) {
             const int ts0 = op.tslot[0], ts1 = op.tslot[1];
-            /* a wave-uniform row base (SGPRs) + the lane's 32-bit byte offset: the loads' saddr form,
-             * no 64-bit address arithmetic per load */
-            const size_t lane_b = (size_t)(tro_lane * 8u);
+            /* a wave-uniform row base (SGPRs) + the lane's 32-bit byte offset */
+            const uint32_t lane_b = tro_lane * 8u;
 #pragma unroll
             for (int r = 0; r < R; ++r) {
-                const char *b0 = (const char *)(a.trig_tab + tro_u + (size_t)r * tro_step + ts0 * 2);
-                const char *b1 = (const char *)(a.trig_tab + tro_u + (size_t)r * tro_step + ts1 * 2);
-                const double2 f0 = *(const double2 *)(b0 + lane_b);
-                const double2 f1 = *(const double2 *)(b1 + lane_b);
+                const double2 f0 = icw_ld_row2(a.trig_tab + tro_u + (size_t)r * tro_step + ts0 * 2, lane_b);
+                const double2 f1 = icw_ld_row2(a.trig_tab + tro_u + (size_t)r * tro_step + ts1 * 2, lane_b);
                 cs[r][0] = f0.x; sn[r][0] = f0.y;
                 cs[r][1] = f1.x; sn[r][1] = f1.y;
             }
@@ -1522,34 +1547,82 @@ __device__ __forceinline__ void icw_chain_frames_rowp(const IcwK2Args &a, icw_cp
     icw_chain_frames<TRIG, R, true>(a, P, s, t0, nv, in, clip_l, clip_r, pk_l, pk_r, dv, tro_lane, tro_u, tro_step);
 }
 
-/* the device library's wave reduction of doubles (declared by HIP only with its extra warp-sync types) */
-extern "C" __device__ __attribute__((const)) double __ockl_wfred_max_f64(double);
-
-/* per-workgroup meters (ICW_K2_TILE threads): wave reduce, LDS, one atomic per stream/channel */
-__device__ __forceinline__ void icw_meters_wg(const IcwK2Args &a, int s, unsigned clip_l, unsigned clip_r, double pk_l,
-                                              double pk_r, unsigned (*red_clip)[ICW_K2_TILE / 64],
-                                              double (*red_pk)[ICW_K2_TILE / 64])
+/* The stereo I / Q exchange between lane l (channel L) and lane l + 32 (channel R) of a wave: with
+ * a = x[r] and b = x[r + 4] of each lane, afterwards a = L's value and b = R's value of the lane's
+ * frame (lane l: frame r, lane l + 32: frame r + 4).  v_permlane32_swap trades the upper half of one
+ * VGPR with the lower half of another on the VALU, two per double, where __shfl_xor(x, 32) took two
+ * ds_bpermute round trips through the LDS plus a select (c2fir kernel 0.331 -> 0.328 ms, c4fir
+ * 3.114 -> 3.084 ms, profiles/r03_fir_swap_ab.jsonl). */
+__device__ __forceinline__ void icw_swap32(double &a, double &b)
 {
-    const int tl = threadIdx.x;
-    /* wave reductions by DPP (the device library's wfred): six dependent __shfl_xor rounds each were
-     * an LDS permute and its wait -- 36 LDS instructions per wave in the fused converter's graph phase.
-     * Sums of the clip counts and maxima of the peaks are exact in any order; the counts are reduced
-     * only when a lane of the wave clipped (a ballot), the usual case being none. */
-    if (__any((clip_l | clip_r) != 0u)) {
-        clip_l = __ockl_wfred_add_u32(clip_l);
-        clip_r = __ockl_wfred_add_u32(clip_r);
+    const unsigned long long ua = __double_as_longlong(a), ub = __double_as_longlong(b);
+    const auto lo = __builtin_amdgcn_permlane32_swap((unsigned)ua, (unsigned)ub, false, false);
+    const auto hi = __builtin_amdgcn_permlane32_swap((unsigned)(ua >> 32), (unsigned)(ub >> 32), false, false);
+    a = __longlong_as_double(((unsigned long long)hi[0] << 32) | lo[0]);
+    b = __longlong_as_double(((unsigned long long)hi[1] << 32) | lo[1]);
+}
+
+/* peak / clip reduction slots of a workgroup: per channel two per wave, one per 16-lane row (icw_meters_wg) */
+#define ICW_PK_SLOTS (ICW_K2_TILE / 32)
+
+/* every lane of a 16-lane row gets the row's largest value, for doubles >= +0.0 that are never a NaN
+ * (so v_max_f64 without canonicalising, and any order gives the same value): DPP row_ror 8, 4, 2, 1,
+ * each two v_mov_b32_dpp and one v_max_f64.  Full EXEC. */
+template <int CTRL>
+__device__ __forceinline__ double icw_dpp_max_nn(double v)
+{
+    const unsigned long long u = (unsigned long long)__double_as_longlong(v);
+    const unsigned lo = (unsigned)__builtin_amdgcn_mov_dpp((int)(unsigned)u, CTRL, 0xf, 0xf, false);
+    const unsigned hi = (unsigned)__builtin_amdgcn_mov_dpp((int)(unsigned)(u >> 32), CTRL, 0xf, 0xf, false);
+    return icw_vmax(v, __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo)));
+}
+
+__device__ __forceinline__ double icw_row_max_nn(double v)
+{
+    v = icw_dpp_max_nn<0x128>(v);                    /* row_ror:8 */
+    v = icw_dpp_max_nn<0x124>(v);                    /* row_ror:4 */
+    v = icw_dpp_max_nn<0x122>(v);                    /* row_ror:2 */
+    return icw_dpp_max_nn<0x121>(v);                 /* row_ror:1 */
+}
+
+/* the sum over a 16-lane row, in every lane of it (the same rotations) */
+__device__ __forceinline__ unsigned icw_row_sum_u32(unsigned v)
+{
+    v += (unsigned)__builtin_amdgcn_mov_dpp((int)v, 0x128, 0xf, 0xf, false);
+    v += (unsigned)__builtin_amdgcn_mov_dpp((int)v, 0x124, 0xf, 0xf, false);
+    v += (unsigned)__builtin_amdgcn_mov_dpp((int)v, 0x122, 0xf, 0xf, false);
+    return v + (unsigned)__builtin_amdgcn_mov_dpp((int)v, 0x121, 0xf, 0xf, false);
+}
+
+/* per-workgroup meters (ICW_K2_TILE threads, full EXEC): row reduce, LDS, one atomic per
+ * stream/channel.  The peaks are maxima of |q| from +0.0 (fmax / v_max_f64 return the number for a
+ * NaN operand), so they are >= +0.0 and never a NaN, and their maximum is the same in any order; the
+ * clip counts are sums of integers.  The two channels share one reduction: v_permlane32_swap leaves
+ * lanes 0-31 with channel L's values of lanes l and l + 32 and lanes 32-63 with channel R's (one
+ * max), each 16-lane row is reduced by DPP, and lanes 0 and 16 (L) / 32 and 48 (R) hand their row's
+ * maximum to the final reduction -- ~15 VALU per wave where two device-library wave reductions
+ * (-inf fills, canonicalising maxima, cross-row steps) took ~75 in the fused converter's graph phase.
+ * The counts are reduced only when a lane of the wave clipped (a ballot), the usual case being none. */
+__device__ __forceinline__ void icw_meters_wg(const IcwK2Args &a, int s, unsigned clip_l, unsigned clip_r, double pk_l,
+                                              double pk_r, unsigned (*red_clip)[ICW_PK_SLOTS],
+                                              double (*red_pk)[ICW_PK_SLOTS])
+{
+    const int tl = threadIdx.x, ln = tl & 63, wv = tl >> 6;
+    const bool any_clip = __any((clip_l | clip_r) != 0u);
+    if (any_clip) {
+        const auto c = __builtin_amdgcn_permlane32_swap(clip_l, clip_r, false, false);
+        const unsigned cs = icw_row_sum_u32(c[0] + c[1]);
+        if ((ln & 15) == 0) red_clip[ln >> 5][2 * wv + ((ln >> 4) & 1)] = cs;
+    } else if ((ln & 15) == 0) {
+        red_clip[ln >> 5][2 * wv + ((ln >> 4) & 1)] = 0u;
     }
-    pk_l = __ockl_wfred_max_f64(pk_l);
-    pk_r = __ockl_wfred_max_f64(pk_r);
-    const int wv = tl >> 6;
-    if ((tl & 63) == 0) {
-        red_clip[0][wv] = clip_l; red_clip[1][wv] = clip_r;
-        red_pk[0][wv] = pk_l; red_pk[1][wv] = pk_r;
-    }
+    icw_swap32(pk_l, pk_r);
+    const double pk = icw_row_max_nn(icw_vmax(pk_l, pk_r));
+    if ((ln & 15) == 0) red_pk[ln >> 5][2 * wv + ((ln >> 4) & 1)] = pk;
     __syncthreads();
     if (tl < 2) {
         unsigned cs = 0; double pm = 0.0;
-        for (int i = 0; i < ICW_K2_TILE / 64; ++i) { cs += red_clip[tl][i]; pm = fmax(pm, red_pk[tl][i]); }
+        for (int i = 0; i < ICW_PK_SLOTS; ++i) { cs += red_clip[tl][i]; pm = fmax(pm, red_pk[tl][i]); }
         if (cs) atomicAdd(&a.clips[s * 2 + tl], cs);
         if (pm > 0.0) atomicMax(&a.peak_bits[s * 2 + tl], (unsigned long long)__double_as_longlong(pm));
     }
@@ -1643,8 +1716,8 @@ __device__ __forceinline__ void icw_output_body(const IcwK2Args &a, int bx, int 
     constexpr int NR = N + 1;                        /* window rows past the tile (row N+t: w[t]) */
     __shared__ double lw[2][4][TILE + 24];
     /* lregs: the DSP register file [n_regs][4][TILE] in dynamic LDS */
-    __shared__ unsigned red_clip[2][TILE / 64];
-    __shared__ double red_pk[2][TILE / 64];
+    __shared__ unsigned red_clip[2][ICW_PK_SLOTS];
+    __shared__ double red_pk[2][ICW_PK_SLOTS];
     const int tl = threadIdx.x;
     const int T = a.T;
     const int tw0 = bx * TILE * a.tpw;
@@ -1759,20 +1832,6 @@ __global__ __launch_bounds__(ICW_K2_TILE, ICW_K2_MINWG) void icw_output(IcwK2Arg
  * live across it in scratch -- 44 B per thread written to HBM, most of the kernel's 2.95x write
  * traffic (profiles/r02_c2fir_pmc.json: 198 MB per launch against 67 MB of output); giving that
  * variant 168 VGPRs instead (3 workgroups per CU) removed the spills but cost c2fir 22 %. */
-/* The stereo I / Q exchange between lane l (channel L) and lane l + 32 (channel R) of a wave: with
- * a = x[r] and b = x[r + 4] of each lane, afterwards a = L's value and b = R's value of the lane's
- * frame (lane l: frame r, lane l + 32: frame r + 4).  v_permlane32_swap trades the upper half of one
- * VGPR with the lower half of another on the VALU, two per double, where __shfl_xor(x, 32) took two
- * ds_bpermute round trips through the LDS plus a select (c2fir kernel 0.331 -> 0.328 ms, c4fir
- * 3.114 -> 3.084 ms, profiles/r03_fir_swap_ab.jsonl). */
-__device__ __forceinline__ void icw_swap32(double &a, double &b)
-{
-    const unsigned long long ua = __double_as_longlong(a), ub = __double_as_longlong(b);
-    const auto lo = __builtin_amdgcn_permlane32_swap((unsigned)ua, (unsigned)ub, false, false);
-    const auto hi = __builtin_amdgcn_permlane32_swap((unsigned)(ua >> 32), (unsigned)(ub >> 32), false, false);
-    a = __longlong_as_double(((unsigned long long)hi[0] << 32) | lo[0]);
-    b = __longlong_as_double(((unsigned long long)hi[1] << 32) | lo[1]);
-}
 
 /* NC: computed channels (1: mono input, 2: stereo), a template parameter so that each form gets its
  * own register allocation (the mono graph phase holds 8 frames per lane, the stereo one 4) */
@@ -1842,8 +1901,8 @@ __global__ __launch_bounds__(256, ICW_FIR_OCC) void icw_fir_graph(IcwFirArgs f, 
     ICW_FIR_STAMP(0);
     ICW_FIR_STAMP(1);                                /* diagnostic build: 0 / 7 = 100 MHz clock, 1-6 shader clock */
     extern __shared__ __attribute__((aligned(16))) double lds[];
-    __shared__ unsigned red_clip[2][ICW_K2_TILE / 64];
-    __shared__ double red_pk[2][ICW_K2_TILE / 64];
+    __shared__ unsigned red_clip[2][ICW_PK_SLOTS];
+    __shared__ double red_pk[2][ICW_PK_SLOTS];
     /* workgroups in stream-fastest order (the grid is streams x tiles): the workgroups of one tile run
      * together, so its rotation-table rows come from the L2 for every stream, where tile-fastest order
      * swept the whole block's table once per stream (a 2^20-frame block's table is 32 MB: c2fir 37 HBM
@@ -2198,8 +2257,8 @@ __device__ __forceinline__ void icw_s1_overlapped(const IcwS1Args &a, double *lr
 {
     auto stamp = [&a](int k) { icw_s1_stamp(a.stamps, k); };
     __shared__ double coef[40];
-    __shared__ unsigned red_clip[2][ICW_K2_TILE / 64], red_sn[4][ICW_K2_TILE / 64];
-    __shared__ double red_pk[2][ICW_K2_TILE / 64];
+    __shared__ unsigned red_clip[2][ICW_PK_SLOTS], red_sn[4][ICW_K2_TILE / 64];
+    __shared__ double red_pk[2][ICW_PK_SLOTS];
     const IcwK2Args &a2 = a.k2;
     const int tid = threadIdx.x, T = a2.T;
     double *rows = lregs + a.rows_off;
