@@ -139,6 +139,8 @@ struct IcwOp {
     int32_t wb_slot;               /* register form: the slot whose final value this op writes (its
                                       output goes to the persistent bus at a block's last frame), -1 */
     int32_t chain_in;              /* chain program: bit 0 reads `in`, bit 1 the previous op's output */
+    int32_t unit_gain[2];          /* gain[c] == 1.0: a scalar test for the kernels (an FP64 compare of an
+                                      SGPR value is a VALU instruction) */
 };
 
 /* A compiled DSP list.  Register form (frame-parallel output kernel): every slot read resolves at
@@ -173,6 +175,7 @@ struct IcwRenderK {
     int32_t sign_delta, norm_shift, is24;
     int32_t render_type, ns_kind, ns_n;
     int32_t lo1, hi1;              /* (int)lo + 1, (int)hi - 1: the clamp's integer bounds (scalar) */
+    int32_t unit_mul;              /* norm_mul == 1.0 (scalar test, as IcwOp.unit_gain) */
     double ns_c[40];
 };
 

@@ -319,6 +319,8 @@ void op_params(const icw_node &n, IcwOp &op)
     op.iqinv[1] = n.iq_invert[1];
     op.gain[0] = n.gain[0];
     op.gain[1] = n.gain[1];
+    op.unit_gain[0] = op.gain[0] == 1.0;
+    op.unit_gain[1] = op.gain[1] == 1.0;
     op.out_slot = n.mode == ICW_MODE_MASTER ? 0 : n.n_out;
     op.in_mask = 0;
     for (int k = 0; k < ICW_N_INPUTS; ++k)
@@ -554,6 +556,7 @@ void render_consts(const icw_render_cfg &cfg, int is24, IcwRenderK &k)
     k.clip_abs = std::min(k.hi, -k.lo);
     k.lo1 = (int32_t)k.lo + 1;
     k.hi1 = (int32_t)k.hi - 1;
+    k.unit_mul = k.norm_mul == 1.0;
     k.is24 = is24;
     k.render_type = (int)cfg.render_type;
     unsigned t = cfg.nshape_type > ICW_NSHAPE_MAX ? ICW_NSHAPE_FLAT : cfg.nshape_type;

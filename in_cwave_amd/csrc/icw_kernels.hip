@@ -250,6 +250,12 @@ __global__ __launch_bounds__(256) void icw_unpack_frames(IcwK0Args a)
 #ifndef ICW_FIR_PAD
 #define ICW_FIR_PAD 2
 #endif
+#ifndef ICW_SCALAR_UNIT
+#define ICW_SCALAR_UNIT 1                            /* A/B: unit gains / norm_mul tested on scalar flags */
+#endif
+#ifndef ICW_RENDER_SH0
+#define ICW_RENDER_SH0 1                             /* A/B: the render-only form specialised for norm_shift 0 */
+#endif
 __device__ __forceinline__ int icw_fir_phys(int i) { return i + ICW_FIR_PAD * (i >> 3); }
 
 
@@ -1251,10 +1257,13 @@ __device__ __forceinline__ double icw_vmax_abs2(double a, double b)
  * -0.5, harmless as above), delta 0.  The integer is the saturating conversion; the clamp to
  * [lo + 1, hi - 1] is needed only where |q| reaches clip_abs = min(hi, -lo) -- the pass's meter test
  * -- so it is applied there with the clip counts.  Then the NaN samples: INT_MIN (delta 0). */
-template <bool MR, int R>
+template <bool MR, bool SH0, int R>
 __device__ __forceinline__ void icw_fast_render(const IcwRenderK &rk, const double (&x)[R][2], int (&dv)[R][2],
                                                 double &lm_l, double &lm_r, unsigned &clip_l, unsigned &clip_r)
 {
+    /* SH0: norm_shift 0 (full sign bits, the usual case) -- no shift after the integer, so the
+     * mid-riser's delta folds into one subtract-with-borrow of the compare */
+    const int sh = SH0 ? 0 : rk.norm_shift;
     static_assert(R >= 2, "the meters start from the first two frames");
     double q[R][2];
     int del[R][2];
@@ -1265,12 +1274,12 @@ __device__ __forceinline__ void icw_fast_render(const IcwRenderK &rk, const doub
         for (int c = 0; c < 2; ++c) {
             if constexpr (MR) {
                 q[r][c] = x[r][c];
-                del[r][c] = x[r][c] < 0.0 ? rk.sign_delta : 0;   /* -1 (icw_launch_fir_graph checks) */
+                del[r][c] = x[r][c] < 0.0 ? -1 : 0;               /* sign_delta -1 (icw_launch_fir_graph checks) */
             } else {
                 q[r][c] = __builtin_copysign(fabs(x[r][c]) + rk.round_offset, x[r][c]);
                 del[r][c] = 0;
             }
-            dv[r][c] = (int)((unsigned)(icw_cvt_sat_i32(q[r][c]) + del[r][c]) << rk.norm_shift);
+            dv[r][c] = (int)((unsigned)(icw_cvt_sat_i32(q[r][c]) + del[r][c]) << sh);
             nan |= q[r][c] != q[r][c];
         }
     }
@@ -1294,7 +1303,7 @@ __device__ __forceinline__ void icw_fast_render(const IcwRenderK &rk, const doub
             clip_r += (q[r][1] >= rk.hi ? 1u : 0u) + (q[r][1] <= rk.lo ? 1u : 0u);
 #pragma unroll
             for (int c = 0; c < 2; ++c)
-                dv[r][c] = (int)((unsigned)(min(max(icw_cvt_sat_i32(q[r][c]), lo1), hi1) + del[r][c]) << rk.norm_shift);
+                dv[r][c] = (int)((unsigned)(min(max(icw_cvt_sat_i32(q[r][c]), lo1), hi1) + del[r][c]) << sh);
         }
     }
     if (nan) {
@@ -1302,7 +1311,7 @@ __device__ __forceinline__ void icw_fast_render(const IcwRenderK &rk, const doub
         for (int r = 0; r < R; ++r)
 #pragma unroll
             for (int c = 0; c < 2; ++c)
-                if (q[r][c] != q[r][c]) dv[r][c] = (int)(0x80000000u << rk.norm_shift);
+                if (q[r][c] != q[r][c]) dv[r][c] = (int)(0x80000000u << sh);
     }
 }
 
@@ -1355,12 +1364,12 @@ __device__ __forceinline__ void icw_sig_fast_ops(const IcwK2Args &a, icw_cprog *
         }
         constexpr bool unit = (SIG & ICW_SIG_UNIT) && mode != ICW_MODE_MASTER;
         const double g0 = op.gain[0], g1 = op.gain[1];
-        if (!unit && g0 != 1.0) {
+        if (!unit && (ICW_SCALAR_UNIT ? !op.unit_gain[0] : g0 != 1.0)) {
             asm volatile("");
 #pragma unroll
             for (int r = 0; r < R; ++r) { d[r].lre *= g0; d[r].lim *= g0; }
         }
-        if (!unit && g1 != 1.0) {
+        if (!unit && (ICW_SCALAR_UNIT ? !op.unit_gain[1] : g1 != 1.0)) {
             asm volatile("");
 #pragma unroll
             for (int r = 0; r < R; ++r) { d[r].rre *= g1; d[r].rim *= g1; }
@@ -1415,16 +1424,19 @@ __device__ __forceinline__ void icw_sig_fast(const IcwK2Args &a, icw_cprog *P, c
     double x[R][2];
 #pragma unroll
     for (int r = 0; r < R; ++r) { x[r][0] = lOut[r]; x[r][1] = rOut[r]; }
-    if (rk.norm_mul != 1.0) {
+    if (ICW_SCALAR_UNIT ? !rk.unit_mul : rk.norm_mul != 1.0) {
         asm volatile("");
 #pragma unroll
         for (int r = 0; r < R; ++r) { x[r][0] *= rk.norm_mul; x[r][1] *= rk.norm_mul; }
     }
     double lm_l, lm_r;
-    if (rk.sign_delta != 0)
-        icw_fast_render<true, R>(rk, x, dv, lm_l, lm_r, clip_l, clip_r);
-    else
-        icw_fast_render<false, R>(rk, x, dv, lm_l, lm_r, clip_l, clip_r);
+    if (ICW_RENDER_SH0 && rk.norm_shift == 0) {
+        if (rk.sign_delta != 0) icw_fast_render<true, true, R>(rk, x, dv, lm_l, lm_r, clip_l, clip_r);
+        else icw_fast_render<false, true, R>(rk, x, dv, lm_l, lm_r, clip_l, clip_r);
+    } else {
+        if (rk.sign_delta != 0) icw_fast_render<true, false, R>(rk, x, dv, lm_l, lm_r, clip_l, clip_r);
+        else icw_fast_render<false, false, R>(rk, x, dv, lm_l, lm_r, clip_l, clip_r);
+    }
     pk_l = icw_vmax(pk_l, lm_l);
     pk_r = icw_vmax(pk_r, lm_r);
 }
