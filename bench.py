@@ -635,10 +635,12 @@ def main():
         for w in os.environ.get("ICW_BENCH_OTHERS_MULTI" if world > 1 else "ICW_BENCH_OTHERS", default).split(","):
             gc.collect()
             torch.cuda.empty_cache()
-            o = measure_gpu(w, None, a.other_frames, 2, 1, 0, dev, local_dev, dist, rank, world)
+            # 3 timed steps after 2 warm-up steps: a leg follows a different workload (round 5's mid-round
+            # default run read c2fir 136 k where --workload c2fir runs read 142-146 k)
+            o = measure_gpu(w, None, a.other_frames, 3, 2, 0, dev, local_dev, dist, rank, world)
             ro = o["roofline"]
-            others[w] = {"value": o["value"], "unit": "Msamples/s", "ms_per_step": o["ms_per_step"], "steps": 2,
-                         "warmup": 1, "n_gpus": world, "workload": o["W"]["desc"], "streams_per_gpu": o["S"],
+            others[w] = {"value": o["value"], "unit": "Msamples/s", "ms_per_step": o["ms_per_step"], "steps": 3,
+                         "warmup": 2, "n_gpus": world, "workload": o["W"]["desc"], "streams_per_gpu": o["S"],
                          "streams_total": o["S"] * world, "frames_per_stream_per_step": o["T"],
                          "k1_kernel": ro["kernel"], "k1_avg_launch_ms": ro["avg_launch_ms"],
                          "k2_avg_launch_ms": ro["output_kernel_avg_launch_ms"], "fp64_frac": ro["frac"]}
