@@ -227,7 +227,8 @@ struct icw_ctx {
     unsigned long long *s1_stamps = nullptr;   /* ICW_S1_STAMPS=1: K5 phase stamps, printed per call */
     unsigned long long calls = 0;         /* icw_process_* calls so far (icw_prepare needs a fresh context) */
     /* per-stream state set by an entry point other than a call (stream_open, seek, set_state, the
-     * resets, set_outbits): icw_prepare's closing icw_stream_init would wipe it, so it refuses */
+     * resets): icw_prepare's closing icw_stream_init would wipe it, so it refuses.  Context-wide
+     * setters (set_outbits, set_render, ...) leave it false: the warm-up runs with them. */
     bool touched = false;
     std::mutex mu;
 };

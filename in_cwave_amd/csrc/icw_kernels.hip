@@ -1574,8 +1574,10 @@ __device__ __forceinline__ void icw_swap32(double &a, double &b)
     b = __longlong_as_double(((unsigned long long)hi[1] << 32) | lo[1]);
 }
 
-/* peak / clip reduction slots of a workgroup: per channel two per wave, one per 16-lane row (icw_meters_wg) */
+/* peak / clip reduction slots of a workgroup: per channel two per wave, one per 16-lane row (icw_meters_wg;
+ * every caller runs ICW_K2_TILE threads, KF2's launch bound included) */
 #define ICW_PK_SLOTS (ICW_K2_TILE / 32)
+static_assert(ICW_K2_TILE == 256, "icw_fir_graph launches 256 threads and shares icw_meters_wg's slots");
 
 /* every lane of a 16-lane row gets the row's largest value, for doubles >= +0.0 that are never a NaN
  * (so v_max_f64 without canonicalising, and any order gives the same value): DPP row_ror 8, 4, 2, 1,
