@@ -444,13 +444,18 @@ __device__ __forceinline__ void icw_fir_stage(const IcwFirArgs &f, int s, int ch
  * inputs -- which bounds the sums: 52 -> 44 LDS reads per 8-tap block of a lane's 8 outputs. */
 typedef const __attribute__((address_space(4))) double icw_ctap;
 
-/* one 8-tap block (k0 = 8b) of a lane's 8 outputs: bl / br = physical index of the first input of
- * the left / right window (both at phase 2 of the pad pattern) */
-__device__ __forceinline__ void icw_fir_block8(const double *xs, icw_ctap *gs, int k0, int bl, int br,
-                                               double (&acc)[ICW_FIR_R])
+/* one NTAP-tap block (k0 = NTAP b) of a lane's 8 outputs: bl / br = physical index of the first input
+ * of the left / right window (both at phase 2 of the pad pattern; NTAP 4 or 8 keeps it there) */
+#ifndef ICW_FIR_NTAP
+#define ICW_FIR_NTAP 8                               /* taps per register block of the sums */
+#endif
+template <int NTAP>
+__device__ __forceinline__ void icw_fir_block(const double *xs, icw_ctap *gs, int k0, int bl, int br,
+                                              double (&acc)[ICW_FIR_R])
 {
-    constexpr int W = ICW_FIR_R + 14;
-    double L[W], Rt[W], g[8];
+    static_assert(NTAP == 4 || NTAP == 8, "a window step of whole pad groups");
+    constexpr int W = ICW_FIR_R + 2 * NTAP - 2;
+    double L[W], Rt[W], g[NTAP];
     if constexpr (ICW_FIR_PAD == 2) {
         /* elements e, e + 1 (e even) never straddle a pad: the window starts at logical phase 2 */
 #pragma unroll
@@ -480,33 +485,36 @@ __device__ __forceinline__ void icw_fir_block8(const double *xs, icw_ctap *gs, i
         }
     }
 #pragma unroll
-    for (int j = 0; j < 8; ++j) g[j] = gs[k0 + j];
+    for (int j = 0; j < NTAP; ++j) g[j] = gs[k0 + j];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
+    for (int j = 0; j < NTAP; ++j) {
 #pragma unroll
         for (int r = 0; r < ICW_FIR_R; ++r)
-            acc[r] = __builtin_fma(g[j], L[r - 2 * j + 14] - Rt[r + 2 * j], acc[r]);
+            acc[r] = __builtin_fma(g[j], L[r - 2 * j + 2 * NTAP - 2] - Rt[r + 2 * j], acc[r]);
     }
 }
 
-/* Q of a lane's 8 outputs tt + 8 ll + r; a = (c - 1 + sh) / 8 */
+/* Q of a lane's 8 outputs tt + 8 ll + r; a = (c - 1 + sh) / 8.  The taps in ascending order, in
+ * register blocks of ICW_FIR_NTAP, then one by one */
 __device__ __forceinline__ void icw_fir_sums(const double *xs, icw_ctap *gs, int nt, int ll, int a, int sh, int c,
                                              double (&acc)[ICW_FIR_R])
 {
 #pragma unroll
     for (int r = 0; r < ICW_FIR_R; ++r) acc[r] = 0.0;
-    const int nb = nt >> 3;
+    constexpr int NB = ICW_FIR_NTAP;
+    const int nb = nt / NB;
     constexpr int G = 8 + ICW_FIR_PAD;                  /* physical doubles per group of 8 */
-    int bl = G * (ll + a - 2) + 2, br = G * (ll + a) + 2;
+    constexpr int GS = G * NB / 4;                      /* physical step of a window per block */
+    int bl = G * (ll + a - NB / 4) + 2, br = G * (ll + a) + 2;
 #pragma unroll 1
     for (int b = 0; b < nb; ++b) {
-        icw_fir_block8(xs, gs, 8 * b, bl, br, acc);
-        bl -= 2 * G;
-        br += 2 * G;
+        icw_fir_block<NB>(xs, gs, NB * b, bl, br, acc);
+        bl -= GS;
+        br += GS;
     }
     const int A = 8 * a;
 #pragma unroll 1
-    for (int k = nb * 8; k < nt; ++k) {
+    for (int k = nb * NB; k < nt; ++k) {
         const double gk = gs[k];
 #pragma unroll
         for (int r = 0; r < ICW_FIR_R; ++r) {
@@ -1869,13 +1877,14 @@ extern "C" int icw_fir_stamps_read(unsigned long long *dst, size_t n)
 
 /* KF2's mono chain form: the lane's ICW_FIR_R frames (from t0, nv of them in the block) two at a time
  * through one signature (SIG; 0: the generic op loop, ROWP: rows at known offsets), the rendered
- * frames packed into w (16-bit: w[0..8), 24-bit: 12 words) */
-template <bool TRIG, int SIG, bool ROWP>
+ * frames packed into w (16-bit: w[0..8), 24-bit: 12 words).  B24 is a template parameter: with a
+ * runtime flag the compiler merged the two packings' stores into one store at a selected index, which
+ * put w in scratch -- c3fir wrote 6.3 GB per launch against 4.3 GB of output (profiles/r05_c3fir_pmc.json) */
+template <bool TRIG, int SIG, bool ROWP, bool B24>
 __device__ __forceinline__ void icw_mono_passes(const IcwK2Args &a, icw_cprog *P, int s, int t0, int nv,
                                                 const double (&vi)[ICW_FIR_R], const double (&q)[ICW_FIR_R],
                                                 unsigned &clip_l, unsigned &clip_r, double &pk_l, double &pk_r,
-                                                unsigned (&w)[ICW_FIR_R / 2 * 3], bool b24, uint32_t tro_lane,
-                                                size_t pq)
+                                                unsigned (&w)[ICW_FIR_R / 2 * 3], uint32_t tro_lane, size_t pq)
 {
 #pragma unroll
     for (int hh = 0; hh < ICW_FIR_R; hh += 2) {
@@ -1895,7 +1904,7 @@ __device__ __forceinline__ void icw_mono_passes(const IcwK2Args &a, icw_cprog *P
         else
             icw_chain_frames<TRIG, 2, true>(a, P, s, t0 + hh, n2, in2, clip_l, clip_r, pk_l, pk_r, dv, tro_lane,
                                             (size_t)hh * pq, pq);
-        if (b24) {
+        if constexpr (B24) {
             const unsigned l0 = (unsigned)dv[0][0] & 0xffffffu, r0 = (unsigned)dv[0][1] & 0xffffffu;
             const unsigned l1 = (unsigned)dv[1][0] & 0xffffffu, r1 = (unsigned)dv[1][1] & 0xffffffu;
             w[hh / 2 * 3 + 0] = l0 | (r0 << 24);
@@ -2090,8 +2099,13 @@ __global__ __launch_bounds__(256, ICW_FIR_OCC) void icw_fir_graph(IcwFirArgs f, 
         const uint32_t tro_lane = (uint32_t)(((size_t)(tt >> 3) + ll) * a.trig_pitch);
         /* the signature is chosen once for the lane's four passes (inside the pass loop every pass
          * carried all variants while the eight inputs stayed live, and the rotating kernel spilled) */
-#define ICW_MONO(SIGV, RP) icw_mono_passes<TRIG, SIGV, RP>(a, P, s, tt + fr0, nf - fr0, vi, q, clip_l, clip_r, pk_l, pk_r, \
-                                                         w, b24, tro_lane, pq)
+#define ICW_MONO(SIGV, RP)                                                                                    \
+    do {                                                                                                      \
+        if (b24) icw_mono_passes<TRIG, SIGV, RP, true>(a, P, s, tt + fr0, nf - fr0, vi, q, clip_l, clip_r, pk_l,  \
+                                                       pk_r, w, tro_lane, pq);                                \
+        else icw_mono_passes<TRIG, SIGV, RP, false>(a, P, s, tt + fr0, nf - fr0, vi, q, clip_l, clip_r, pk_l,    \
+                                                    pk_r, w, tro_lane, pq);                                   \
+    } while (0)
         if (!rowp) {
             ICW_MONO(0, false);
         } else if constexpr (TRIG) {
