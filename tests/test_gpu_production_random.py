@@ -16,6 +16,7 @@ Paths: "k2" (3 streams, the quadrature IIR, K2's frame graph), "kf2" (the FIR co
 graph, order 254, beta 8: KF2 with its render-only passes), "k5" (one stream, one launch per call: the
 drop-in's K5).  FIR parity is unpinned: its oracle is the design's own restatement."""
 import ctypes as C
+import os
 
 import numpy as np
 import pytest
@@ -26,7 +27,7 @@ from tests.test_gpu_graph_random import counter_start
 
 pytestmark = pytest.mark.gpu
 
-SEEDS = 64                      # per generator and path
+SEEDS = int(os.environ.get("ICW_RANDOM_SEEDS", 64))   # per generator and path (a multiple of BATCH)
 BATCH = 8
 FIR_ORDER, FIR_BETA = 254, 8.0
 CALLS = {"k2": (1500, 2117), "kf2": (2560, 3190), "k5": (576, 1900)}
