@@ -7,6 +7,8 @@ The Shift / PM factors are glibc-identical on the device (icw_libm.h), so no cas
 tolerance.  Some cases start the frame counter a few hundred frames below the scaled-mode wrap
 (fs * 1000) or far out in exact mode, with all streams in step (the per-frame rotation table)
 or each at its own counter (K2's inline factors / the serial graph kernel)."""
+import os
+
 import numpy as np
 import pytest
 
@@ -15,7 +17,7 @@ from tests import graphgen
 
 pytestmark = pytest.mark.gpu
 
-N_CASES = 240
+N_CASES = int(os.environ.get("ICW_RANDOM_CASES", 240))   # a multiple of BATCH (wider sweeps: the env)
 BATCH = 24
 N_STREAMS = 3
 CALLS = (317, 400)          # two calls: state carried across a call boundary

@@ -8,6 +8,8 @@ full scale (clips; the next block runs exact and re-arms), inputs hovering at th
 an infinity in float input, for FIR shapers of every tap count, the flat shaper with dither, the IIR
 shaper (never clamp-free), both quantisers, 16 / 24 bit and reduced sign bits, every dither type.
 Bytes, pre-render doubles and meters equal the oracle's."""
+import os
+
 import numpy as np
 import pytest
 
@@ -16,6 +18,7 @@ from in_cwave_amd import abi, graph
 pytestmark = pytest.mark.gpu
 
 N = 9000
+REPS = int(os.environ.get("ICW_SPEC_REPS", 1))       # inputs per case (wider sweeps: the env)
 
 
 def bursty_f32(n_streams, n, seed, amp):
@@ -68,17 +71,18 @@ RENDERS = [(ns, rt) for ns in (0, 4, 2, 14, 5, 6, 16) for rt in (abi.RENDER_ROUN
            if (ns, rt) != (0, abi.RENDER_ROUND)]
 
 
+@pytest.mark.parametrize("rep", range(REPS))
 @pytest.mark.parametrize("ns,rtype", RENDERS)
 @pytest.mark.parametrize("quantz", [abi.QUANTZ_MID_RISER, abi.QUANTZ_MID_TREAD])
 @pytest.mark.parametrize("b24", [False, True])
-def test_clamp_free_blocks(oracle, icw, monkeypatch, ns, rtype, quantz, b24):
+def test_clamp_free_blocks(oracle, icw, monkeypatch, ns, rtype, quantz, b24, rep):
     monkeypatch.setenv("ICW_RENDER", "row")
     cfg = graph.default_config(48000, fmt=abi.FMT_F32, need24bits=b24)
     cfg.render.render_type = rtype
     cfg.render.nshape_type = ns
     cfg.render.quantz_type = quantz
     nodes = [graph.master(gain=1.0, tout=abi.S_RE)]          # the I channel: the input, delayed
-    raw = bursty_f32(6, N, seed=ns * 100 + rtype * 10 + quantz * 2 + b24, amp=(0.2, 0.6, 0.93, 0.99))
+    raw = bursty_f32(6, N, seed=ns * 100 + rtype * 10 + quantz * 2 + b24 + 100003 * rep, amp=(0.2, 0.6, 0.93, 0.99))
     run(oracle, icw, cfg, nodes, raw, N, blocks=(4007, N - 4007))
 
 
