@@ -1842,9 +1842,8 @@ __global__ __launch_bounds__(ICW_K2_TILE, ICW_K2_MINWG) void icw_output(IcwK2Arg
 /* Fused FIR converter + graph + render (KF2): one workgroup per stream and 1024-frame tile (2048
  * for mono).  Wave w owns frames [256 w, 256 w + 256) of the tile: lanes 0-31 sum channel L's
  * outputs and lanes 32-63 channel R's, 8 consecutive frames each (icw_fir_sums).  A lane pair
- * (l, l + 32) then swaps half of its Q values (v_permlane32_swap) and reads both channels' I values
- * from the staged inputs, so lane l holds both channels of frames 0-3 of its eight and lane l + 32
- * of frames 4-7, and each takes its 4 frames straight
+ * (l, l + 32) then swaps half of its I / Q values (v_permlane32_swap), so lane l holds both channels
+ * of frames 0-3 of its eight and lane l + 32 of frames 4-7, and each takes its 4 frames straight
  * through K2's per-frame code (icw_frame_graph: DSP list, pre-render, ROUND render, meters).  The
  * analytic signal never leaves the registers (KF + K2 move 32 B per frame through HBM twice); the
  * sums are KF's, in the same order, so the results are KF + K2's bit for bit.  Dynamic LDS: the
@@ -1958,20 +1957,8 @@ __global__ __launch_bounds__(256, ICW_FIR_OCC) void icw_fir_graph(IcwFirArgs f, 
     icw_fir_sums(lds + ch * px, gs, f.nt, ll, av, sh, c, q);
 #endif
     const int ix = 8 * av + 1;                               /* logical index of x[tt - c] */
-    if constexpr (NC == 2) {
-        /* the I values of the four frames this lane takes through the graph (lane l: frames 0-3 of
-         * its eight, lane l + 32: frames 4-7), both channels straight from the staged inputs: vi[j] L,
-         * vi[j + 4] R of frame h + j -- only the sums' Q values need the lane exchange */
-        const int h = ch ? 4 : 0;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            vi[j] = lds[icw_fir_phys(ICW_FIR_R * ll + h + j + ix)];
-            vi[j + 4] = lds[px + icw_fir_phys(ICW_FIR_R * ll + h + j + ix)];
-        }
-    } else {
-#pragma unroll
-        for (int r = 0; r < ICW_FIR_R; ++r) vi[r] = lds[icw_fir_phys(ICW_FIR_R * ll + r + ix)];
-    }
+    for (int r = 0; r < ICW_FIR_R; ++r) vi[r] = lds[ch * px + icw_fir_phys(ICW_FIR_R * ll + r + ix)];
 #if ICW_FIR_STAMPS
     if (threadIdx.x == 0 && q[0] + vi[0] == 1.2345e300) icw_fir_stp[0] = 1;     /* the sums before stamp 4 */
 #endif
@@ -2025,8 +2012,8 @@ __global__ __launch_bounds__(256, ICW_FIR_OCC) void icw_fir_graph(IcwFirArgs f, 
 #pragma unroll
                 for (int j = 0; j < 2; ++j) {
                     const int r = hh + j;
-                    const double xl = vi[r], xr = vi[r + 4];
-                    double yl = q[r], yr = q[r + 4];
+                    double xl = vi[r], xr = vi[r + 4], yl = q[r], yr = q[r + 4];
+                    icw_swap32(xl, xr);
                     icw_swap32(yl, yr);
                     in2[j].lre = xl; in2[j].lim = yl; in2[j].rre = xr; in2[j].rim = yr;
                 }
@@ -2043,8 +2030,8 @@ __global__ __launch_bounds__(256, ICW_FIR_OCC) void icw_fir_graph(IcwFirArgs f, 
         } else {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-            const double xl = vi[r], xr = vi[r + 4];
-            double yl = q[r], yr = q[r + 4];
+            double xl = vi[r], xr = vi[r + 4], yl = q[r], yr = q[r + 4];
+            icw_swap32(xl, xr);
             icw_swap32(yl, yr);
             const int fr = fr0 + r;
             dv[r][0] = dv[r][1] = 0;
