@@ -193,10 +193,16 @@ struct IcwK3Args {
     unsigned long long *peak_bits; /* [n_streams][2] */
     int32_t n_gen, mt_pitch;
     IcwRenderK rk;
-    double *dith;                  /* [T][dith_pitch] rnd * dth_mul per sample, time-major (K3a -> K3b); null: ROUND */
+    double *dith;                  /* rnd * dth_mul per sample (K3a -> the render); null: ROUND.  dith_gm 0:
+                                      time-major [T][dith_pitch] (K3b, K3f: a lane per channel reads one
+                                      row coalesced); 1: generator-major [n_gen][dith_pitch] (K3r and the
+                                      frame-parallel renders read runs of one channel; K3a writes 512-byte runs) */
     size_t dith_pitch;
     uint32_t *fes;                 /* FP_CHECK census, as in IcwK1Args; null: no FC() */
     int32_t row;                   /* render kernel: 1 row broadcast (K3r, small batches), 0 lane per channel */
+    int32_t dith_gm;               /* layout of dith (above) */
+    int32_t comp;                  /* K3r: 1 with a companion wave (staging and flush off the chain's wave) */
+    int32_t *err;                  /* nonzero after a companion hand-off that never came (never in a healthy run) */
 };
 
 /* Arguments of the output kernel (frame-parallel: Kahan output sums, unmix, graph, render). */

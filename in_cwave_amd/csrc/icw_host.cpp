@@ -207,6 +207,7 @@ struct icw_ctx {
     int k1_mode = -1;         /* K1 variant: -1 auto (row / plain), 0 plain lanes, 3 row broadcast
                                  (ICW_K1_MODE=plain|row, A/B runs) */
     bool dither_lane = false; /* ICW_DITHER=lane: lane-per-channel dither generator (A/B only) */
+    bool k3r_comp = true;     /* ICW_K3R_COMP=0: the row render without its companion wave (K3r, A/B) */
     int render_row = -1;      /* serial render kernel: -1 auto (row broadcast for <= kRowRenderMax
                                  channels), 0 lane per channel, 1 row (ICW_RENDER=serial|row) */
     bool serialize = false;   /* ICW_SERIALIZE=1: every kernel on the caller's stream (profiling) */
@@ -1054,6 +1055,8 @@ int icw_create(const icw_config *cfg, const icw_node *nodes, int n_nodes, int n_
         if (rr && !strcmp(rr, "row")) c->render_row = 1;
         const char *d = getenv("ICW_DITHER");
         c->dither_lane = d && !strcmp(d, "lane");
+        const char *kc = getenv("ICW_K3R_COMP");
+        if (kc && !strcmp(kc, "0")) c->k3r_comp = false;
         const char *z = getenv("ICW_SERIALIZE");
         c->serialize = z && !strcmp(z, "1");
         const char *cs = getenv("ICW_CU_SPLIT");
@@ -1673,7 +1676,7 @@ int icw_process_streams(icw_ctx *c, int first, int count, const void *in, size_t
     const bool dither = c->serial_render && cfg.render.render_type != ICW_RENDER_ROUND;
     if (dither)
         for (int p = 0; p < n_sets; ++p)
-            if (grow((void **)&c->dith[p], &c->dith_bytes[p], S * 2 * (size_t)Tb * sizeof(double))) return ICW_ENOMEM;
+            if (grow((void **)&c->dith[p], &c->dith_bytes[p], S * 2 * (size_t)(Tb + 1) * sizeof(double))) return ICW_ENOMEM;
 
     /* Streams.  sK runs the IIR state kernel K1 (the serial, issue-bound one); sA runs the input
      * prep K0, the output kernel K2 and the serial graph / render; sD the dither generator.  When
@@ -2081,10 +2084,15 @@ int icw_process_streams(icw_ctx *c, int first, int count, const void *in, size_t
             /* the row-broadcast render (16 lanes per channel) while its waves stay few; FP_CHECK
              * keeps the compact lane-per-channel form */
             a3.row = !fcm && (c->render_row == 1 || (c->render_row < 0 && a3.n_gen <= kRowRenderMax)) ? 1 : 0;
+            a3.comp = a3.row && c->k3r_comp;
+            a3.err = ds.err;
             if (dither) {
                 /* K3a for this block on its own stream: dith[p] was last read by K3b of block b-2 */
                 a3.dith = c->dith[p];
-                a3.dith_pitch = (size_t)count * 2;    /* time-major [T][count*2] */
+                /* the row render reads runs of one channel: generator-major [count*2][T rounded up to
+                 * even] (16-byte pairs); the lane-per-channel renders time-major [T][count*2] */
+                a3.dith_gm = a3.row;
+                a3.dith_pitch = a3.row ? (size_t)(T + (T & 1)) : (size_t)count * 2;
                 if (b >= n_sets && sD != sR && hipStreamWaitEvent(sD, c->k3done[p], 0) != hipSuccess) return ICW_EDEVICE;
                 const hipError_t ed = c->dither_lane ? icw_launch_dither_lane(&a3, sD) : icw_launch_dither(&a3, sD);
                 if (ed != hipSuccess || hipEventRecord(c->ditdone[p], sD) != hipSuccess ||

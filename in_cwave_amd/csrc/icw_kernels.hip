@@ -2585,8 +2585,9 @@ __global__ __launch_bounds__(64) void icw_dither_gen(IcwK3Args a)
     double *rs = a.rs + (size_t)g * ICW_RSTATE;
     double prev_rnd = rs[0];
     const double dth_mul = a.rk.dth_mul;
-    double *dd = a.dith + g;            /* time-major [t][dith_pitch]: one store per sample is coalesced */
-    const size_t dp = a.dith_pitch;
+    /* time-major [t][dith_pitch]: one store per sample is coalesced; generator-major: a lane's own run */
+    double *dd = a.dith_gm ? a.dith + (size_t)g * a.dith_pitch : a.dith + g;
+    const size_t dp = a.dith_gm ? 1 : a.dith_pitch;
     const int T = a.T;
     int t = 0;
     while (t < T) {
@@ -2691,8 +2692,10 @@ __global__ __launch_bounds__(64) void icw_dither_coop(IcwK3Args a)
     double *rs = a.rs + (size_t)g * ICW_RSTATE;
     double prev_rnd = rs[0];
     const double dth_mul = a.rk.dth_mul;
-    double *dd = a.dith + g;
-    const size_t dp = a.dith_pitch;
+    /* generator-major (dith_gm): the wave's samples of a window are one contiguous run, each store
+     * instruction writes 64 consecutive doubles; time-major: one double per row (K3b's layout) */
+    double *dd = a.dith_gm ? a.dith + (size_t)g * a.dith_pitch : a.dith + g;
+    const size_t dp = a.dith_gm ? 1 : a.dith_pitch;
     const int T = a.T;
     int t = 0, k = 0, c = 0;               /* samples done, carried values, carried word (0/1) */
     uint32_t cword = 0;
@@ -3015,7 +3018,7 @@ struct IcwRowNs {
 template <int KIND, int NN, int R, int J, bool MR, bool FAST>
 __device__ __forceinline__ void icw_rrow_step(double xs, double d, double &prev_err, double (&E)[R], double (&O)[R],
                                               double (&P)[R], double (&P2)[R], const IcwRowNs &c,
-                                              const IcwRenderK &k, double *qst, double &qh)
+                                              const IcwRenderK &k, double *qst, double &qh, double &mq)
 {
     constexpr int S = J % R;
     const double input = xs - prev_err;                /* xs = x * norm_mul, formed in the staging */
@@ -3032,8 +3035,12 @@ __device__ __forceinline__ void icw_rrow_step(double xs, double d, double &prev_
      * clamp-free block (FAST, icw_render_row) has lo < q < hi for every sample, where the reference's
      * clip stage changes nothing and trunc(q) is already in [lo + 1, hi - 1] */
     double vd;
-    if constexpr (FAST) vd = __builtin_trunc(q) + dd;
-    else vd = __builtin_trunc(fmax(fmin(q, k.hi - 1.0), k.lo + 1.0)) + dd;
+    if constexpr (FAST) {
+        vd = __builtin_trunc(q) + dd;
+    } else {
+        vd = __builtin_trunc(fmax(fmin(q, k.hi - 1.0), k.lo + 1.0)) + dd;
+        mq = icw_vmax_abs(mq, q);       /* the block's largest |q| (icw_render_rowc's calm test; unused otherwise) */
+    }
     if constexpr (J & 1) *(double2 *)(qst + (J >> 1) * 32) = make_double2(qh, q);   /* the integer is the flush's */
     else qh = q;
     const double ev = vd - input;
@@ -3065,20 +3072,20 @@ template <int KIND, int NN, int R, int J, bool MR, bool FAST>
 __device__ __forceinline__ void icw_rrow_block(double (&xin)[ICW_MAX_NS_TAPS], double (&dv)[ICW_MAX_NS_TAPS],
                                                double &prev_err, double (&E)[R], double (&O)[R], double (&P)[R],
                                                double (&P2)[R], const IcwRowNs &c, const IcwRenderK &k, double *qst,
-                                               const double *xn, const double *dn)
+                                               const double *xn, const double *dn, double &mq)
 {
     if constexpr (J < ICW_MAX_NS_TAPS) {
         /* the next block's samples J, J + 1 by one ds_read_b128 each for x and d (16-byte aligned rows) */
         double qh;
-        icw_rrow_step<KIND, NN, R, J, MR, FAST>(xin[J], dv[J], prev_err, E, O, P, P2, c, k, qst, qh);
-        icw_rrow_step<KIND, NN, R, J + 1, MR, FAST>(xin[J + 1], dv[J + 1], prev_err, E, O, P, P2, c, k, qst, qh);
+        icw_rrow_step<KIND, NN, R, J, MR, FAST>(xin[J], dv[J], prev_err, E, O, P, P2, c, k, qst, qh, mq);
+        icw_rrow_step<KIND, NN, R, J + 1, MR, FAST>(xin[J + 1], dv[J + 1], prev_err, E, O, P, P2, c, k, qst, qh, mq);
         /* after both steps, so the 16 bytes land in the pair's own registers (no moves) */
         const double2 x2 = *(const double2 *)(xn + J), d2 = *(const double2 *)(dn + J);
         xin[J] = x2.x;
         xin[J + 1] = x2.y;
         dv[J] = d2.x;
         dv[J + 1] = d2.y;
-        icw_rrow_block<KIND, NN, R, J + 2, MR, FAST>(xin, dv, prev_err, E, O, P, P2, c, k, qst, xn, dn);
+        icw_rrow_block<KIND, NN, R, J + 2, MR, FAST>(xin, dv, prev_err, E, O, P, P2, c, k, qst, xn, dn, mq);
     }
 }
 
@@ -3086,15 +3093,15 @@ template <int KIND, int NN, int R, int J, bool MR>
 __device__ __forceinline__ void icw_rrow_block_lim(const double (&xin)[ICW_MAX_NS_TAPS], const double (&dv)[ICW_MAX_NS_TAPS],
                                                    double &prev_err, double (&E)[R], double (&O)[R], double (&P)[R],
                                                    double (&P2)[R], const IcwRowNs &c, const IcwRenderK &k, double *qst,
-                                                   int lim)
+                                                   int lim, double &mq)
 {
     if constexpr (J < ICW_MAX_NS_TAPS) {
         if (J < lim) {
             double qh;
-            icw_rrow_step<KIND, NN, R, J, MR, false>(xin[J], dv[J], prev_err, E, O, P, P2, c, k, qst, qh);
+            icw_rrow_step<KIND, NN, R, J, MR, false>(xin[J], dv[J], prev_err, E, O, P, P2, c, k, qst, qh, mq);
             if (J + 1 < lim) {
-                icw_rrow_step<KIND, NN, R, J + 1, MR, false>(xin[J + 1], dv[J + 1], prev_err, E, O, P, P2, c, k, qst, qh);
-                icw_rrow_block_lim<KIND, NN, R, J + 2, MR>(xin, dv, prev_err, E, O, P, P2, c, k, qst, lim);
+                icw_rrow_step<KIND, NN, R, J + 1, MR, false>(xin[J + 1], dv[J + 1], prev_err, E, O, P, P2, c, k, qst, qh, mq);
+                icw_rrow_block_lim<KIND, NN, R, J + 2, MR>(xin, dv, prev_err, E, O, P, P2, c, k, qst, lim, mq);
             } else {
                 qst[(J >> 1) * 32] = qh;                 /* the last sample, an even one, alone */
             }
@@ -3117,11 +3124,14 @@ struct IcwRowStage {
  * loads at all, and its LDS offsets inside one buffer (the buffer's own offset is a scalar) */
 struct IcwRowLane {
     const double *xp, *dp;
-    int xi, di;
+    size_t dstr;                 /* dither elements per frame: dith_pitch (time-major) or 1 (generator-major) */
+    int xi, di, di1;             /* frame of the x pair; frames of the dither pair's two values */
     bool xv, dvv;
-    uint32_t xo, dof;
+    uint32_t xo, dof, d2;        /* LDS byte offsets of the x pair and the dither pair; d2 the second value's in doubles */
 };
 
+/* dither values, 40 lanes x 16 bytes: time-major, lane 2i + h loads channels 2h, 2h + 1 at frame i (LDS rows
+ * 2h, 2h + 1); generator-major (dith_gm), lane 10c + p loads frames 2p, 2p + 1 of channel c (LDS row c) */
 __device__ __forceinline__ IcwRowLane icw_rrow_lane(const IcwK3Args &a, int lane)
 {
     constexpr int U = ICW_MAX_NS_TAPS;
@@ -3131,12 +3141,26 @@ __device__ __forceinline__ IcwRowLane icw_rrow_lane(const IcwK3Args &a, int lane
     L.xi = i;
     L.xv = i < U && 2 * s < a.n_gen;
     L.xp = L.xv ? a.pre + (size_t)s * a.pre_stride + (size_t)i * 2 : a.pre;
-    const int tt = lane >> 1, h = lane & 1;
-    L.di = tt;
-    L.dvv = a.dith && lane < 2 * U && (int)blockIdx.x * 4 + 2 * h < a.n_gen;
-    L.dp = L.dvv ? a.dith + (size_t)tt * a.dith_pitch + blockIdx.x * 4 + 2 * h : a.dith;
     L.xo = (uint32_t)(((2 * sb) * U + (i < U ? i : 0)) * sizeof(double));
-    L.dof = (uint32_t)(((2 * h) * U + (lane < 2 * U ? tt : 0)) * sizeof(double));
+    const int ld = lane < 2 * U ? lane : 0;
+    if (a.dith_gm) {
+        const int ch = ld / (U / 2), p = ld % (U / 2);
+        L.di = 2 * p;
+        L.di1 = 2 * p + 1;
+        L.dvv = a.dith && lane < 2 * U && (int)blockIdx.x * 4 + ch < a.n_gen;
+        L.dp = L.dvv ? a.dith + (size_t)(blockIdx.x * 4 + ch) * a.dith_pitch + 2 * p : a.dith;
+        L.dstr = 1;
+        L.dof = (uint32_t)((ch * U + 2 * p) * sizeof(double));
+        L.d2 = 1;
+    } else {
+        const int tt = ld >> 1, h = ld & 1;
+        L.di = L.di1 = tt;
+        L.dvv = a.dith && lane < 2 * U && (int)blockIdx.x * 4 + 2 * h < a.n_gen;
+        L.dp = L.dvv ? a.dith + (size_t)tt * a.dith_pitch + blockIdx.x * 4 + 2 * h : a.dith;
+        L.dstr = a.dith_pitch;
+        L.dof = (uint32_t)(((2 * h) * U + tt) * sizeof(double));
+        L.d2 = U;
+    }
     return L;
 }
 
@@ -3148,7 +3172,8 @@ __device__ __forceinline__ void icw_rrow_stage_load(const IcwK3Args &a, const Ic
     st.x = make_double2(0.0, 0.0);
     st.d = make_double2(0.0, 0.0);
     if (L.xv && t0 + L.xi < a.T) st.x = *(const double2 *)(L.xp + (size_t)t0 * 2);
-    if (L.dvv && t0 + L.di < a.T) st.d = *(const double2 *)(L.dp + (size_t)t0 * a.dith_pitch);
+    if (L.dvv && t0 + L.di1 < a.T) st.d = *(const double2 *)(L.dp + (size_t)t0 * L.dstr);
+    else if (L.dvv && t0 + L.di < a.T) st.d.x = L.dp[(size_t)t0 * L.dstr];   /* generator-major: the last, odd frame */
 }
 
 /* The inputs go to LDS as x * norm_mul (sound_render.c:754's product, formed here lane-parallel: two
@@ -3172,7 +3197,7 @@ __device__ __forceinline__ bool icw_rrow_stage_store(double (*xs)[ICW_MAX_NS_TAP
     if (lane < 2 * U) {
         double *p = (double *)((char *)&ds[0][0] + L.dof);
         p[0] = st.d.x;
-        p[U] = st.d.y;
+        p[L.d2] = st.d.y;
     }
     return __all(ok);
 }
@@ -3348,6 +3373,7 @@ __global__ __launch_bounds__(64) void icw_render_row(IcwK3Args a)
      * every block paid ~80 AGPR / VGPR moves for it (more than the clamp it saved). */
     bool calm = false;
     int t = 0, kb = 0;
+    double mq_unused = 0.0;             /* this kernel's calm test is the flush's */
     /* one block of either form, the staging of block kb + 2 (into the buffer block kb has left), the
      * block's flush, and block kb + 3 on its way.  The staging comes before the flush: its stores to
      * LDS wait for the registers loaded one block ago, and on gfx950 that wait (vmcnt) also counts
@@ -3358,7 +3384,7 @@ __global__ __launch_bounds__(64) void icw_render_row(IcwK3Args a)
         const int nb = (kb + 1) & 1;
         unsigned char *ot0 = oA ? oA + (size_t)t * 2 * osz : nullptr, *ot1 = oB ? oB + (size_t)t * 2 * osz : nullptr;
         icw_rrow_block<KIND, NN, R, 0, MR, FAST>(xin, dv, prev_err, E, O, P, P2, c, k, qst, &xsl[nb][r][0],
-                                                 &dsl[nb][r][0]);
+                                                 &dsl[nb][r][0], mq_unused);
         x_ok0 = x_ok1;
         x_ok1 = icw_rrow_stage_store(xsl[kb & 1], dsl[kb & 1], lane, sl, stg, nm, thr);
         if constexpr (FAST) {
@@ -3382,7 +3408,7 @@ __global__ __launch_bounds__(64) void icw_render_row(IcwK3Args a)
     }
     const int rem = T - t;
     if (rem > 0) {
-        icw_rrow_block_lim<KIND, NN, R, 0, MR>(xin, dv, prev_err, E, O, P, P2, c, k, qst, rem);
+        icw_rrow_block_lim<KIND, NN, R, 0, MR>(xin, dv, prev_err, E, O, P, P2, c, k, qst, rem, mq_unused);
         icw_rrow_flush<MR>(qs, r, lr, lane, rem, k, clips, pk, oA ? oA + (size_t)t * 2 * osz : nullptr,
                            oB ? oB + (size_t)t * 2 * osz : nullptr, osz);
         /* back to the block-start mapping: rotate left by rem mod R */
@@ -3402,6 +3428,320 @@ __global__ __launch_bounds__(64) void icw_render_row(IcwK3Args a)
     for (int i = 0; i < R; ++i) { rs[2 + i] = E[(R - 1 - i) % R]; rs[2 + U + i] = O[(R - 1 - i) % R]; }
     if (clips) atomicAdd(&a.clips[g], clips);
     if (pk > 0.0) atomicMax(&a.peak_bits[g], (unsigned long long)__double_as_longlong(pk));
+}
+
+/* ------------------------------------------- render, row broadcast + companion wave (K3c) ------ */
+/* icw_render_row with everything that is not the error-feedback chain moved to a second wave of the
+ * workgroup, which the dispatcher puts on another SIMD of the CU.  A lone wave issues one FP64 op per
+ * ~5 cycles, so in K3r every staging load, LDS store, integer conversion, meter update and
+ * output store was issue time taken from the chain: 18.9 VALU + 2.5 SALU + 1.8 LDS per sample for a
+ * 16-op chain (MEW44).  Here
+ *   wave 0 (chain)      runs only the chain of sound_render.c:754-809 on its four channels: per sample
+ *                       the row-uniform chain, one ds_read_b128 per two samples for x and for the
+ *                       dither value (the next block, staged), one ds_write_b128 per two samples for q;
+ *                       per block one counter read and one counter write;
+ *   wave 1 (companion)  stages block n (global loads issued four blocks ahead, x * norm_mul, the
+ *                       clamp-free input test) into staging buffer n mod 4 and publishes `staged`;
+ *                       flushes block n - 4 once the chain has published it `done` (the exact flush of
+ *                       icw_rrow_flush: integers, clips, peak, packed frames) and publishes `flushed`.
+ * The hand-offs are LDS counters.  The LDS executes one wave's DS instructions in order, so a counter
+ * written after a block's data is seen only once the data is there; the compiler is kept from
+ * moving memory accesses across a counter access by a fence of its own.  The chain checks, at each
+ * block start, the counters it read at the previous one (the companion runs a block ahead), so the
+ * check costs no wait; it spins (s_sleep) only if the companion fell behind.  Every spin is bounded:
+ * a hand-off that never comes flags a.err and the wave goes on, so the grid drains.
+ * The clamp-free decision needs the block before to have been calm (no |q| >= clip_abs, no NaN):
+ * the chain itself keeps max |q| in an exact block (one v_max_f64 per sample, only there); a NaN q
+ * makes the chain's error, and so prev_ns_err, NaN for good (the shaper's sum of a NaN), which the
+ * block-end test also sees; a FIR shaper's NaN is never self-clearing, a flat one has no history.
+ * Results are icw_render_row's bit for bit: the same chain code, the same exact flush for every
+ * block (a clamp-free block gives the same integers through it: no clip, no NaN). */
+#define ICW_K3C_NSB 4                  /* staging buffers (blocks) */
+#define ICW_K3C_NQB 4                  /* q buffers (blocks) */
+#define ICW_K3C_SPIN (1u << 24)        /* spin bound: ~2^24 s_sleep(1), far beyond any healthy wait */
+
+__device__ __forceinline__ void icw_cfence() { asm volatile("" ::: "memory"); }
+
+__device__ __forceinline__ unsigned long long icw_lds_ld64(const unsigned long long *p)
+{
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+__device__ __forceinline__ int icw_lds_ld32(const int *p)
+{
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+__device__ __forceinline__ void icw_lds_st32(int *p, int v)
+{
+    icw_cfence();
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+/* chain side: the counters (staged word | flushed << 32) once staged >= ns and flushed >= nf.  The
+ * staged word is (blocks staged) << 4 | the clamp-free input tests of the last four staged blocks (bit
+ * n mod 4 for block n), so one 64-bit read per block brings the chain both counters and block j + 1's
+ * test (inline, as every hand-off here: a call would make the callee wait for all memory traffic) */
+__device__ __forceinline__ unsigned long long icw_k3c_wait(const unsigned long long *sf, int ns, int nf, int32_t *err)
+{
+    unsigned long long v = icw_lds_ld64(sf);
+    for (unsigned spin = 0;; ++spin) {
+        const int st = __builtin_amdgcn_readfirstlane((int)(uint32_t)v) >> 4;
+        const int fl = __builtin_amdgcn_readfirstlane((int)(uint32_t)(v >> 32));
+        if (st >= ns && fl >= nf) break;
+        if (spin >= ICW_K3C_SPIN) {
+            if (err && threadIdx.x == 0) atomicOr(err, 1);
+            break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+        v = icw_lds_ld64(sf);
+    }
+    icw_cfence();
+    return v;
+}
+
+/* companion side: wait until the chain has published at least n blocks done */
+__device__ __forceinline__ void icw_k3c_wait_done(const int *dn, int n, int32_t *err)
+{
+    for (unsigned spin = 0; __builtin_amdgcn_readfirstlane(icw_lds_ld32(dn)) < n; ++spin) {
+        if (spin >= ICW_K3C_SPIN) {
+            if (err && threadIdx.x == 64) atomicOr(err, 1);
+            break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+    }
+    icw_cfence();
+}
+
+/* The companion's staging (generator-major dither rows).  Loads are issued by every lane from a
+ * clamped, always valid address (the frame index held to T - 1, a spare lane on its row's first frame)
+ * and the values a lane has no business loading are zeroed only at the store, four blocks later: a load
+ * under a branch, or a select right after it, made the compiler wait for all memory traffic
+ * (vmcnt(0)) every block.  A dither pair starting at the block's last, even frame reads the row's
+ * padding (dith_pitch is T rounded up to even). */
+struct IcwCompLane {
+    const double *xr, *dr;       /* the lane's x row and dither row (frame 0; a spare lane: row 0 of the batch) */
+    int xi, di;                  /* frame offsets in a block: x frame, first frame of the dither pair */
+    bool xv, dvv;
+    uint32_t xo, dof;            /* LDS byte offsets in a staging buffer */
+};
+
+__device__ __forceinline__ IcwCompLane icw_k3c_lane(const IcwK3Args &a, int lane)
+{
+    constexpr int U = ICW_MAX_NS_TAPS;
+    IcwCompLane L;
+    const int sb = lane >> 5, i = lane & 31;
+    const int s = blockIdx.x * 2 + sb;
+    L.xi = i < U ? i : 0;
+    L.xv = i < U && 2 * s < a.n_gen;
+    L.xr = L.xv ? a.pre + (size_t)s * a.pre_stride : a.pre;
+    L.xo = (uint32_t)(((2 * sb) * U + L.xi) * sizeof(double));
+    const int ld = lane < 2 * U ? lane : 0;
+    const int ch = ld / (U / 2), p = ld % (U / 2);
+    L.di = 2 * p;
+    L.dvv = a.dith && lane < 2 * U && (int)blockIdx.x * 4 + ch < a.n_gen;
+    L.dr = L.dvv ? a.dith + (size_t)(blockIdx.x * 4 + ch) * a.dith_pitch : a.pre;
+    L.dof = (uint32_t)((ch * U + 2 * p) * sizeof(double));
+    return L;
+}
+
+__device__ __forceinline__ void icw_k3c_stage_load(const IcwK3Args &a, const IcwCompLane &L, int t0, IcwRowStage &st)
+{
+    const int T1 = a.T - 1;
+    const int fx = t0 + L.xi < T1 ? t0 + L.xi : T1;
+    const int fd = t0 + L.di < T1 ? t0 + L.di : (T1 & ~1);
+    st.x = *(const double2 *)(L.xr + (size_t)fx * 2);
+    st.d = *(const double2 *)(L.dr + fd);
+}
+
+/* block t0's values to staging buffer (xs, ds); returns, wave-uniform, the clamp-free input test.
+ * Branch-free: the lanes without a slot store into dum (a scratch area of 64 x 32 bytes), so every
+ * loaded register is consumed on every path (a skipped store left its pending load's register free for
+ * reuse, and the write to it waited for all memory traffic). */
+__device__ __forceinline__ bool icw_k3c_stage_store(double (*xs)[ICW_MAX_NS_TAPS], double (*ds)[ICW_MAX_NS_TAPS], double *dum,
+                                                    int lane, const IcwCompLane &L, const IcwRowStage &st, int t0, int T,
+                                                    double nm, double thr)
+{
+    constexpr int U = ICW_MAX_NS_TAPS;
+    const bool xl = (lane & 31) < U, dl = lane < 2 * U;
+    const bool v = L.xv && t0 + L.xi < T;
+    const double a = (v ? st.x.x : 0.0) * nm, b = (v ? st.x.y : 0.0) * nm;
+    double *px = xl ? (double *)((char *)&xs[0][0] + L.xo) : dum + lane * 4;
+    px[0] = a;
+    px[xl ? U : 1] = b;
+    const bool ok = !xl || (fabs(a) <= thr && fabs(b) <= thr);
+    const bool v0 = L.dvv && t0 + L.di < T, v1 = L.dvv && t0 + L.di + 1 < T;
+    double *pd = dl ? (double *)((char *)&ds[0][0] + L.dof) : dum + lane * 4 + 2;
+    *(double2 *)pd = make_double2(v0 ? st.d.x : 0.0, v1 ? st.d.y : 0.0);
+    return __all(ok);
+}
+
+template <int KIND, int NN, bool MR>
+__global__ __launch_bounds__(128) void icw_render_rowc(IcwK3Args a)
+{
+    constexpr int U = ICW_MAX_NS_TAPS, NSB = ICW_K3C_NSB, NQB = ICW_K3C_NQB;
+    constexpr int R = KIND == 1 ? U : (KIND == 2 ? 4 : 1);
+    constexpr int QSTR = 4 * (U / 2) * 16 * 2;          /* doubles per q buffer */
+    static_assert(U % R == 0, "ring period must divide the unroll");
+    static_assert(U % 2 == 0, "samples go in pairs");
+    static_assert(NSB == 4 && NQB == 4, "the companion's schedule below assumes four buffers of each");
+    __shared__ __attribute__((aligned(16))) double qsb[NQB][4][U / 2][16][2];
+    __shared__ __attribute__((aligned(16))) double xsl[NSB][4][U];
+    __shared__ __attribute__((aligned(16))) double dsl[NSB][4][U];
+    __shared__ __attribute__((aligned(8))) int cnt[4];  /* staged word (icw_k3c_wait), flushed, done (blocks) */
+    __shared__ __attribute__((aligned(16))) double dum[64 * 4];   /* the companion's slotless stores */
+    const int T = a.T;
+    if (T <= 0) return;
+    const int nbk = (T + U - 1) / U, nfull = T / U;
+    const IcwRenderK &k = a.rk;
+    const int osz = k.is24 ? 3 : 2;
+    if (threadIdx.x == 0) { cnt[0] = 0; cnt[1] = 0; cnt[2] = 0; cnt[3] = 0; }
+    __syncthreads();
+    const unsigned long long *sfp = (const unsigned long long *)&cnt[0];
+    if (threadIdx.x < 64) {
+        /* ------------------------------------------------------------------ the chain ------ */
+        const int lane = threadIdx.x, r = lane >> 4, lr = lane & 15;
+        const int g0 = blockIdx.x * 4 + r;
+        const bool valid = g0 < a.n_gen;
+        const int g = valid ? g0 : a.n_gen - 1;
+        double *rs = a.rs + (size_t)g * ICW_RSTATE;
+        double prev_err = rs[1];
+        double E[R], O[R], P[R], P2[R];
+        IcwRowNs c;
+        c.one = 1.0;
+        c.c0 = k.ns_c[0];
+        c.cN = KIND == 2 ? k.ns_c[NN] : 0.0;
+        if constexpr (KIND == 2) {
+            c.pl = lr + 1 < NN ? k.ns_c[lr + 1] : 0.0;
+            c.pl2 = lr + 1 < NN ? k.ns_c[lr + 1 + NN] : 0.0;
+        } else {
+            c.pl = lr + 1 < NN ? k.ns_c[lr + 1] : 0.0;
+            c.pl2 = lr + 17 < NN ? k.ns_c[lr + 17] : 0.0;
+        }
+#pragma unroll
+        for (int i = 0; i < R; ++i) {
+            E[(R - 1 - i) % R] = rs[2 + i];
+            O[(R - 1 - i) % R] = rs[2 + U + i];
+        }
+        if constexpr (KIND == 1) {
+#pragma unroll
+            for (int m = 0; m < R; ++m) {
+                P[m] = icw_rmul(c.pl, E[m]);
+                if constexpr (NN > 17) P2[m] = icw_rmul(c.pl2, E[m]);
+            }
+        } else if constexpr (KIND == 2) {
+#pragma unroll
+            for (int m = 0; m < R; ++m) P[m] = icw_rsub(icw_rmul(c.pl, E[m]), icw_rmul(c.pl2, O[(m + R - 1) % R]));
+        }
+        asm volatile("s_nop 1");                       /* VALU write -> DPP read of P / P2 */
+        double *const qst = &qsb[0][r][0][lr][0];
+        /* blocks 0 and 1 staged: block 0 into registers, block 1 is read during block 0 */
+        unsigned long long sf = icw_k3c_wait(sfp, nbk < 2 ? nbk : 2, 0, a.err);
+        double xin[U], dv[U];
+#pragma unroll
+        for (int j = 0; j < U; ++j) {
+            xin[j] = xsl[0][r][j];
+            dv[j] = dsl[0][r][j];
+        }
+        bool okn = (__builtin_amdgcn_readfirstlane((int)(uint32_t)sf) & 1) != 0;   /* block j's clamp-free input test */
+        bool calm = false;                             /* the block before j clipped nowhere (no NaN) */
+        int j = 0;
+        auto step = [&](auto fast) {
+            constexpr bool FAST = decltype(fast)::value;
+            /* the counters read one block ago: block j + 1 staged, block j - NQB flushed */
+            const int ns = j + 2 < nbk ? j + 2 : nbk, nf = j + 1 - NQB;
+            if ((__builtin_amdgcn_readfirstlane((int)(uint32_t)sf) >> 4) < ns ||
+                __builtin_amdgcn_readfirstlane((int)(uint32_t)(sf >> 32)) < nf)
+                sf = icw_k3c_wait(sfp, ns, nf, a.err);
+            icw_cfence();
+            /* for the next block's check, and block j + 1's input test: staged then covers blocks up to
+             * at most j + 3 (the companion stages block n after the chain's block n - 4), j + 1 among its
+             * last four */
+            sf = icw_lds_ld64(sfp);
+            const int nb = (j + 1) & (NSB - 1);
+            double mq = 0.0;
+            icw_rrow_block<KIND, NN, R, 0, MR, FAST>(xin, dv, prev_err, E, O, P, P2, c, k, qst + (j & (NQB - 1)) * QSTR,
+                                                     &xsl[nb][r][0], &dsl[nb][r][0], mq);
+            if constexpr (!FAST) calm = __all(mq < k.clip_abs && prev_err == prev_err);
+            icw_lds_st32(&cnt[2], j + 1);
+            __builtin_amdgcn_sched_barrier(0);         /* the read of sf stays a block ahead of this use */
+            okn = ((__builtin_amdgcn_readfirstlane((int)(uint32_t)sf) >> nb) & 1) != 0;
+            ++j;
+        };
+        while (j < nfull) {
+            while (j < nfull && !(KIND != 2 && calm && okn)) step(icw_ic<0>());
+            if constexpr (KIND != 2) {
+                while (j < nfull && okn) step(icw_ic<1>());
+            }
+        }
+        const int rem = T - nfull * U;
+        if (rem > 0) {
+            const int nf = j + 1 - NQB;
+            if (__builtin_amdgcn_readfirstlane((int)(uint32_t)(sf >> 32)) < nf) sf = icw_k3c_wait(sfp, nbk, nf, a.err);
+            icw_cfence();
+            double mq = 0.0;
+            icw_rrow_block_lim<KIND, NN, R, 0, MR>(xin, dv, prev_err, E, O, P, P2, c, k, qst + (j & (NQB - 1)) * QSTR,
+                                                   rem, mq);
+            icw_lds_st32(&cnt[2], j + 1);
+#pragma unroll
+            for (int q = 1; q < U; ++q)
+                if (q <= rem) { icw_ring_rotate1<R>(E); icw_ring_rotate1<R>(O); }
+        }
+        if (!valid || lr != 0) return;
+        rs[1] = prev_err;
+#pragma unroll
+        for (int i = 0; i < R; ++i) { rs[2 + i] = E[(R - 1 - i) % R]; rs[2 + U + i] = O[(R - 1 - i) % R]; }
+    } else {
+        /* -------------------------------------------------------------- the companion ------ */
+        const int lane = threadIdx.x - 64, r = lane >> 4, lr = lane & 15;
+        const bool valid = (int)blockIdx.x * 4 + r < a.n_gen;
+        const IcwCompLane sl = icw_k3c_lane(a, lane);
+        const double nm = k.norm_mul, thr = k.spec_thr;
+        const int sA = blockIdx.x * 2, sB = sA + 1;
+        unsigned char *oA = 2 * sA < a.n_gen ? a.out + (size_t)sA * a.out_stride : nullptr;
+        unsigned char *oB = 2 * sB < a.n_gen ? a.out + (size_t)sB * a.out_stride : nullptr;
+        unsigned clips = 0;
+        double pk = 0.0;
+        IcwRowStage rg[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) icw_k3c_stage_load(a, sl, i * U, rg[i]);
+        unsigned okm = 0;                              /* clamp-free input tests of the last four staged blocks */
+        /* iteration n: flush block n - 4 (the chain has moved on to n - 3), then stage block n into
+         * buffer n mod 4 (its last reader, block n - 5, is done) and send its registers for block n + 4 */
+        auto iter = [&](int n, IcwRowStage &st) {
+            if (n >= 4 && n - 4 < nbk) {
+                const int jf = n - 4;
+                icw_k3c_wait_done(&cnt[2], jf + 1, a.err);
+                const int t = jf * U, nf = T - t < U ? T - t : U;
+                (void)icw_rrow_flush<MR>(qsb[jf & (NQB - 1)], r, lr, lane, nf, k, clips, pk,
+                                         oA ? oA + (size_t)t * 2 * osz : nullptr, oB ? oB + (size_t)t * 2 * osz : nullptr, osz);
+                icw_lds_st32(&cnt[1], jf + 1);
+            }
+            /* unconditional, past the last block too (zeros into a buffer nobody reads any more, a
+             * staged count past nbk): with the loads under a branch, the compiler's wait for a register
+             * set assumed the path without the later loads and waited for everything */
+            const int b = n & (NSB - 1);
+            const bool ok = icw_k3c_stage_store(xsl[b], dsl[b], dum, lane, sl, st, n * U, T, nm, thr);
+            okm = (okm & ~(1u << b)) | ((ok ? 1u : 0u) << b);
+            icw_lds_st32(&cnt[0], (int)(((unsigned)(n + 1) << 4) | okm));
+            icw_k3c_stage_load(a, sl, (n + 4) * U, st);
+        };
+        for (int n0 = 0; n0 < nbk + 4; n0 += 4) {
+            iter(n0, rg[0]);
+            iter(n0 + 1, rg[1]);
+            iter(n0 + 2, rg[2]);
+            iter(n0 + 3, rg[3]);
+        }
+#pragma unroll
+        for (int off = 1; off < 16; off <<= 1) {
+            clips += __shfl_xor(clips, off);
+            pk = fmax(pk, __shfl_xor(pk, off));
+        }
+        if (!valid || lr != 0) return;
+        const int g = blockIdx.x * 4 + r;
+        if (clips) atomicAdd(&a.clips[g], clips);
+        if (pk > 0.0) atomicMax(&a.peak_bits[g], (unsigned long long)__double_as_longlong(pk));
+    }
 }
 
 /* Render with FP_CHECK (K3f): sound_render_value's WITH FC CHECKS arithmetic (sound_render.c:
@@ -3602,23 +3942,32 @@ extern "C" hipError_t icw_launch_dither_lane(const IcwK3Args *a, hipStream_t st)
     return hipGetLastError();
 }
 
+template <int KIND, int NN, bool MR>
+static void icw_launch_rr(const IcwK3Args *a, int rb, hipStream_t st)
+{
+    /* K3c (a companion wave beside the chain, 128 threads) or K3r (one wave) */
+    if (a->comp) hipLaunchKernelGGL((icw_render_rowc<KIND, NN, MR>), dim3(rb), dim3(128), 0, st, *a);
+    else hipLaunchKernelGGL((icw_render_row<KIND, NN, MR>), dim3(rb), dim3(64), 0, st, *a);
+}
+
 template <bool MR>
 static hipError_t icw_launch_render_row(const IcwK3Args *a, int rb, int nn, hipStream_t st)
 {
+    if (a->comp && a->dith && !a->dith_gm) return hipErrorInvalidValue;   /* K3c stages generator-major rows */
     if (a->rk.ns_kind == 0) {
-        hipLaunchKernelGGL((icw_render_row<0, 0, MR>), dim3(rb), dim3(64), 0, st, *a);
+        icw_launch_rr<0, 0, MR>(a, rb, st);
     } else if (a->rk.ns_kind == 1) {
         switch (nn) {
-        case 5: hipLaunchKernelGGL((icw_render_row<1, 5, MR>), dim3(rb), dim3(64), 0, st, *a); break;
-        case 9: hipLaunchKernelGGL((icw_render_row<1, 9, MR>), dim3(rb), dim3(64), 0, st, *a); break;
-        case 15: hipLaunchKernelGGL((icw_render_row<1, 15, MR>), dim3(rb), dim3(64), 0, st, *a); break;
-        case 16: hipLaunchKernelGGL((icw_render_row<1, 16, MR>), dim3(rb), dim3(64), 0, st, *a); break;
-        case 20: hipLaunchKernelGGL((icw_render_row<1, 20, MR>), dim3(rb), dim3(64), 0, st, *a); break;
+        case 5: icw_launch_rr<1, 5, MR>(a, rb, st); break;
+        case 9: icw_launch_rr<1, 9, MR>(a, rb, st); break;
+        case 15: icw_launch_rr<1, 15, MR>(a, rb, st); break;
+        case 16: icw_launch_rr<1, 16, MR>(a, rb, st); break;
+        case 20: icw_launch_rr<1, 20, MR>(a, rb, st); break;
         default: return hipErrorInvalidValue;
         }
     } else {
         if (nn != 4) return hipErrorInvalidValue;
-        hipLaunchKernelGGL((icw_render_row<2, 4, MR>), dim3(rb), dim3(64), 0, st, *a);
+        icw_launch_rr<2, 4, MR>(a, rb, st);
     }
     return hipGetLastError();
 }
