@@ -126,6 +126,13 @@ def workload_config(w):
     if w["render"] == "tpdf24_mew44":
         cfg.render.render_type = abi.RENDER_TPDF
         cfg.render.nshape_type = abi.NSHAPE_MEW44
+    # ICW_BENCH_RENDER (diagnostics only, never the headline): a dithered render with the flat shaper,
+    # "<rpdf|tpdf|stpdf|gauss>_flat", on the same shape (the frame-parallel dithered render's A/B)
+    rr = os.environ.get("ICW_BENCH_RENDER")
+    if rr:
+        cfg.render.render_type = {"rpdf": abi.RENDER_RPDF, "tpdf": abi.RENDER_TPDF, "stpdf": abi.RENDER_STPDF,
+                                  "gauss": abi.RENDER_GAUSS}[rr.split("_")[0]]
+        cfg.render.nshape_type = abi.NSHAPE_FLAT
     # ICW_BENCH_GRAPH (diagnostics only, never the headline): another of the three lists on the same shape
     g = os.environ.get("ICW_BENCH_GRAPH") or w["graph"]
     nodes = {"shift_master": graph.graph_shift_master, "master_only": graph.graph_master_only,

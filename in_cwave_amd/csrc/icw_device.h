@@ -243,6 +243,10 @@ struct IcwK2Args {
     int32_t zero;                  /* always 0: an offset the compiler cannot fold (keeps loads in a loop) */
     uint32_t *fes;                 /* FP_CHECK census, as in IcwK1Args; null: no FC() */
     int32_t tpw;                   /* tiles per workgroup (1..ICW_K2_TPW), set by the launcher */
+    const double *dith;            /* nullable: a dithered render with the flat shaper, rendered here
+                                      frame-parallel -- K3a's rnd * dth_mul, generator-major
+                                      [n_streams * 2][dith_pitch] (row 2s + ch, frame t of the block) */
+    size_t dith_pitch;
 };
 
 /* Per-frame rotation table (one thread per frame): the Shift / PM factors depend only on the frame

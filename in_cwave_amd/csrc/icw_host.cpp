@@ -200,6 +200,7 @@ struct icw_ctx {
      * fallback (whose out-of-line call cost it scratch spills) */
     std::vector<unsigned long long> nf_host;
     bool serial_render = false;
+    bool render_state = false;            /* needs_render_state: the state blob carries the render words */
     uint32_t mt_seed_state[2][624];       /* seeded MT19937 states for L / R (mtrnd_init_seed) */
     hipStream_t stream = nullptr;
     std::vector<hipEvent_t> ev;
@@ -609,13 +610,31 @@ int build_prog(const icw_config &cfg, std::vector<icw_node> nodes, IcwProg &P)
     return ICW_OK;
 }
 
-/* ROUND + flat is elementwise (rendered inside the output kernel); every other render keeps serial
- * per-channel state and runs in the serial render kernel, and so does every render behind a
- * bus-form graph (frame-serial, hands lOut / rOut over) or with FP_CHECK (the FC() render
- * arithmetic lives in the serial render kernel only) */
+/* A render with the flat shaper is elementwise: ns_empty returns 0.0 (sound_render.c:396-400), so
+ * prev_ns_err stays 0.0 (:800) and sound_render_value (:754-809) is a function of the sample and its
+ * dither term alone.  ROUND draws no dither; RPDF / TPDF / STPDF / GAUSS take theirs from K3a (the
+ * MT19937 stream is serial per channel, the render is not), so all of them render inside the output
+ * kernel, frame-parallel (ICW_DITH_PAR=0: the dithered ones through the serial render, A/B).  A noise
+ * shaper feeds each sample's error into the next: serial per channel, in the serial render kernel --
+ * as is every render behind a bus-form graph (frame-serial, hands lOut / rOut over) or with FP_CHECK
+ * (the FC() render arithmetic lives in the serial render kernel only). */
+bool dith_par_on()
+{
+    static const bool on = !getenv("ICW_DITH_PAR") || atoi(getenv("ICW_DITH_PAR")) != 0;
+    return on;
+}
+
 bool needs_serial(const icw_config &cfg, const IcwRenderK &rk, const IcwProg &P)
 {
-    return !(cfg.render.render_type == ICW_RENDER_ROUND && rk.ns_kind == 0) || P.is_bus || cfg.fp_check;
+    const bool elementwise = rk.ns_kind == 0 && (cfg.render.render_type == ICW_RENDER_ROUND || dith_par_on());
+    return !elementwise || P.is_bus || cfg.fp_check;
+}
+
+/* the per-channel render state (MT19937 words, prev_rnd, shaper rings): a serial render, or a dithered
+ * one rendered frame-parallel (its generator still runs, K3a) */
+bool needs_render_state(const icw_config &cfg, const IcwRenderK &rk, const IcwProg &P)
+{
+    return needs_serial(cfg, rk, P) || cfg.render.render_type != ICW_RENDER_ROUND;
 }
 
 bool render_cfg_ok(const icw_render_cfg &r)
@@ -933,13 +952,14 @@ int apply_graph(icw_ctx *c, std::vector<icw_node> &nv, int bypass, const std::ve
     int rc = build_prog(cfg, nv, P);
     if (rc) return rc;
     if (!c->chain_ok) P.chain = P.sig = 0;
-    const bool serial = needs_serial(cfg, c->rk, P);
-    if (serial && (rc = ensure_render_state(c))) return rc;
+    const bool serial = needs_serial(cfg, c->rk, P), rstate = needs_render_state(cfg, c->rk, P);
+    if (rstate && (rc = ensure_render_state(c))) return rc;
     if (hipMemcpy(c->d_prog, &P, sizeof(IcwProg), hipMemcpyHostToDevice) != hipSuccess) return ICW_EDEVICE;
     c->cfg.bypass_list = cfg.bypass_list;
     c->nodes = nv;
     c->prog = P;
     c->serial_render = serial;
+    c->render_state = rstate;
     for (int slot : clears)
         if (clear_slot(c, slot) != ICW_OK) return ICW_EDEVICE;
     return ICW_OK;
@@ -992,6 +1012,7 @@ int icw_create(const icw_config *cfg, const icw_node *nodes, int n_nodes, int n_
     set_filter(c);
     render_consts(cfg->render, cfg->need24bits, c->rk);
     c->serial_render = needs_serial(*cfg, c->rk, c->prog);
+    c->render_state = needs_render_state(*cfg, c->rk, c->prog);
     for (int ch = 0; ch < 2; ++ch) {
         uint32_t *st = c->mt_seed_state[ch];
         st[0] = ch ? cfg->seed_right : cfg->seed_left;         /* mtrnd_init_seed, mt_jrnd.c:28-47 */
@@ -1011,7 +1032,7 @@ int icw_create(const icw_config *cfg, const icw_node *nodes, int n_nodes, int n_
     rc |= dalloc(&s.clips, S * 2);
     rc |= dalloc(&s.peak_bits, S * 2);
     rc |= dalloc(&s.err, 1);
-    if (c->serial_render) {
+    if (c->render_state) {
         rc |= dalloc(&s.mt, (size_t)624 * S * 2);
         rc |= dalloc(&s.mt_idx, S * 2);
         rc |= dalloc(&s.rs, S * 2 * ICW_RSTATE);
@@ -1057,6 +1078,7 @@ int icw_create(const icw_config *cfg, const icw_node *nodes, int n_nodes, int n_
         c->dither_lane = d && !strcmp(d, "lane");
         const char *kc = getenv("ICW_K3R_COMP");
         if (kc && !strcmp(kc, "0")) c->k3r_comp = false;
+
         const char *z = getenv("ICW_SERIALIZE");
         c->serialize = z && !strcmp(z, "1");
         const char *cs = getenv("ICW_CU_SPLIT");
@@ -1408,9 +1430,9 @@ int icw_set_render(icw_ctx *c, const icw_render_cfg *r)
     render_consts(*r, c->cfg.need24bits, k);
     icw_config cfg = c->cfg;
     cfg.render = *r;
-    const bool serial = needs_serial(cfg, k, c->prog);
+    const bool serial = needs_serial(cfg, k, c->prog), rstate = needs_render_state(cfg, k, c->prog);
     int rc;
-    if (serial && (rc = ensure_render_state(c))) return rc;
+    if (rstate && (rc = ensure_render_state(c))) return rc;
     if (k.hi != c->rk.hi && !fold_peaks(c)) return ICW_EDEVICE;
     /* sound_render_recalc: prev_rnd, the shaper rings and prev_ns_err start again, the RNG goes on */
     if (c->st.rs && hipMemset(c->st.rs, 0, (size_t)c->n_streams * 2 * ICW_RSTATE * sizeof(double)) != hipSuccess)
@@ -1418,6 +1440,7 @@ int icw_set_render(icw_ctx *c, const icw_render_cfg *r)
     c->cfg.render = *r;
     c->rk = k;
     c->serial_render = serial;
+    c->render_state = rstate;
     return ICW_OK;
 }
 
@@ -1436,9 +1459,9 @@ int icw_set_outbits(icw_ctx *c, int need24bits)
     render_consts(c->cfg.render, is24, k);
     icw_config cfg = c->cfg;
     cfg.need24bits = is24;
-    const bool serial = needs_serial(cfg, k, c->prog);
+    const bool serial = needs_serial(cfg, k, c->prog), rstate = needs_render_state(cfg, k, c->prog);
     int rc;
-    if (serial && (rc = ensure_render_state(c))) return rc;
+    if (rstate && (rc = ensure_render_state(c))) return rc;
     /* peaks so far in dB against the old bound (sound_render.c:769-780 converts each sample with the
      * bound of its time) */
     if (k.hi != c->rk.hi && !fold_peaks(c)) return ICW_EDEVICE;
@@ -1447,6 +1470,7 @@ int icw_set_outbits(icw_ctx *c, int need24bits)
     c->cfg.need24bits = is24;
     c->rk = k;
     c->serial_render = serial;
+    c->render_state = rstate;
     return ICW_OK;
 }
 
@@ -1554,7 +1578,11 @@ int icw_process_streams(icw_ctx *c, int first, int count, const void *in, size_t
      * (65 536 -> 16 384 -> 4 096 -> 1 024: the drain stays one short K2) measured +0.8 % on C2
      * (3 170 -> 3 196 Msamples/s; 32 768 with r = 0.5 +0.5 %, 65 536 with no tail +0.5 %). */
     const bool row_long = !cw && k1_mode == 3 && !c->serial_render && !c->block_env && n_frames >= 4 * kMaxBlockFrames;
-    const bool fir_long = fir_fused && dev && !c->serial_render && !bus;
+    /* a dithered render with the flat shaper, rendered frame-parallel in the output kernel (K2 / KF2 /
+     * K5) from K3a's dither rows (needs_serial) */
+    const bool dith_par = !c->serial_render && cfg.render.render_type != ICW_RENDER_ROUND;
+    /* (with a dither generator, blocks of kMaxBlockFrames let K3a of the next block run beside KF2) */
+    const bool fir_long = fir_fused && dev && !c->serial_render && !bus && !dith_par;
     const int Tb = std::min(n_frames, ((fir_fused || row_long) && !c->block_env)
                                           ? (fir_long ? kMaxFirBlockFrames : kMaxBlockFrames) : c->max_block);
     const double taper = c->taper >= 0.0 ? c->taper
@@ -1673,7 +1701,7 @@ int icw_process_streams(icw_ctx *c, int first, int count, const void *in, size_t
     if (bus)
         for (int p = 0; p < n_sets; ++p)
             if (grow((void **)&c->iq[p], &c->iq_bytes[p], S * (size_t)Tb * 4 * sizeof(double))) return ICW_ENOMEM;
-    const bool dither = c->serial_render && cfg.render.render_type != ICW_RENDER_ROUND;
+    const bool dither = cfg.render.render_type != ICW_RENDER_ROUND;     /* K3a: serial or frame-parallel render */
     if (dither)
         for (int p = 0; p < n_sets; ++p)
             if (grow((void **)&c->dith[p], &c->dith_bytes[p], S * 2 * (size_t)(Tb + 1) * sizeof(double))) return ICW_ENOMEM;
@@ -1712,8 +1740,9 @@ int icw_process_streams(icw_ctx *c, int first, int count, const void *in, size_t
          * the converter / output kernel on sA, beside the serial render of the previous block on sR.
          * On its own stream it shared a hardware queue with the render (4 queues per process,
          * GPU_MAX_HW_QUEUES, streams dealt round-robin): K3a of block b + 1 waited for K3r of block b,
-         * 1.2 of every 6.7 ms per c5fir block (profiles/r04_c5fir_timeline.txt) */
-        sD = sA;
+         * 1.2 of every 6.7 ms per c5fir block (profiles/r04_c5fir_timeline.txt).  With a frame-parallel
+         * render (no render stream) it gets a stream of its own, ahead of the converter. */
+        sD = dith_par ? c->stream3 : sA;
     }
     hipStream_t sC = pipe_io ? c->stream_io : nullptr;
     if (pipe_io && (int)c->ev_io.size() < n_blocks) {
@@ -1906,6 +1935,41 @@ int icw_process_streams(icw_ctx *c, int first, int count, const void *in, size_t
         a2.fes = fcm ? ds.fes + f0 * 4 * ICW_FES_PITCH : nullptr;
         return a2;
     };
+    /* the dither generator's / serial render's arguments for block b */
+    auto k3_args = [&](int b, const IcwK2Args &a2) {
+        const int T = blocks[b].second, p = b % n_sets;
+        IcwK3Args a3;
+        memset(&a3, 0, sizeof(a3));
+        a3.pre = a2.pre;
+        a3.pre_stride = a2.pre_stride;
+        a3.n_streams = count;
+        a3.T = T;
+        a3.out = a2.out;
+        a3.out_stride = dos;
+        a3.mt = ds.mt + f0 * 2;          /* column offset: [624][G] layout, pitch G */
+        a3.mt_idx = ds.mt_idx + f0 * 2;
+        a3.rs = ds.rs + f0 * 2 * ICW_RSTATE;
+        a3.clips = ds.clips + f0 * 2;
+        a3.peak_bits = ds.peak_bits + f0 * 2;
+        a3.n_gen = count * 2;
+        a3.mt_pitch = c->n_streams * 2;
+        a3.rk = c->rk;
+        a3.fes = fcm ? ds.fes + f0 * 4 * ICW_FES_PITCH : nullptr;
+        /* the row-broadcast render (16 lanes per channel) while its waves stay few; FP_CHECK
+         * keeps the compact lane-per-channel form */
+        a3.row = c->serial_render && !fcm && (c->render_row == 1 || (c->render_row < 0 && a3.n_gen <= kRowRenderMax)) ? 1 : 0;
+        a3.comp = a3.row && c->k3r_comp;
+        a3.err = ds.err;
+        if (dither) {
+            a3.dith = c->dith[p];
+            /* the row render and the frame-parallel one read runs of one channel: generator-major
+             * [count*2][T rounded up to even] (16-byte pairs); the lane-per-channel renders time-major
+             * [T][count*2] */
+            a3.dith_gm = (a3.row || !c->serial_render) ? 1 : 0;
+            a3.dith_pitch = a3.dith_gm ? (size_t)(T + (T & 1)) : (size_t)count * 2;
+        }
+        return a3;
+    };
     auto adv_args = [&]() {
         IcwAdvArgs av;
         memset(&av, 0, sizeof(av));
@@ -1957,6 +2021,14 @@ int icw_process_streams(icw_ctx *c, int first, int count, const void *in, size_t
             a5.has_trig = 1;
             a5.k2.trig_tab = c->trig;
             a5.k2.trig_pitch = at.trig_pitch;
+        }
+        if (dith_par) {
+            /* the dithered flat render: K3a of the call's block first, on the same stream */
+            const IcwK3Args a3 = k3_args(0, a5.k2);
+            if ((c->dither_lane ? icw_launch_dither_lane(&a3, st) : icw_launch_dither(&a3, st)) != hipSuccess)
+                return ICW_EDEVICE;
+            a5.k2.dith = a3.dith;
+            a5.k2.dith_pitch = a3.dith_pitch;
         }
         if (timing && hipEventRecord(c->ev[0], st) != hipSuccess) return ICW_EDEVICE;
         if (icw_launch_stream1(&a5, N, st) != hipSuccess) return ICW_EDEVICE;
@@ -2030,6 +2102,19 @@ int icw_process_streams(icw_ctx *c, int first, int count, const void *in, size_t
         /* rpre[p] / iq[p] were last read by the serial render of block b - n_sets (on sR) */
         if (c->serial_render && b >= n_sets && sR != s2 && hipStreamWaitEvent(s2, c->k3done[p], 0) != hipSuccess)
             return ICW_EDEVICE;
+        if (dith_par) {
+            /* K3a of this block on its own stream (it depends only on the generators' state, so it runs
+             * ahead, beside the converter / output kernel of the block before); dith[p] was last read
+             * by the output kernel of block b - n_sets */
+            const IcwK3Args a3 = k3_args(b, a2);
+            if (b >= n_sets && sD != s2 && hipStreamWaitEvent(sD, c->k2done[p], 0) != hipSuccess) return ICW_EDEVICE;
+            const hipError_t ed = c->dither_lane ? icw_launch_dither_lane(&a3, sD) : icw_launch_dither(&a3, sD);
+            if (ed != hipSuccess || hipEventRecord(c->ditdone[p], sD) != hipSuccess ||
+                (sD != s2 && hipStreamWaitEvent(s2, c->ditdone[p], 0) != hipSuccess))
+                return ICW_EDEVICE;
+            a2.dith = a3.dith;
+            a2.dith_pitch = a3.dith_pitch;
+        }
         if (timing && hipEventRecord(c->ev[4 * b + 2], s2) != hipSuccess) return ICW_EDEVICE;
         if (fir_fused) {
             const IcwFirArgs af = fir_args(b);
@@ -2064,35 +2149,9 @@ int icw_process_streams(icw_ctx *c, int first, int count, const void *in, size_t
             if (icw_launch_graph_serial(&a4, sR) != hipSuccess) return ICW_EDEVICE;
         }
         if (c->serial_render) {
-            IcwK3Args a3;
-            memset(&a3, 0, sizeof(a3));
-            a3.pre = a2.pre;
-            a3.pre_stride = a2.pre_stride;
-            a3.n_streams = count;
-            a3.T = T;
-            a3.out = a2.out;
-            a3.out_stride = dos;
-            a3.mt = ds.mt + f0 * 2;          /* column offset: [624][G] layout, pitch G */
-            a3.mt_idx = ds.mt_idx + f0 * 2;
-            a3.rs = ds.rs + f0 * 2 * ICW_RSTATE;
-            a3.clips = ds.clips + f0 * 2;
-            a3.peak_bits = ds.peak_bits + f0 * 2;
-            a3.n_gen = count * 2;
-            a3.mt_pitch = c->n_streams * 2;
-            a3.rk = c->rk;
-            a3.fes = fcm ? ds.fes + f0 * 4 * ICW_FES_PITCH : nullptr;
-            /* the row-broadcast render (16 lanes per channel) while its waves stay few; FP_CHECK
-             * keeps the compact lane-per-channel form */
-            a3.row = !fcm && (c->render_row == 1 || (c->render_row < 0 && a3.n_gen <= kRowRenderMax)) ? 1 : 0;
-            a3.comp = a3.row && c->k3r_comp;
-            a3.err = ds.err;
+            IcwK3Args a3 = k3_args(b, a2);
             if (dither) {
                 /* K3a for this block on its own stream: dith[p] was last read by K3b of block b-2 */
-                a3.dith = c->dith[p];
-                /* the row render reads runs of one channel: generator-major [count*2][T rounded up to
-                 * even] (16-byte pairs); the lane-per-channel renders time-major [T][count*2] */
-                a3.dith_gm = a3.row;
-                a3.dith_pitch = a3.row ? (size_t)(T + (T & 1)) : (size_t)count * 2;
                 if (b >= n_sets && sD != sR && hipStreamWaitEvent(sD, c->k3done[p], 0) != hipSuccess) return ICW_EDEVICE;
                 const hipError_t ed = c->dither_lane ? icw_launch_dither_lane(&a3, sD) : icw_launch_dither(&a3, sD);
                 if (ed != hipSuccess || hipEventRecord(c->ditdone[p], sD) != hipSuccess ||
@@ -2351,7 +2410,7 @@ int icw_get_state(icw_ctx *c, int s, void *blob, size_t size)
     memset(&b, 0, sizeof(b));
     b.magic = kBlobMagic;
     b.nord = (uint32_t)c->nord;
-    b.has_render = c->serial_render ? 1u : 0u;
+    b.has_render = c->render_state ? 1u : 0u;
     b.fir_M = (uint32_t)c->fir_M;
     long long fd[3];
     bool ok = quiesce(c) == hipSuccess;
@@ -2362,7 +2421,7 @@ int icw_get_state(icw_ctx *c, int s, void *blob, size_t size)
     ok &= hipMemcpy(b.hist, c->st.hist + (size_t)s * 4 * ICW_HIST_PITCH, sizeof(b.hist), hipMemcpyDeviceToHost) == hipSuccess;
     ok &= hipMemcpy(b.sncnt, c->st.sncnt + (size_t)s * 4, sizeof(b.sncnt), hipMemcpyDeviceToHost) == hipSuccess;
     ok &= hipMemcpy(b.bus, c->st.bus + (size_t)s * ICW_N_INPUTS * 4, sizeof(b.bus), hipMemcpyDeviceToHost) == hipSuccess;
-    if (c->serial_render) {
+    if (c->render_state) {
         const size_t G = (size_t)c->n_streams * 2;
         for (int ch = 0; ch < 2; ++ch)
             ok &= hipMemcpy2D(b.mt[ch], 4, c->st.mt + (size_t)s * 2 + ch, G * 4, 4, 624, hipMemcpyDeviceToHost) == hipSuccess;
@@ -2387,7 +2446,7 @@ int icw_set_state(icw_ctx *c, int s, const void *blob, size_t size)
     memcpy(&b, blob, sizeof(b));
     /* a blob holds the state of the render and converter forms in force when it was saved: the
      * serial-render words exist only with a dithered / shaped render, the FIR history only at its order */
-    if (b.magic != kBlobMagic || b.nord != (uint32_t)c->nord || b.has_render != (c->serial_render ? 1u : 0u) ||
+    if (b.magic != kBlobMagic || b.nord != (uint32_t)c->nord || b.has_render != (c->render_state ? 1u : 0u) ||
         b.fir_M != (uint32_t)c->fir_M)
         return ICW_EINVAL;
     std::lock_guard<std::mutex> lk(c->mu);
@@ -2407,7 +2466,7 @@ int icw_set_state(icw_ctx *c, int s, const void *blob, size_t size)
     const uint32_t eq2[2] = {eq, eq};
     ok &= hipMemcpy(c->st.lr_equal + (size_t)s * 2, eq2, sizeof(eq2), hipMemcpyHostToDevice) == hipSuccess;
     c->lr_known[s] = eq ? 1 : 0;
-    if (c->serial_render) {
+    if (c->render_state) {
         const size_t G = (size_t)c->n_streams * 2;
         for (int ch = 0; ch < 2; ++ch)
             ok &= hipMemcpy2D(c->st.mt + (size_t)s * 2 + ch, G * 4, b.mt[ch], 4, 4, 624, hipMemcpyHostToDevice) == hipSuccess;

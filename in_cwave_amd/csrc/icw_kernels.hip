@@ -810,11 +810,30 @@ __device__ __forceinline__ int icw_render_round_q(double input, const IcwRenderK
     return (v + delta) << k.norm_shift;
 }
 
-/* sound_render_value for ROUND render + flat shaper (sound_render.c:691-809): elementwise */
-__device__ __forceinline__ int icw_render_round(double input, const IcwRenderK &k, unsigned &clips, double &pk)
+/* The q of a dithered render with the flat shaper (sound_render.c:711-767): the dither term d =
+ * rnd * dth_mul comes from K3a (the same product), input = x * norm_mul - prev_ns_err is x * norm_mul
+ * exactly (ns_empty keeps prev_ns_err at 0.0, sound_render.c:396-400, and x - 0.0 is x, a -0.0
+ * included), qinput = input + d; then the rounding offset as icw_round_in (a mid-riser's +- 0.0
+ * changes only a zero's sign, which nothing downstream sees). */
+__device__ __forceinline__ double icw_round_in_d(double x, double d, const IcwRenderK &k, int &delta)
+{
+    if (k.norm_mul != 1.0) x = x * k.norm_mul;
+    x = x + d;
+    if (k.sign_delta) {
+        delta = x < 0.0 ? k.sign_delta : 0;
+        return x;
+    }
+    return icw_round_q(x, k.round_offset, k.sign_delta, delta);
+}
+
+/* sound_render_value for a flat-shaper render (sound_render.c:691-809): elementwise.  DITH: the
+ * dither term d of a RPDF / TPDF / STPDF / GAUSS render (K3a's); ROUND has none. */
+template <bool DITH = false>
+__device__ __forceinline__ int icw_render_round(double input, const IcwRenderK &k, unsigned &clips, double &pk,
+                                                double d = 0.0)
 {
     int delta;
-    const double q = icw_round_in(input, k, delta);
+    const double q = DITH ? icw_round_in_d(input, d, k, delta) : icw_round_in(input, k, delta);
     pk = fmax(pk, fabs(q));
     /* x86 cvttsd2si semantics: NaN -> INT_MIN ("integer indefinite") */
     const int vc = icw_clamp_int(q, k, clips);    /* unconditional: a NaN counts no clip */
@@ -1053,8 +1072,17 @@ __device__ __forceinline__ void icw_frame_graph(const IcwK2Args &a, icw_cprog *P
             p[0] = lOut; p[1] = rOut;
         }
         if (a.do_render) {
-            const int vl = icw_render_round(lOut, a.rk, clip_l, pk_l);
-            const int vr = icw_render_round(rOut, a.rk, clip_r, pk_r);
+            int vl, vr;
+            if (a.dith) {
+                /* a dithered render with the flat shaper: K3a's terms of this frame, rows 2s, 2s + 1 */
+                const double *dd = a.dith + (size_t)(2 * s) * a.dith_pitch + t;
+                const double dl = dd[0], dr = dd[a.dith_pitch];
+                vl = icw_render_round<true>(lOut, a.rk, clip_l, pk_l, dl);
+                vr = icw_render_round<true>(rOut, a.rk, clip_r, pk_r, dr);
+            } else {
+                vl = icw_render_round(lOut, a.rk, clip_l, pk_l);
+                vr = icw_render_round(rOut, a.rk, clip_r, pk_r);
+            }
             if constexpr (DEFER) {
                 dv[0] = vl;
                 dv[1] = vr;
@@ -1995,7 +2023,7 @@ __global__ __launch_bounds__(256, ICW_FIR_OCC) void icw_fir_graph(IcwFirArgs f, 
         const int h = ch ? 4 : 0;
         int dv[4][2];
         const int fr0 = ICW_FIR_R * ll + h;
-        if (ICW_CHAIN4 && P->chain && (TAB || !TRIG) && !a.iq_out && a.do_render) {
+        if (ICW_CHAIN4 && P->chain && (TAB || !TRIG) && !a.iq_out && a.do_render && !a.dith) {
             /* chain program, factors from the table (or none): the four frames op by op, two per
              * pass (four at once spill at 128 VGPRs), each pass's I / Q exchange just before it.
              * Frame tt + fr0 + hh + j (tt a multiple of 8, fr0 = 8 ll + h) sits in table row
@@ -2086,7 +2114,7 @@ __global__ __launch_bounds__(256, ICW_FIR_OCC) void icw_fir_graph(IcwFirArgs f, 
                 }
             }
         }
-    } else if (ICW_CHAIN4 && P->chain && (TAB || !TRIG) && !a.iq_out && a.do_render) {
+    } else if (ICW_CHAIN4 && P->chain && (TAB || !TRIG) && !a.iq_out && a.do_render && !a.dith) {
         /* mono input, chain program: the lane's 8 frames op by op, two at a time, and their 8
          * rendered frames stored together (32 / 48 contiguous bytes per lane) */
         const int fr0 = ICW_FIR_R * ll;
