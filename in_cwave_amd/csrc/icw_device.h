@@ -203,7 +203,13 @@ struct IcwK3Args {
     int32_t dith_gm;               /* layout of dith (above) */
     int32_t comp;                  /* K3r: 1 with a companion wave (staging and flush off the chain's wave) */
     int32_t *err;                  /* nonzero after a companion hand-off that never came (never in a healthy run) */
+    /* the split dither generator (icw_launch_dither; null wbuf: the one-kernel K3a, ICW_DITHER=coop) */
+    uint32_t *wbuf;                /* [n_gen][wpitch] tempered MT words of a chunk (K3t -> K3s) */
+    size_t wpitch, wcap;           /* words per generator row; rows' capacity in words (chunking) */
+    int32_t *dflag;                /* [n_gen] a rejected dsopen pair in the chunk: K3f redoes the channel */
+    uint32_t *dbk;                 /* [n_gen][ICW_DBK] the chunk's starting generator state (K3t -> K3f) */
 };
+#define ICW_DBK 628                /* u32 per backup: 624 words, idx, pad, prev_rnd (a double at 626) */
 
 /* Arguments of the output kernel (frame-parallel: Kahan output sums, unmix, graph, render). */
 struct IcwK2Args {

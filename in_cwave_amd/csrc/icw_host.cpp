@@ -161,6 +161,12 @@ struct icw_ctx {
     hipEvent_t ditdone[kSets] = {};
     double *dith[kSets] = {};
     size_t dith_bytes[kSets] = {};
+    /* the split dither generator's chunk buffers (icw_launch_dither): tempered words, rejection flags,
+     * starting-state backups; one set, used in order on the dither stream */
+    uint32_t *dwords = nullptr, *dbk = nullptr;
+    int32_t *dflag = nullptr;
+    size_t dwords_bytes = 0, dbk_bytes = 0, dflag_bytes = 0;
+    size_t dwcap = 0;                     /* words per generator row of dwords */
     unsigned char *d_in = nullptr, *d_out = nullptr;
     size_t d_in_bytes = 0, d_out_bytes = 0;
     double *d_pre = nullptr;
@@ -208,6 +214,7 @@ struct icw_ctx {
     int k1_mode = -1;         /* K1 variant: -1 auto (row / plain), 0 plain lanes, 3 row broadcast
                                  (ICW_K1_MODE=plain|row, A/B runs) */
     bool dither_lane = false; /* ICW_DITHER=lane: lane-per-channel dither generator (A/B only) */
+    bool dither_coop = false; /* ICW_DITHER=coop: the one-kernel wave-per-channel generator K3a (A/B only) */
     bool k3r_comp = true;     /* ICW_K3R_COMP=0: the row render without its companion wave (K3r, A/B) */
     int render_row = -1;      /* serial render kernel: -1 auto (row broadcast for <= kRowRenderMax
                                  channels), 0 lane per channel, 1 row (ICW_RENDER=serial|row) */
@@ -823,7 +830,7 @@ void free_all(icw_ctx *c)
     DevState &s = c->st;
     void *ptrs[] = {c->s1_stamps, s.mt, s.mt_idx, s.rs, s.lr_equal, s.fes, s.err, s.hist, s.sncnt, s.hq_phase, s.pos, s.fade,
                     s.n_frame, s.bus, s.clips, s.peak_bits, c->d_prog, c->trig, c->d_in, c->d_out, c->d_pre, c->d_xin,
-                    c->d_fir_g, c->fir_hist[0], c->fir_hist[1]};
+                    c->d_fir_g, c->fir_hist[0], c->fir_hist[1], c->dwords, c->dbk, c->dflag};
     for (void *p : ptrs)
         if (p) (void)hipFree(p);
     for (int p = 0; p < kSets; ++p) {
@@ -1076,6 +1083,7 @@ int icw_create(const icw_config *cfg, const icw_node *nodes, int n_nodes, int n_
         if (rr && !strcmp(rr, "row")) c->render_row = 1;
         const char *d = getenv("ICW_DITHER");
         c->dither_lane = d && !strcmp(d, "lane");
+        c->dither_coop = d && !strcmp(d, "coop");
         const char *kc = getenv("ICW_K3R_COMP");
         if (kc && !strcmp(kc, "0")) c->k3r_comp = false;
 
@@ -1705,6 +1713,19 @@ int icw_process_streams(icw_ctx *c, int first, int count, const void *in, size_t
     if (dither)
         for (int p = 0; p < n_sets; ++p)
             if (grow((void **)&c->dith[p], &c->dith_bytes[p], S * 2 * (size_t)(Tb + 1) * sizeof(double))) return ICW_ENOMEM;
+    if (dither && !c->dither_coop && !c->dither_lane) {
+        /* chunk rows of at most 2^26 words in all (256 MB), at least 1 024 frames of the widest draw (GAUSS,
+         * 24 words per sample), at most the block's */
+        const size_t G = S * 2;
+        size_t cap = std::max<size_t>(((size_t)1 << 26) / G, (size_t)24 * 1024);
+        cap = std::min(cap, (size_t)24 * (size_t)(Tb + 1));
+        cap = (cap + 3) & ~(size_t)3;                      /* rows 16-byte aligned */
+        if (grow((void **)&c->dwords, &c->dwords_bytes, G * cap * 4) ||
+            grow((void **)&c->dbk, &c->dbk_bytes, G * ICW_DBK * 4) ||
+            grow((void **)&c->dflag, &c->dflag_bytes, G * 4))
+            return ICW_ENOMEM;
+        c->dwcap = cap;
+    }
 
     /* Streams.  sK runs the IIR state kernel K1 (the serial, issue-bound one); sA runs the input
      * prep K0, the output kernel K2 and the serial graph / render; sD the dither generator.  When
@@ -1967,6 +1988,12 @@ int icw_process_streams(icw_ctx *c, int first, int count, const void *in, size_t
              * [T][count*2] */
             a3.dith_gm = (a3.row || !c->serial_render) ? 1 : 0;
             a3.dith_pitch = a3.dith_gm ? (size_t)(T + (T & 1)) : (size_t)count * 2;
+            if (!c->dither_coop && !c->dither_lane) {
+                a3.wbuf = c->dwords;
+                a3.wpitch = a3.wcap = c->dwcap;
+                a3.dflag = c->dflag;
+                a3.dbk = c->dbk;
+            }
         }
         return a3;
     };

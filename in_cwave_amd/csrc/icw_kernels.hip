@@ -18,6 +18,8 @@
 #include <math.h>
 #include <stdint.h>
 
+#include <algorithm>
+
 #include "../../include/icw.h"
 #include "icw_device.h"
 #include "icw_iir_dev.h"
@@ -2705,20 +2707,30 @@ __device__ __forceinline__ void icw_coop_twist(uint32_t *mt, int lane)
     __syncthreads();
 }
 
+/* the generator g's samples of the block (or chunk) the sequential way: from the state in a.mt /
+ * a.mt_idx / rs[0], or (bk) from the chunk's backup K3t made -- K3f's redo of a channel whose words
+ * held a rejected pair */
 template <int RT>
-__global__ __launch_bounds__(64) void icw_dither_coop(IcwK3Args a)
+__device__ __forceinline__ void icw_dither_coop_body(const IcwK3Args &a, int g, const uint32_t *bk)
 {
     constexpr int V = RT == ICW_RENDER_GAUSS ? 12 : (RT == ICW_RENDER_TPDF ? 2 : 1);
     __shared__ uint32_t mt[624];
     __shared__ uint32_t tw[626];           /* the window's word list: [carried word] + tempered mt[idx..623] */
     __shared__ double vals[313 + 16];      /* [carried values] + the window's accepted values */
     __shared__ short pidx[313];            /* pair index of each accepted value of the window */
-    const int lane = threadIdx.x;
-    const int g = blockIdx.x;              /* one wave per generator: everything below is wave-uniform */
-    for (int i = lane; i < 624; i += 64) mt[i] = a.mt[(size_t)i * a.mt_pitch + g];
-    int idx = a.mt_idx[g];
+    const int lane = threadIdx.x;          /* one wave per generator: everything below is wave-uniform */
     double *rs = a.rs + (size_t)g * ICW_RSTATE;
-    double prev_rnd = rs[0];
+    int idx;
+    double prev_rnd;
+    if (bk) {
+        for (int i = lane; i < 624; i += 64) mt[i] = bk[i];
+        idx = (int)bk[624];
+        prev_rnd = *(const double *)(bk + 626);
+    } else {
+        for (int i = lane; i < 624; i += 64) mt[i] = a.mt[(size_t)i * a.mt_pitch + g];
+        idx = a.mt_idx[g];
+        prev_rnd = rs[0];
+    }
     const double dth_mul = a.rk.dth_mul;
     /* generator-major (dith_gm): the wave's samples of a window are one contiguous run, each store
      * instruction writes 64 consecutive doubles; time-major: one double per row (K3b's layout) */
@@ -2802,6 +2814,137 @@ __global__ __launch_bounds__(64) void icw_dither_coop(IcwK3Args a)
         a.mt_idx[g] = idx;
         rs[0] = prev_rnd;
     }
+}
+
+template <int RT>
+__global__ __launch_bounds__(64) void icw_dither_coop(IcwK3Args a)
+{
+    icw_dither_coop_body<RT>(a, blockIdx.x, nullptr);
+}
+
+/* ------------------------------------------------------ split dither generator (K3t/K3s/K3f) ---- */
+/* The dither term of sound_render_value (sound_render.c:711-751) consumes the channel's MT19937 words
+ * in a fixed order: sample t of a chunk takes words [W t, W t + W) after the chunk's starting
+ * position (W = 2 V: V dsopen values of two words each, mt_jrnd.c:218-256) -- unless a pair is
+ * rejected (exactly -1.0, probability 2^-53 per pair), which shifts every later sample.  So
+ *   K3t  icw_dith_twist    one wave per generator: saves the starting state (the backup), then runs
+ *                          the twists (mt_jrnd.c:99-124) and writes the chunk's W T tempered words,
+ *                          coalesced, and the generator's state after them (mt, idx);
+ *   K3s  icw_dith_samples  a thread per sample, frame-parallel: its W words -> the V values -> rnd *
+ *                          dth_mul (STPDF: the previous sample's value, or the backup's prev_rnd);
+ *                          a rejected pair flags the generator;
+ *   K3f  icw_dith_fix      a wave per flagged generator only: the chunk again from the backup, the
+ *                          sequential way (icw_dither_coop_body, rejections and all), output and state.
+ * The serial part left is the twist chain itself; K3a did the windows' tempering, pairing, ballots and
+ * samples on the same wave between twists.  Chunks of at most a.wcap / W frames (icw_launch_dither). */
+__global__ __launch_bounds__(64) void icw_dith_twist(IcwK3Args a, int W)
+{
+    __shared__ uint32_t mt[624];
+    const int lane = threadIdx.x, g = blockIdx.x;
+    uint32_t *bk = a.dbk + (size_t)g * ICW_DBK;
+    double *rs = a.rs + (size_t)g * ICW_RSTATE;
+    for (int i = lane; i < 624; i += 64) {
+        const uint32_t v = a.mt[(size_t)i * a.mt_pitch + g];
+        mt[i] = v;
+        bk[i] = v;
+    }
+    int idx = a.mt_idx[g];
+    if (lane == 0) {
+        bk[624] = (uint32_t)idx;
+        *(double *)(bk + 626) = rs[0];
+        a.dflag[g] = 0;
+    }
+    __syncthreads();
+    uint32_t *wr = a.wbuf + (size_t)g * a.wpitch;
+    const long long nw = (long long)W * a.T;
+    long long pos = 0;
+    bool twisted = false;
+    while (pos < nw) {
+        if (idx >= 624) {
+            icw_coop_twist(mt, lane);
+            idx = 0;
+            twisted = true;
+        }
+        const int n = (int)min((long long)(624 - idx), nw - pos);
+        for (int j = lane; j < n; j += 64) wr[pos + j] = icw_mt_temper(mt[idx + j]);
+        pos += n;
+        idx += n;
+    }
+    if (twisted)
+        for (int i = lane; i < 624; i += 64) a.mt[(size_t)i * a.mt_pitch + g] = mt[i];
+    if (lane == 0) a.mt_idx[g] = idx;
+}
+
+/* the dsopen value of a word pair (mt_jrnd.c:218-256); rej: the pair is the rejected -1.0 */
+__device__ __forceinline__ double icw_dsopen_pair(uint32_t wa, uint32_t wb, bool &rej)
+{
+    const uint32_t ua = wa >> 5, ub = wb >> 6;
+    rej |= ua == 0u && ub == 0u;
+    return ((ua * 67108864.0 + ub) * (1.0 / 9007199254740992.0)) * 2.0 - 1.0;
+}
+
+/* gm: a thread per (generator, sample), samples fastest (generator-major rows, coalesced); tm: the
+ * generators fastest (time-major rows, K3b / K3f) */
+template <int RT>
+__global__ __launch_bounds__(256) void icw_dith_samples(IcwK3Args a)
+{
+    constexpr int V = RT == ICW_RENDER_GAUSS ? 12 : (RT == ICW_RENDER_TPDF ? 2 : 1);
+    constexpr int W = 2 * V;
+    const long long id = (long long)blockIdx.x * 256 + threadIdx.x;
+    const long long tot = (long long)a.n_gen * a.T;
+    if (id >= tot) return;
+    int g, t;
+    if (a.dith_gm) { g = (int)(id / a.T); t = (int)(id - (long long)g * a.T); }
+    else { t = (int)(id / a.n_gen); g = (int)(id - (long long)t * a.n_gen); }
+    const uint32_t *w = a.wbuf + (size_t)g * a.wpitch + (size_t)t * W;
+    uint32_t u[W];
+    if constexpr (W % 4 == 0) {
+#pragma unroll
+        for (int i = 0; i < W; i += 4) {
+            const uint4 q = *(const uint4 *)(w + i);
+            u[i] = q.x; u[i + 1] = q.y; u[i + 2] = q.z; u[i + 3] = q.w;
+        }
+    } else {
+        const uint2 q = *(const uint2 *)w;
+        u[0] = q.x; u[1] = q.y;
+    }
+    bool rej = false;
+    double rnd;
+    if constexpr (RT == ICW_RENDER_RPDF) {
+        rnd = icw_dsopen_pair(u[0], u[1], rej) / ICW_SQRT2;
+    } else if constexpr (RT == ICW_RENDER_TPDF) {
+        rnd = icw_dsopen_pair(u[0], u[1], rej);
+        rnd += icw_dsopen_pair(u[2], u[3], rej);
+        rnd /= 2.0;
+    } else if constexpr (RT == ICW_RENDER_STPDF) {
+        double prev;
+        if (t == 0) {
+            prev = *(const double *)(a.dbk + (size_t)g * ICW_DBK + 626);
+        } else {
+            bool r2 = false;               /* the previous sample's own pair is flagged by its thread */
+            prev = icw_dsopen_pair(w[-2], w[-1], r2);
+        }
+        const double tr = icw_dsopen_pair(u[0], u[1], rej);
+        rnd = (tr - prev) / 2.0;
+        if (t == a.T - 1) a.rs[(size_t)g * ICW_RSTATE] = tr;     /* prev_rnd after the chunk */
+    } else {
+        rnd = icw_dsopen_pair(u[0], u[1], rej);
+#pragma unroll
+        for (int i = 1; i < 12; ++i) rnd += icw_dsopen_pair(u[2 * i], u[2 * i + 1], rej);
+        rnd /= (2.0 * ICW_SQRT6);
+    }
+    const size_t o = a.dith_gm ? (size_t)g * a.dith_pitch + t : (size_t)t * a.dith_pitch + g;
+    a.dith[o] = rnd * a.rk.dth_mul;
+    if (rej) atomicOr(&a.dflag[g], 1);
+}
+
+template <int RT>
+__global__ __launch_bounds__(64) void icw_dith_fix(IcwK3Args a)
+{
+    const int g = blockIdx.x;
+    if (!a.dflag[g]) return;               /* wave-uniform: the usual case, no rejected pair */
+    icw_dither_coop_body<RT>(a, g, a.dbk + (size_t)g * ICW_DBK);
+    if (threadIdx.x == 0) a.dflag[g] = 0;
 }
 
 /* Shaper history as a ring of R values (R = ICW_MAX_NS_TAPS for the FIR shapers, 4 for the
@@ -3943,17 +4086,38 @@ static hipError_t launch_k2_t(IcwK2Args a, hipStream_t st)
     return hipGetLastError();
 }
 
-extern "C" hipError_t icw_launch_dither(const IcwK3Args *a, hipStream_t st)
+template <int RT>
+static hipError_t icw_launch_dither_t(const IcwK3Args *a, hipStream_t st)
 {
-    const int blocks = a->n_gen;           /* one wave per render channel */
-    switch (a->rk.render_type) {
-    case ICW_RENDER_RPDF: hipLaunchKernelGGL(icw_dither_coop<ICW_RENDER_RPDF>, dim3(blocks), dim3(64), 0, st, *a); break;
-    case ICW_RENDER_TPDF: hipLaunchKernelGGL(icw_dither_coop<ICW_RENDER_TPDF>, dim3(blocks), dim3(64), 0, st, *a); break;
-    case ICW_RENDER_STPDF: hipLaunchKernelGGL(icw_dither_coop<ICW_RENDER_STPDF>, dim3(blocks), dim3(64), 0, st, *a); break;
-    case ICW_RENDER_GAUSS: hipLaunchKernelGGL(icw_dither_coop<ICW_RENDER_GAUSS>, dim3(blocks), dim3(64), 0, st, *a); break;
-    default: return hipErrorInvalidValue;
+    if (!a->wbuf) {                        /* the one-kernel K3a (ICW_DITHER=coop, A/B) */
+        hipLaunchKernelGGL(icw_dither_coop<RT>, dim3(a->n_gen), dim3(64), 0, st, *a);
+        return hipGetLastError();
+    }
+    constexpr int W = 2 * (RT == ICW_RENDER_GAUSS ? 12 : (RT == ICW_RENDER_TPDF ? 2 : 1));
+    const int chunk = (int)std::min<size_t>((size_t)a->T, a->wcap / W);
+    if (chunk <= 0) return hipErrorInvalidValue;
+    for (int t0 = 0; t0 < a->T; t0 += chunk) {
+        IcwK3Args c = *a;
+        c.T = std::min(chunk, a->T - t0);
+        c.dith = a->dith + (a->dith_gm ? (size_t)t0 : (size_t)t0 * a->dith_pitch);
+        hipLaunchKernelGGL(icw_dith_twist, dim3(c.n_gen), dim3(64), 0, st, c, W);
+        const long long tot = (long long)c.n_gen * c.T;
+        hipLaunchKernelGGL(icw_dith_samples<RT>, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, st, c);
+        hipLaunchKernelGGL(icw_dith_fix<RT>, dim3(c.n_gen), dim3(64), 0, st, c);
     }
     return hipGetLastError();
+}
+
+extern "C" hipError_t icw_launch_dither(const IcwK3Args *a, hipStream_t st)
+{
+    if (a->T <= 0) return hipSuccess;
+    switch (a->rk.render_type) {
+    case ICW_RENDER_RPDF: return icw_launch_dither_t<ICW_RENDER_RPDF>(a, st);
+    case ICW_RENDER_TPDF: return icw_launch_dither_t<ICW_RENDER_TPDF>(a, st);
+    case ICW_RENDER_STPDF: return icw_launch_dither_t<ICW_RENDER_STPDF>(a, st);
+    case ICW_RENDER_GAUSS: return icw_launch_dither_t<ICW_RENDER_GAUSS>(a, st);
+    default: return hipErrorInvalidValue;
+    }
 }
 
 /* the lane-per-channel generator, kept for A/B timing (ICW_DITHER=lane) */
