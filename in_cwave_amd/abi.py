@@ -198,5 +198,6 @@ SIGNATURES = {
                                          C.POINTER(C.c_char_p), _i, C.POINTER(BatchOpts), C.POINTER(_i), _i,
                                          C.POINTER(BatchStats), C.POINTER(_i)]),
     "icw_version": (C.c_char_p, []),
+    "icw_abi_version": (C.c_int, []),
     "icw_strerror": (C.c_char_p, [_i]),
 }

@@ -70,18 +70,21 @@ int icw_mod_context_fopen(icw_mod_context *mc, uint32_t sample_rate, uint32_t fm
 {
     int rc;
     if (!mc) return ICW_EINVAL;
+    /* the arguments the context would refuse, before anything changes (icw_set_input repeats them) */
+    if (fmt > ICW_FMT_CW_F32 || channels == 0 || sample_rate == 0 || sample_rate > ICW_MAX_FS_SRC || n_samples < 0)
+        return ICW_EINVAL;
     rc = icw_set_input(mc->ctx, sample_rate, fmt, channels);
     if (rc != ICW_OK) return rc;
     mc->cfg.sample_rate = sample_rate;
     mc->cfg.in_format = fmt;
     mc->cfg.in_channels = channels;
     rc = icw_stream_open(mc->ctx, 0, n_samples, fade_in_ms, fade_out_ms, sec_align, clr_nframe, clr_hilb);
-    if (rc != ICW_OK) return rc;
-    rc = icw_set_outbits(mc->ctx, need24bits);
-    if (rc != ICW_OK) return rc;
-    mc->cfg.need24bits = need24bits ? 1 : 0;
+    if (rc == ICW_OK) rc = icw_set_outbits(mc->ctx, need24bits);
+    /* out_size and the depth always describe the context as it now is, even after a device error part
+     * way (the caller sizes its next buffers from them; after ICW_EDEVICE it should reopen the track) */
     mc->out_size = 2 * icw_render_size(mc->ctx);
-    return ICW_OK;
+    mc->cfg.need24bits = mc->out_size == 6 ? 1 : 0;
+    return rc;
 }
 
 int icw_amod_process_samples(char *buf, icw_mod_context *mc, const void *tbuff, unsigned n_frames)

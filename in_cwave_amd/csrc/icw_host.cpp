@@ -978,6 +978,8 @@ extern "C" {
 
 const char *icw_version(void) { return "in_cwave_amd 0.1 (gfx950)"; }
 
+int icw_abi_version(void) { return ICW_ABI_VERSION; }
+
 const char *icw_strerror(int s)
 {
     switch (s) {

@@ -252,6 +252,9 @@ __global__ __launch_bounds__(256) void icw_unpack_frames(IcwK0Args a)
 #ifndef ICW_FIR_PAD
 #define ICW_FIR_PAD 2
 #endif
+#if ICW_FIR_PAD != 1 && ICW_FIR_PAD != 2
+#error "ICW_FIR_PAD: icw_fir_block's window reads are written for 1 or 2 pad doubles per 8"
+#endif
 #ifndef ICW_SCALAR_UNIT
 #define ICW_SCALAR_UNIT 1                            /* A/B: unit gains / norm_mul tested on scalar flags */
 #endif

@@ -350,6 +350,13 @@ int icw_get_fp_census(icw_ctx *ctx, int s, int reset, uint32_t counts[4][ICW_FES
 const char *icw_version(void);
 const char *icw_strerror(int status);
 
+/* The C ABI's version, for bindings to check at load time against the header they were built with.
+ *   1  rounds 1-4;
+ *   2  icw_mod_context_fopen takes need24bits (its 11th argument, in_cwave.c:212) -- a binding built
+ *      against version 1 would pass an undefined bit depth. */
+#define ICW_ABI_VERSION 2
+int icw_abi_version(void);
+
 #ifdef __cplusplus
 }
 #endif

@@ -15,7 +15,6 @@ from in_cwave_amd import abi
 
 HERE = Path(__file__).resolve().parent
 LIB = HERE / "liboracle.so"
-REF_MT = HERE / "_ref" / "libref_mt.so"
 _lib = None
 
 

@@ -40,6 +40,9 @@ def test_library_loads_without_gpu():
     l = L.load()
     assert l.icw_version().startswith(b"in_cwave_amd")
     assert l.icw_strerror(abi.EUNSUPPORTED)
+    # the header's ICW_ABI_VERSION is the library's (2: icw_mod_context_fopen takes need24bits)
+    hdr = (ROOT / "include" / "icw.h").read_text()
+    assert l.icw_abi_version() == int(re.search(r"#define ICW_ABI_VERSION (\d+)", hdr).group(1)) == 2
 
 
 def test_ctypes_layout_matches_c():
