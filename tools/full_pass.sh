@@ -1,6 +1,7 @@
 #!/bin/bash
-# Full GPU suite, smoke and the driver's default bench command on this tree (round 5)
-mkdir -p gpurun_out; TAG=${TAG:-r5full}
+# The round-end pass on this tree: the full -m gpu suite, smoke, and the driver's default bench command
+# (TAG names the outputs under gpurun_out/).  Every step has its own time limit.
+mkdir -p gpurun_out; TAG=${TAG:-full}
 timeout -k 10 1000 python -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread > gpurun_out/${TAG}_pytest.txt 2>&1
 rc=$?; echo "[pytest] rc=$rc"; tail -3 gpurun_out/${TAG}_pytest.txt
 [ $rc -le 1 ] || exit 2
