@@ -413,7 +413,12 @@ def fir_roofline(wname, W, S, T, kf_ms, kf_n, k2_ms, k2_n, fused):
     frames_per_launch = float(S) * T / max(1, kf_n)
     avg_s = kf_ms / 1e3 / max(1, kf_n)
     flops_per_frame = chans * nt * 3
-    kname = "icw_fir_graph" if fused else "icw_fir_hilbert"
+    # the fused converter's ROUND renders run the signature form (icw_fir_sig) over every tile but the
+    # one holding a launch block's last frame, which icw_fir_graph takes in a second launch; the HIP
+    # events span both (icw_fir_graph's tile is 1/1024 of a c2fir launch's frames)
+    sig = (fused and W["render"] == "round16" and not os.environ.get("ICW_BENCH_RENDER")
+           and os.environ.get("ICW_FIR_SIG", "1") != "0")
+    kname = ("icw_fir_sig" if sig else "icw_fir_graph") if fused else "icw_fir_hilbert"
     traffic, src = pmc_traffic(wname, kname, frames_per_launch)
     tf = flops_per_frame * frames_per_launch / avg_s / 1e12 if avg_s > 0 else None
     alg_b = W["bytes"] * frames_per_launch

@@ -59,6 +59,9 @@ struct IcwFirArgs {
     double *xd;                    /* [n_streams*4][x_pitch] rows s*4 + ch*2 + {0: I, 1: Q} */
     size_t x_pitch;
     int32_t zero;                  /* always 0: keeps the lane's 4 output strides opaque (no LDS read pairing) */
+    int32_t sig;                   /* KF2: the program's chain signature (IcwProg.sig; 0: not a chain), so the
+                                      launcher can pick the signature form (icw_fir_sig) */
+    int32_t tile0;                 /* KF2: index of the first tile icw_fir_graph's grid covers (set by the launcher) */
 };
 
 /* Arguments of the call-end bookkeeping kernel: one thread per stream.  During a call every

@@ -1821,6 +1821,7 @@ int icw_process_streams(icw_ctx *c, int first, int count, const void *in, size_t
         af.hist_out = c->fir_hist[(c->fir_par + b + 1) & 1] + f0 * hrow;
         af.xd = c->xd[b % n_sets];
         af.x_pitch = x_pitch;
+        af.sig = c->prog.chain ? c->prog.sig : 0;
         return af;
     };
     /* pinned host input: block b's input slice of every stream goes in on the copy stream, and the

@@ -501,12 +501,12 @@ __device__ __forceinline__ void icw_fir_block(const double *xs, icw_ctap *gs, in
 
 /* Q of a lane's 8 outputs tt + 8 ll + r; a = (c - 1 + sh) / 8.  The taps in ascending order, in
  * register blocks of ICW_FIR_NTAP, then one by one */
+template <int NB = ICW_FIR_NTAP>
 __device__ __forceinline__ void icw_fir_sums(const double *xs, icw_ctap *gs, int nt, int ll, int a, int sh, int c,
                                              double (&acc)[ICW_FIR_R])
 {
 #pragma unroll
     for (int r = 0; r < ICW_FIR_R; ++r) acc[r] = 0.0;
-    constexpr int NB = ICW_FIR_NTAP;
     const int nb = nt / NB;
     constexpr int G = 8 + ICW_FIR_PAD;                  /* physical doubles per group of 8 */
     constexpr int GS = G * NB / 4;                      /* physical step of a window per block */
@@ -1966,7 +1966,7 @@ __global__ __launch_bounds__(256, ICW_FIR_OCC) void icw_fir_graph(IcwFirArgs f, 
     const int s = blockIdx.x;
     constexpr int nchc = NC;
     const int TF = 256 * ICW_FIR_R / nchc;
-    const int tt = blockIdx.y * TF;
+    const int tt = (blockIdx.y + f.tile0) * TF;
     const int M = f.M, c = M >> 1;
     const int sh = (8 - ((c - 1) & 7)) & 7;
     const int av = (c - 1 + sh) >> 3;
@@ -2197,6 +2197,162 @@ __global__ __launch_bounds__(256, ICW_FIR_OCC) void icw_fir_graph(IcwFirArgs f, 
     if (a.do_render) icw_meters_wg(a, s, clip_l, clip_r, pk_l, pk_r, red_clip, red_pk);
     ICW_FIR_STAMP(6);
     ICW_FIR_STAMP(7);
+}
+
+/* KF2's signature form (icw_fir_sig): the tiles of a launch block before the one holding its last
+ * frame, for a chain program of one of the specialised signatures (ICW_SIG_*), a ROUND / flat render
+ * and no pre-render doubles -- the production form of the BASELINE FIR legs.  Every lane then takes
+ * icw_chain_frames' render-only branch (full frames, no block-end bus write), so the kernel holds only
+ * the staging, the sums, that branch (SIG and the output depth B24 at compile time) and the meters:
+ * icw_fir_graph's register allocation is set by its generic paths (the per-frame graph, the exact
+ * chain pass, the runtime signature switch), and their scalars spilled to VGPR lanes in the hot
+ * phases.  icw_launch_fir_graph runs the last tile of each stream through icw_fir_graph (tile0).
+ * Same staging, sums and render arithmetic, so the bytes and meters are icw_fir_graph's. */
+/* Occupancy of the signature form: without the generic paths it fits 114 VGPRs at 4 workgroups per CU,
+ * no scratch.  It also fits 96 (5 per CU) with 4-tap register blocks in the sums, and the mono form 80
+ * (6 per CU): measured the same within the box noise (c2fir -1 / +1.7 %, c4fir +0.5 / +0.8 %, c3fir
+ * -1.9 / +0.2 %, profiles/r06_fir_sig_ab.txt) with 24 more VALU and 48 more LDS instructions per wave,
+ * so the FP64 pipe, not latency, bounds it at 4. */
+#ifndef ICW_FIR_SIG_OCC
+#define ICW_FIR_SIG_OCC 4
+#endif
+#ifndef ICW_FIR_SIG_OCC1
+#define ICW_FIR_SIG_OCC1 4                           /* the mono form */
+#endif
+#ifndef ICW_FIR_SIG_NTAP
+#define ICW_FIR_SIG_NTAP ICW_FIR_NTAP
+#endif
+template <int SIG, int NC, bool B24>
+__global__ __launch_bounds__(256, NC == 2 ? ICW_FIR_SIG_OCC : ICW_FIR_SIG_OCC1) void icw_fir_sig(IcwFirArgs f, IcwK2Args a)
+{
+    extern __shared__ __attribute__((aligned(16))) double lds[];
+    __shared__ unsigned red_clip[2][ICW_PK_SLOTS];
+    __shared__ double red_pk[2][ICW_PK_SLOTS];
+    constexpr bool TRIG = (SIG & ~ICW_SIG_UNIT) != ICW_SIG_M;
+    constexpr int TF = 256 * ICW_FIR_R / NC;
+    const int s = blockIdx.x;
+    const int tt = blockIdx.y * TF;
+    const int M = f.M, c = M >> 1;
+    const int sh = (8 - ((c - 1) & 7)) & 7;
+    const int av = (c - 1 + sh) >> 3;
+    const int px = (icw_fir_phys(sh + M + TF + 24) + 2) & ~1;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int ch = NC == 2 ? lane >> 5 : 0;
+    const int ll = NC == 2 ? wv * 32 + (lane & 31) : threadIdx.x;
+    icw_fir_stage<NC>(f, s, 0, lds, px, tt, TF, sh, threadIdx.x, 256);
+    __syncthreads();
+    double q[ICW_FIR_R], vi[ICW_FIR_R];
+    icw_fir_sums<ICW_FIR_SIG_NTAP>(lds + ch * px, (icw_ctap *)f.g, f.nt, ll, av, sh, c, q);
+    const int ix = 8 * av + 1;
+#pragma unroll
+    for (int r = 0; r < ICW_FIR_R; ++r) vi[r] = lds[ch * px + icw_fir_phys(ICW_FIR_R * ll + r + ix)];
+    icw_cprog *P = icw_prog_c(a.prog);
+    unsigned clip_l = 0, clip_r = 0;
+    double pk_l = 0.0, pk_r = 0.0;
+    const size_t pq = (size_t)a.trig_perm_q * a.trig_pitch;
+    unsigned char *o = a.out + (size_t)s * a.out_stride;
+    if constexpr (NC == 2) {
+        /* lane l (L) frames 0-3 of its eight with R's values swapped in, lane l + 32 frames 4-7 */
+        const int h = ch ? 4 : 0;
+        const int fr0 = ICW_FIR_R * ll + h;
+        const uint32_t tro_lane = (uint32_t)(((size_t)h * a.trig_perm_q + (size_t)(tt >> 3) + ll) * a.trig_pitch);
+        int dv[4][2];
+#pragma unroll
+        for (int hh = 0; hh < 4; hh += 2) {
+            IcwLR in2[2];
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                const int r = hh + j;
+                double xl = vi[r], xr = vi[r + 4], yl = q[r], yr = q[r + 4];
+                icw_swap32(xl, xr);
+                icw_swap32(yl, yr);
+                in2[j].lre = xl; in2[j].lim = yl; in2[j].rre = xr; in2[j].rim = yr;
+            }
+            int dv2[2][2];
+            icw_sig_fast<TRIG, 2, SIG>(a, P, in2, clip_l, clip_r, pk_l, pk_r, dv2, tro_lane, (size_t)hh * pq, pq);
+            dv[hh][0] = dv2[0][0]; dv[hh][1] = dv2[0][1];
+            dv[hh + 1][0] = dv2[1][0]; dv[hh + 1][1] = dv2[1][1];
+        }
+        if constexpr (B24) {
+            unsigned char *p = o + (size_t)(tt + fr0) * 6;
+            unsigned w[6];
+#pragma unroll
+            for (int r = 0; r < 4; r += 2) {
+                const unsigned l0 = (unsigned)dv[r][0] & 0xffffffu, r0 = (unsigned)dv[r][1] & 0xffffffu;
+                const unsigned l1 = (unsigned)dv[r + 1][0] & 0xffffffu, r1 = (unsigned)dv[r + 1][1] & 0xffffffu;
+                w[r / 2 * 3 + 0] = l0 | (r0 << 24);
+                w[r / 2 * 3 + 1] = (r0 >> 8) | (l1 << 16);
+                w[r / 2 * 3 + 2] = (l1 >> 16) | (r1 << 8);
+            }
+            if (!((uintptr_t)p & 7)) {
+                uint2 *q2 = (uint2 *)p;
+                q2[0] = make_uint2(w[0], w[1]);
+                q2[1] = make_uint2(w[2], w[3]);
+                q2[2] = make_uint2(w[4], w[5]);
+            } else {
+#pragma unroll
+                for (int i = 0; i < 24; ++i) p[i] = (unsigned char)(w[i >> 2] >> (8 * (i & 3)));
+            }
+        } else {
+            unsigned pk[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) pk[r] = ((unsigned)dv[r][0] & 0xffffu) | ((unsigned)dv[r][1] << 16);
+            unsigned *p = (unsigned *)(o + (size_t)(tt + fr0) * 4);
+            if (!((uintptr_t)p & 15)) {
+                *(uint4 *)p = make_uint4(pk[0], pk[1], pk[2], pk[3]);
+            } else {
+#pragma unroll
+                for (int r = 0; r < 4; ++r) p[r] = pk[r];
+            }
+        }
+    } else {
+        /* mono: the lane's 8 frames two at a time, packed as icw_mono_passes does */
+        const int fr0 = ICW_FIR_R * ll;
+        const uint32_t tro_lane = (uint32_t)(((size_t)(tt >> 3) + ll) * a.trig_pitch);
+        unsigned w[ICW_FIR_R / 2 * 3];
+#pragma unroll
+        for (int hh = 0; hh < ICW_FIR_R; hh += 2) {
+            IcwLR in2[2];
+#pragma unroll
+            for (int r = 0; r < 2; ++r) {
+                in2[r].lre = in2[r].rre = vi[hh + r];
+                in2[r].lim = in2[r].rim = q[hh + r];
+            }
+            int dv[2][2];
+            icw_sig_fast<TRIG, 2, SIG>(a, P, in2, clip_l, clip_r, pk_l, pk_r, dv, tro_lane, (size_t)hh * pq, pq);
+            if constexpr (B24) {
+                const unsigned l0 = (unsigned)dv[0][0] & 0xffffffu, r0 = (unsigned)dv[0][1] & 0xffffffu;
+                const unsigned l1 = (unsigned)dv[1][0] & 0xffffffu, r1 = (unsigned)dv[1][1] & 0xffffffu;
+                w[hh / 2 * 3 + 0] = l0 | (r0 << 24);
+                w[hh / 2 * 3 + 1] = (r0 >> 8) | (l1 << 16);
+                w[hh / 2 * 3 + 2] = (l1 >> 16) | (r1 << 8);
+            } else {
+                w[hh] = ((unsigned)dv[0][0] & 0xffffu) | ((unsigned)dv[0][1] << 16);
+                w[hh + 1] = ((unsigned)dv[1][0] & 0xffffu) | ((unsigned)dv[1][1] << 16);
+            }
+        }
+        if constexpr (B24) {
+            unsigned char *p = o + (size_t)(tt + fr0) * 6;
+            if (!((uintptr_t)p & 7)) {
+                uint2 *q2 = (uint2 *)p;
+#pragma unroll
+                for (int i = 0; i < ICW_FIR_R / 2 * 3 / 2; ++i) q2[i] = make_uint2(w[2 * i], w[2 * i + 1]);
+            } else {
+#pragma unroll
+                for (int i = 0; i < ICW_FIR_R * 6; ++i) p[i] = (unsigned char)(w[i >> 2] >> (8 * (i & 3)));
+            }
+        } else {
+            unsigned *p = (unsigned *)(o + (size_t)(tt + fr0) * 4);
+            if (!((uintptr_t)p & 15)) {
+                *(uint4 *)p = make_uint4(w[0], w[1], w[2], w[3]);
+                *(uint4 *)(p + 4) = make_uint4(w[4], w[5], w[6], w[7]);
+            } else {
+#pragma unroll
+                for (int r = 0; r < ICW_FIR_R; ++r) p[r] = w[r];
+            }
+        }
+    }
+    icw_meters_wg(a, s, clip_l, clip_r, pk_l, pk_r, red_clip, red_pk);
 }
 
 /* Per-frame rotation table: the Shift / PM factors of frame t depend only on the modulator frame
@@ -4048,7 +4204,7 @@ template <int NC>
 static hipError_t launch_fir_graph_nc(const IcwFirArgs *f, const IcwK2Args *a, int in_step, size_t lds, hipStream_t st)
 {
     const int TF = 256 * ICW_FIR_R / NC;
-    dim3 grid(f->n_streams, (f->T + TF - 1) / TF);        /* stream-fastest (icw_fir_graph); <= 1 024 tiles */
+    dim3 grid(f->n_streams, (f->T + TF - 1) / TF - f->tile0);  /* stream-fastest (icw_fir_graph); <= 1 024 tiles */
     const void *fn = !a->trig ? (const void *)icw_fir_graph<false, false, NC>
                    : in_step ? (const void *)icw_fir_graph<true, true, NC> : (const void *)icw_fir_graph<true, false, NC>;
     if (fir_lds_attr(fn, lds) != hipSuccess) return hipErrorInvalidValue;
@@ -4056,6 +4212,40 @@ static hipError_t launch_fir_graph_nc(const IcwFirArgs *f, const IcwK2Args *a, i
     else if (in_step) hipLaunchKernelGGL((icw_fir_graph<true, true, NC>), grid, dim3(256), lds, st, *f, *a);
     else hipLaunchKernelGGL((icw_fir_graph<true, false, NC>), grid, dim3(256), lds, st, *f, *a);
     return hipGetLastError();
+}
+
+/* the signature form over tiles [0, ntile) of every stream */
+template <int SIG, int NC, bool B24>
+static hipError_t launch_fir_sig_t(const IcwFirArgs *f, const IcwK2Args *a, int ntile, size_t lds, hipStream_t st)
+{
+    const void *fn = (const void *)icw_fir_sig<SIG, NC, B24>;
+    if (fir_lds_attr(fn, lds) != hipSuccess) return hipErrorInvalidValue;
+    hipLaunchKernelGGL((icw_fir_sig<SIG, NC, B24>), dim3(f->n_streams, ntile), dim3(256), lds, st, *f, *a);
+    return hipGetLastError();
+}
+
+template <int NC, bool B24>
+static hipError_t launch_fir_sig_d(const IcwFirArgs *f, const IcwK2Args *a, int sig, int ntile, size_t lds,
+                                   hipStream_t st)
+{
+    switch (sig) {
+    case ICW_SIG_M:
+    case ICW_SIG_M | ICW_SIG_UNIT: return launch_fir_sig_t<ICW_SIG_M | ICW_SIG_UNIT, NC, B24>(f, a, ntile, lds, st);
+    case ICW_SIG_SM: return launch_fir_sig_t<ICW_SIG_SM, NC, B24>(f, a, ntile, lds, st);
+    case ICW_SIG_SM | ICW_SIG_UNIT: return launch_fir_sig_t<ICW_SIG_SM | ICW_SIG_UNIT, NC, B24>(f, a, ntile, lds, st);
+    case ICW_SIG_PSXM: return launch_fir_sig_t<ICW_SIG_PSXM, NC, B24>(f, a, ntile, lds, st);
+    case ICW_SIG_PSXM | ICW_SIG_UNIT: return launch_fir_sig_t<ICW_SIG_PSXM | ICW_SIG_UNIT, NC, B24>(f, a, ntile, lds, st);
+    default: return hipErrorInvalidValue;
+    }
+}
+
+static bool fir_sig_known(int sig)
+{
+    switch (sig) {
+    case ICW_SIG_M: case ICW_SIG_M | ICW_SIG_UNIT: case ICW_SIG_SM: case ICW_SIG_SM | ICW_SIG_UNIT:
+    case ICW_SIG_PSXM: case ICW_SIG_PSXM | ICW_SIG_UNIT: return true;
+    default: return false;
+    }
 }
 
 extern "C" hipError_t icw_launch_fir_graph(const IcwFirArgs *f, const IcwK2Args *a, int in_step, hipStream_t st)
@@ -4068,7 +4258,32 @@ extern "C" hipError_t icw_launch_fir_graph(const IcwFirArgs *f, const IcwK2Args 
     const size_t lds = icw_fir_graph_lds(f->M, f->nt, f->nch, a->n_regs);
     if (!lds) return hipErrorInvalidValue;
     if (in_step && !(a->trig && a->trig_tab)) return hipErrorInvalidValue;
-    return f->nch > 1 ? launch_fir_graph_nc<2>(f, a, in_step, lds, st) : launch_fir_graph_nc<1>(f, a, in_step, lds, st);
+    const int nc = f->nch > 1 ? 2 : 1, TF = 256 * ICW_FIR_R / nc;
+    IcwFirArgs fl = *f;
+    fl.tile0 = 0;
+    /* the signature form takes the tiles before the one holding the block's last frame when every
+     * lane of them would take icw_chain_frames' render-only branch: a chain program of a known
+     * signature, its rotation factors (if any) from the table, a render here, no pre-render doubles,
+     * no I / Q hand-off, no dither rows.  ICW_FIR_SIG=0: icw_fir_graph for every tile (A/B). */
+    const char *sig_env = getenv("ICW_FIR_SIG");
+    const bool sig_on = !sig_env || atoi(sig_env) != 0;
+    const int sig = f->sig;
+    const bool rot = (sig & ~ICW_SIG_UNIT) != ICW_SIG_M;
+    if (sig_on && ICW_CHAIN4 && fir_sig_known(sig) && (rot ? (a->trig && in_step) : !a->trig) && a->do_render &&
+        !a->iq_out && !a->pre && !a->dith) {
+        const int nsig = (f->T - 1) / TF;
+        if (nsig > 0) {
+            const bool b24 = a->rk.is24 != 0;
+            const size_t ls = icw_fir_graph_lds(f->M, f->nt, f->nch, 0);   /* no DSP register file */
+            const hipError_t e = nc == 2 ? (b24 ? launch_fir_sig_d<2, true>(f, a, sig, nsig, ls, st)
+                                                : launch_fir_sig_d<2, false>(f, a, sig, nsig, ls, st))
+                                         : (b24 ? launch_fir_sig_d<1, true>(f, a, sig, nsig, ls, st)
+                                                : launch_fir_sig_d<1, false>(f, a, sig, nsig, ls, st));
+            if (e != hipSuccess) return e;
+            fl.tile0 = nsig;
+        }
+    }
+    return nc == 2 ? launch_fir_graph_nc<2>(&fl, a, in_step, lds, st) : launch_fir_graph_nc<1>(&fl, a, in_step, lds, st);
 }
 
 template <int N, bool K>
