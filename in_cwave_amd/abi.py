@@ -165,6 +165,7 @@ SIGNATURES = {
     "icw_synchronize": (_i, [_vp]),
     "icw_host_alloc": (_i, [C.c_size_t, C.POINTER(_vp)]),
     "icw_host_free": (_i, [_vp]),
+    "icw_host_pinned": (_i, [_vp, _i]),
     "icw_get_meters": (_i, [_vp, _i, _i, C.POINTER(Meters)]),
     "icw_render_size": (_i, [_vp]),
     "icw_n_frame": (_i, [_vp, _i, C.POINTER(C.c_uint64)]),

@@ -2345,6 +2345,11 @@ int icw_host_free(void *p)
     return (!p || hipHostFree(p) == hipSuccess) ? ICW_OK : ICW_EINVAL;
 }
 
+int icw_host_pinned(const void *p, int device)
+{
+    return p && host_pinned(p, device) ? 1 : 0;
+}
+
 int icw_synchronize(icw_ctx *c)
 {
     if (!c) return ICW_EINVAL;

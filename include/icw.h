@@ -311,6 +311,11 @@ int icw_synchronize(icw_ctx *ctx);
  * kernels (cudaMallocHost-style helper; the reference's buffers are the caller's own).  0 / ICW_ENOMEM. */
 int icw_host_alloc(size_t bytes, void **p);
 int icw_host_free(void *p);
+/* Whether a host buffer takes the block-by-block copies on a context of `device`: 1 when it is
+ * page-locked and was pinned while `device` was current or pinned portable (icw_host_alloc,
+ * hipHostMallocPortable, hipHostRegisterPortable), 0 otherwise (the call then stages it through the
+ * context's own pinned buffers: correct for any host memory, without the overlap). */
+int icw_host_pinned(const void *p, int device);
 /* Meters of stream s (amod_get_clips_peaks, adv_modulator.c:445-465).  reset != 0 clears the clip
  * counters and peaks FIRST, as the reference does, so the call returns 0 clips and
  * ICW_SR_ZERO_SIGNAL_DB peaks; the de-subnorm count is not reset (mod_context_get_desubnorm_counter,

@@ -71,6 +71,32 @@ def test_group_pinned_host_buffers(oracle, icw):
     ctx.close()
 
 
+def test_host_pinned_query():
+    """icw_host_pinned is the check each shard context makes before it pipelines a caller slice
+    (host_pinned): a portable block (icw_host_alloc) counts for the allocating device 0 and, through
+    the allocation-flags branch, for device 1 as well (the query compares indices, so device 1 need
+    not exist); pageable memory counts for neither; memory registered while device 0 was current
+    counts for device 0"""
+    import ctypes as C
+    lib = L.load()
+    pin = L.host_array((4096,))
+    p = pin.ctypes.data
+    assert lib.icw_host_pinned(p, 0) == 1
+    assert lib.icw_host_pinned(p, 1) == 1
+    assert lib.icw_host_pinned(p + 100, 1) == 1        # an interior slice, as a shard gets
+    pageable = np.zeros(1 << 16, dtype=np.uint8)
+    assert lib.icw_host_pinned(pageable.ctypes.data, 0) == 0
+    assert lib.icw_host_pinned(pageable.ctypes.data, 1) == 0
+    assert lib.icw_host_pinned(None, 0) == 0
+    hip = C.CDLL("libamdhip64.so.7")                    # the runtime libicw links (the same handle)
+    buf = np.zeros(1 << 16, dtype=np.uint8)
+    assert hip.hipHostRegister(C.c_void_p(buf.ctypes.data), C.c_size_t(buf.nbytes), C.c_uint(0)) == 0
+    try:
+        assert lib.icw_host_pinned(buf.ctypes.data, 0) == 1
+    finally:
+        assert hip.hipHostUnregister(C.c_void_p(buf.ctypes.data)) == 0
+
+
 def test_transcode_files_devices_byte_identical(tmp_path):
     """the many-file transcoder split over two 'devices' (both device 0) writes the same files as
     one device"""
