@@ -57,11 +57,16 @@ constexpr int kDefBlockFrames = 1 << 14;   /* launch block: shorter pipeline fil
 constexpr int kSets = 3;                    /* most block scratch sets (ICW_SETS); default 2 */
 constexpr double kAutoTaper = 0.85;          /* tail block ratio where the taper is on by default */
 constexpr double kRowTaper = 0.25;           /* tail ratio of the row kernel's long blocks (no serial render) */
-/* FIR converter + serial render: the first blocks grow by this ratio from kFirRenderFirst frames (the
- * render K3r takes ~2.6x the converter + dither generator's time per frame, so each block's
- * converter and dither are done before the render of the block before it ends) */
-constexpr double kFirRenderRamp = 2.5;
-constexpr int kFirRenderFirst = 4096;
+/* FIR converter + serial render: the first blocks grow by this ratio from kFirRenderFirst frames, so
+ * that each block's converter and dither generator (one stream, ~30 us per 1 000 frames of c5fir) are
+ * done before the render of the block before it ends (K3c: ~52 us per 1 000 frames).  Round 4's 2.5
+ * was set for K3r at ~2.6x the converter + generator; with K3c the ratio is ~1.7, and 2.5 left ~1 ms of
+ * gaps per c5fir step (profiles/r06_c5fir_fill.txt).  2 048 / 1.5 measured best of the first-block x
+ * ramp grid, c5fir 9 110 -> 9 482 Msamples/s over three runs (profiles/r06_c5fir_ramp_ab.txt).
+ * Running the generator beside the converter on a stream of its own removed the gaps but lowered
+ * the render's clock more than that (same file). */
+constexpr double kFirRenderRamp = 1.5;
+constexpr int kFirRenderFirst = 2048;
 /* the fused FIR converter on device buffers with nothing after it (no serial render, no host copies
  * to overlap): one launch block per 2^20 frames.  At 65 536 each block paid a rotation-table launch
  * and two ~12 us gaps beside its 0.26 ms kernel, 13 % of a c2fir step */

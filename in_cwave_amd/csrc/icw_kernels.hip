@@ -4355,9 +4355,19 @@ extern "C" hipError_t icw_launch_dither_lane(const IcwK3Args *a, hipStream_t st)
 template <int KIND, int NN, bool MR>
 static void icw_launch_rr(const IcwK3Args *a, int rb, hipStream_t st)
 {
-    /* K3c (a companion wave beside the chain, 128 threads) or K3r (one wave) */
-    if (a->comp) hipLaunchKernelGGL((icw_render_rowc<KIND, NN, MR>), dim3(rb), dim3(128), 0, st, *a);
-    else hipLaunchKernelGGL((icw_render_row<KIND, NN, MR>), dim3(rb), dim3(64), 0, st, *a);
+    /* K3c (a companion wave beside the chain, 128 threads) or K3r (one wave).  ICW_K3C_LDS (A/B): dynamic
+     * LDS bytes K3c reserves on top of its own, so that fewer other workgroups share its CUs */
+    if (a->comp) {
+        const char *e = getenv("ICW_K3C_LDS");
+        size_t pad = e ? (size_t)atol(e) : 0;
+        if (pad > 150 * 1024) pad = 150 * 1024;
+        if (pad > 64 * 1024)
+            (void)hipFuncSetAttribute((const void *)icw_render_rowc<KIND, NN, MR>,
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)pad);
+        hipLaunchKernelGGL((icw_render_rowc<KIND, NN, MR>), dim3(rb), dim3(128), pad, st, *a);
+    } else {
+        hipLaunchKernelGGL((icw_render_row<KIND, NN, MR>), dim3(rb), dim3(64), 0, st, *a);
+    }
 }
 
 template <bool MR>
