@@ -14,7 +14,7 @@ import csv
 import json
 from pathlib import Path
 
-KERNELS = ("icw_fir_hilbert", "icw_fir_graph", "icw_fir_sig", "icw_unpack_frames", "icw_iir_state", "icw_iir_row", "icw_output", "icw_trig_table", "icw_dither_coop",
+KERNELS = ("icw_fir_hilbert", "icw_fir_graph", "icw_fir_sig", "icw_unpack_frames", "icw_iir_state", "icw_iir_row", "icw_output", "icw_trig_table", "icw_dither_coop", "icw_dith_twist", "icw_dith_samples", "icw_dith_fix",
            "icw_render_serial", "icw_render_row")
 
 
