@@ -62,6 +62,8 @@ struct IcwFirArgs {
     int32_t sig;                   /* KF2: the program's chain signature (IcwProg.sig; 0: not a chain), so the
                                       launcher can pick the signature form (icw_fir_sig) */
     int32_t tile0;                 /* KF2: index of the first tile icw_fir_graph's grid covers (set by the launcher) */
+    int32_t lr_same;               /* KF2, mono input: a Master-only chain whose two gains are the same double, so
+                                      both output channels are one computation (icw_fir_sig) */
 };
 
 /* Arguments of the call-end bookkeeping kernel: one thread per stream.  During a call every

@@ -1827,6 +1827,13 @@ int icw_process_streams(icw_ctx *c, int first, int count, const void *in, size_t
         af.xd = c->xd[b % n_sets];
         af.x_pitch = x_pitch;
         af.sig = c->prog.chain ? c->prog.sig : 0;
+        {
+            /* mono input through a Master-only chain (signature count 1, mode MASTER, chain_in `in`:
+             * ICW_SIG_M in icw_kernels.hip) whose gains are bit-identical: L and R are one computation */
+            const IcwOp &m = c->prog.ops[0];
+            af.lr_same = nch == 1 && c->prog.chain && (c->prog.sig & ~(1 << 30)) == 0x41 &&
+                         !memcmp(&m.gain[0], &m.gain[1], sizeof(double)) && m.unit_gain[0] == m.unit_gain[1];
+        }
         return af;
     };
     /* pinned host input: block b's input slice of every stream goes in on the copy stream, and the

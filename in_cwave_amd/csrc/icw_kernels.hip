@@ -2309,26 +2309,61 @@ __global__ __launch_bounds__(256, NC == 2 ? ICW_FIR_SIG_OCC : ICW_FIR_SIG_OCC1) 
         /* mono: the lane's 8 frames two at a time, packed as icw_mono_passes does */
         const int fr0 = ICW_FIR_R * ll;
         const uint32_t tro_lane = (uint32_t)(((size_t)(tt >> 3) + ll) * a.trig_pitch);
+        int dl[ICW_FIR_R], dr[ICW_FIR_R];
+        if (!TRIG && f.lr_same) {
+            /* both channels run the same arithmetic on the same inputs (mono input, a Master whose two
+             * gains are the same double: icw_launch_fir_graph's lr_same), so a pass takes two frames in
+             * its L / R slots and each result serves both channels: half the graph and render */
+#pragma unroll
+            for (int hh = 0; hh < ICW_FIR_R; hh += 4) {
+                IcwLR in2[2];
+#pragma unroll
+                for (int r = 0; r < 2; ++r) {
+                    in2[r].lre = vi[hh + 2 * r];
+                    in2[r].lim = q[hh + 2 * r];
+                    in2[r].rre = vi[hh + 2 * r + 1];
+                    in2[r].rim = q[hh + 2 * r + 1];
+                }
+                int dv[2][2];
+                icw_sig_fast<TRIG, 2, SIG>(a, P, in2, clip_l, clip_r, pk_l, pk_r, dv, tro_lane, 0, pq);
+#pragma unroll
+                for (int r = 0; r < 2; ++r)
+#pragma unroll
+                    for (int c = 0; c < 2; ++c) dl[hh + 2 * r + c] = dr[hh + 2 * r + c] = dv[r][c];
+            }
+            /* the slots held frames: every frame's clips and peak count for both channels */
+            clip_l = clip_r = clip_l + clip_r;
+            pk_l = pk_r = icw_vmax(pk_l, pk_r);
+        } else {
+#pragma unroll
+            for (int hh = 0; hh < ICW_FIR_R; hh += 2) {
+                IcwLR in2[2];
+#pragma unroll
+                for (int r = 0; r < 2; ++r) {
+                    in2[r].lre = in2[r].rre = vi[hh + r];
+                    in2[r].lim = in2[r].rim = q[hh + r];
+                }
+                int dv[2][2];
+                icw_sig_fast<TRIG, 2, SIG>(a, P, in2, clip_l, clip_r, pk_l, pk_r, dv, tro_lane, (size_t)hh * pq, pq);
+#pragma unroll
+                for (int r = 0; r < 2; ++r) {
+                    dl[hh + r] = dv[r][0];
+                    dr[hh + r] = dv[r][1];
+                }
+            }
+        }
         unsigned w[ICW_FIR_R / 2 * 3];
 #pragma unroll
         for (int hh = 0; hh < ICW_FIR_R; hh += 2) {
-            IcwLR in2[2];
-#pragma unroll
-            for (int r = 0; r < 2; ++r) {
-                in2[r].lre = in2[r].rre = vi[hh + r];
-                in2[r].lim = in2[r].rim = q[hh + r];
-            }
-            int dv[2][2];
-            icw_sig_fast<TRIG, 2, SIG>(a, P, in2, clip_l, clip_r, pk_l, pk_r, dv, tro_lane, (size_t)hh * pq, pq);
             if constexpr (B24) {
-                const unsigned l0 = (unsigned)dv[0][0] & 0xffffffu, r0 = (unsigned)dv[0][1] & 0xffffffu;
-                const unsigned l1 = (unsigned)dv[1][0] & 0xffffffu, r1 = (unsigned)dv[1][1] & 0xffffffu;
+                const unsigned l0 = (unsigned)dl[hh] & 0xffffffu, r0 = (unsigned)dr[hh] & 0xffffffu;
+                const unsigned l1 = (unsigned)dl[hh + 1] & 0xffffffu, r1 = (unsigned)dr[hh + 1] & 0xffffffu;
                 w[hh / 2 * 3 + 0] = l0 | (r0 << 24);
                 w[hh / 2 * 3 + 1] = (r0 >> 8) | (l1 << 16);
                 w[hh / 2 * 3 + 2] = (l1 >> 16) | (r1 << 8);
             } else {
-                w[hh] = ((unsigned)dv[0][0] & 0xffffu) | ((unsigned)dv[0][1] << 16);
-                w[hh + 1] = ((unsigned)dv[1][0] & 0xffffu) | ((unsigned)dv[1][1] << 16);
+                w[hh] = ((unsigned)dl[hh] & 0xffffu) | ((unsigned)dr[hh] << 16);
+                w[hh + 1] = ((unsigned)dl[hh + 1] & 0xffffu) | ((unsigned)dr[hh + 1] << 16);
             }
         }
         if constexpr (B24) {

@@ -63,3 +63,36 @@ def test_signature_form_calls(oracle, icw, gname, ch, b24, quantz, monkeypatch):
             st.process(raw[s, t * fsz:(t + b) * fsz], b)
             t += b
         assert m_on[s] == st.meters(), s
+
+
+@pytest.mark.parametrize("gains", [(1.0, 1.0), (0.5, 0.5), (0.5, 0.75), (0.0, 0.0), (-0.0, 0.0)])
+@pytest.mark.parametrize("b24", [False, True])
+def test_mono_master_one_computation(oracle, icw, gains, b24, monkeypatch):
+    """mono input through a Master whose two gains are the same double: icw_fir_sig computes both
+    channels once, two frames per pass in the L / R slots (IcwFirArgs.lr_same); unequal gains, and
+    +0.0 against -0.0, keep the two-channel passes.  Bytes and meters are the oracle's and the
+    ICW_FIR_SIG=0 form's"""
+    nodes = graph.graph_master_only()
+    nodes[0].gain[0], nodes[0].gain[1] = gains
+    cfg = graph.default_config(48000, fmt=abi.FMT_F32, channels=1, need24bits=b24)
+    lens = [5 * 2048 + 7, 2048, 3 * 2048 + 1]
+    n = sum(lens)
+    rng = np.random.default_rng(int(gains[0] * 1000 + gains[1] * 10 + b24))
+    x = (rng.standard_normal((2, n)) * 1.7).astype(np.float32)     # past full scale: clips counted
+    x[:, 100:140] = -0.0
+    x[0, 3000] = np.nan
+    raw = x.view(np.uint8)
+    on, m_on = run(icw, cfg, nodes, raw, lens, monkeypatch, "1")
+    off, m_off = run(icw, cfg, nodes, raw, lens, monkeypatch, "0")
+    assert np.array_equal(on, off)
+    assert m_on == m_off
+    ref, _ = oracle.process_streams(cfg, nodes, raw, n, want_pre=False, fir=(ORDER, BETA))
+    assert np.array_equal(on, ref)
+    for s in range(2):
+        st = oracle.Stream(cfg, nodes)
+        st.set_fir(ORDER, BETA)
+        t = 0
+        for b in lens:
+            st.process(raw[s, t * 4:(t + b) * 4], b)
+            t += b
+        assert m_on[s] == st.meters(), s
